@@ -1,0 +1,195 @@
+"""Synthetic vocabularies and corpora for the five BASELINE.json configurations.
+
+No Llama-2 ``tokenizer.model`` exists offline (SURVEY.md §0 finding 6), so every
+report that uses ``llama_shaped_vocab`` says "synthetic Llama-shaped 32k vocab".
+
+Vocabulary recipe, shaped like ``LlamaTokenizer.get_vocab()``
+(the dict that ``dp_tokenize_llama`` turns into ``t2i``/``vocab`` at
+reference ``packages/tokenizer_utils.py:53-57``):
+
+* ids 0..2 ``<unk>``, ``<s>``, ``</s>``; ids 3..258 the byte tokens ``<0x00>``..``<0xFF>``;
+* ``'▁'``, the 94 printable ASCII characters 0x21..0x7E, and ``'▁'+c`` for each;
+* (our extension, for the Arabic-shaped config 5) the code points U+0621..U+064A,
+  ``'▁'+c`` for each, and random 2..5-letter Arabic entries;
+* seeded random fill up to ``size``: length drawn from {2,2,2,3,3,4,5,6,7,8}; each
+  character from ``etaoinshrdlucmfwypvbgkjqxz`` with p=0.8, otherwise printable
+  ASCII; a ``'▁'`` prefix with p=0.4; duplicates dropped.
+
+This guarantees every raw-mode ASCII atom is in the vocab,
+so random printable strings never fail except for a leading space (atom ``'▁ '``).
+
+Corpora are generated from a counter-based PRNG (numpy Philox) keyed by
+``(seed, global string index)``, so a shard is identical at any GPU count.
+"""
+from __future__ import annotations
+
+import random
+from typing import Dict, List, Tuple
+
+import numpy as np
+
+SPACE_MARK = "▁"  # '▁'
+PRINTABLE = [chr(c) for c in range(0x21, 0x7F)]
+LETTERS = "etaoinshrdlucmfwypvbgkjqxz"
+ARABIC = [chr(c) for c in range(0x0621, 0x064B)]
+
+
+def _fill(vocab: Dict[str, int], size: int, rng: random.Random, lengths, p_letter, p_mark):
+    while len(vocab) < size:
+        n = rng.choice(lengths)
+        chars = []
+        for _ in range(n):
+            if rng.random() < p_letter:
+                chars.append(rng.choice(LETTERS))
+            else:
+                chars.append(rng.choice(PRINTABLE))
+        tok = "".join(chars)
+        if rng.random() < p_mark:
+            tok = SPACE_MARK + tok
+        if tok not in vocab:
+            vocab[tok] = len(vocab)
+
+
+def llama_shaped_vocab(size: int = 32000, seed: int = 0, arabic: bool = True) -> Dict[str, int]:
+    """Synthetic Llama-shaped vocabulary: token string -> id (ids contiguous)."""
+    rng = random.Random(seed)
+    vocab: Dict[str, int] = {}
+    for t in ("<unk>", "<s>", "</s>"):
+        vocab[t] = len(vocab)
+    for b in range(256):
+        vocab["<0x%02X>" % b] = len(vocab)
+    vocab.setdefault(SPACE_MARK, len(vocab))
+    for c in PRINTABLE:
+        vocab.setdefault(c, len(vocab))
+    for c in PRINTABLE:
+        vocab.setdefault(SPACE_MARK + c, len(vocab))
+    if arabic:
+        for c in ARABIC:
+            vocab.setdefault(c, len(vocab))
+            vocab.setdefault(SPACE_MARK + c, len(vocab))
+        n_ar = 0
+        while n_ar < 1500:
+            tok = "".join(rng.choice(ARABIC) for _ in range(rng.choice((2, 2, 3, 3, 4, 5))))
+            if rng.random() < 0.4:
+                tok = SPACE_MARK + tok
+            if tok not in vocab:
+                vocab[tok] = len(vocab)
+                n_ar += 1
+    _fill(vocab, size, rng, (2, 2, 2, 3, 3, 4, 5, 6, 7, 8), 0.8, 0.4)
+    return vocab
+
+
+def toy_vocab(size: int = 1000, seed: int = 0) -> Dict[str, int]:
+    """1000-entry toy vocabulary for config 1 (CPU plumbing case)."""
+    rng = random.Random(seed + 1000003)
+    vocab: Dict[str, int] = {}
+    for t in ("<unk>", "<s>", "</s>", "<0x0A>"):
+        vocab[t] = len(vocab)
+    vocab[SPACE_MARK] = len(vocab)
+    for c in PRINTABLE:
+        vocab.setdefault(c, len(vocab))
+    for c in PRINTABLE:
+        vocab.setdefault(SPACE_MARK + c, len(vocab))
+    _fill(vocab, size, rng, (2, 2, 2, 3, 3, 4), 0.85, 0.4)
+    return vocab
+
+
+# --------------------------------------------------------------------------- corpora
+
+def _philox_bytes(seed: int, first_block: int, n_u64: int) -> np.ndarray:
+    bg = np.random.Philox(key=np.uint64(seed), counter=np.array([first_block, 0, 0, 0], dtype=np.uint64))
+    return bg.random_raw(n_u64).view(np.uint8)
+
+
+def random_ascii_corpus(n: int, length: int = 256, seed: int = 1, start: int = 0,
+                        chunk: int = 1 << 16) -> Tuple[np.ndarray, np.ndarray]:
+    """Config 1/2/3: ``n`` random printable-ASCII strings of ``length`` bytes.
+
+    Byte 0 is drawn over 0x21..0x7E, bytes 1.. over 0x20..0x7E (space ~1/85).
+    String ``g`` (global index ``start + i``) uses Philox blocks ``[g*B, (g+1)*B)``
+    with ``B = ceil(length/32)`` (a block is 4 x u64 = 32 bytes).
+    Returns ``(text u8[n*length], offsets u64[n+1])``.
+    """
+    blocks = (length + 31) // 32
+    out = np.empty(n * length, dtype=np.uint8)
+    for c0 in range(0, n, chunk):
+        m = min(chunk, n - c0)
+        raw = _philox_bytes(seed, (start + c0) * blocks, m * blocks * 4).reshape(m, blocks * 32)[:, :length]
+        raw = raw.astype(np.uint16)
+        s = (0x20 + ((raw * 95) >> 8)).astype(np.uint8)
+        s[:, 0] = (0x21 + ((raw[:, 0] * 94) >> 8)).astype(np.uint8)
+        out[c0 * length:(c0 + m) * length] = s.reshape(-1)
+    offs = np.arange(n + 1, dtype=np.uint64) * np.uint64(length)
+    return out, offs
+
+
+_EN_FREQ = np.array([8.2, 1.5, 2.8, 4.3, 12.7, 2.2, 2.0, 6.1, 7.0, 0.15, 0.77, 4.0, 2.4, 6.7,
+                     7.5, 1.9, 0.095, 6.0, 6.3, 9.1, 2.8, 0.98, 2.4, 0.15, 2.0, 0.074])
+_EN_FREQ = _EN_FREQ / _EN_FREQ.sum()
+
+
+def s2orc_like_corpus(n: int, seed: int = 4, start: int = 0) -> Tuple[np.ndarray, np.ndarray]:
+    """Config 4: abstract-shaped strings, lengths ~ N(1200, 400) clipped to [64, 4096].
+
+    Pseudo-words (geometric lengths, mean ~6 letters, English letter frequencies,
+    ~8% capitalised), separated by spaces; ~2% punctuation/digits; occasional
+    '\\n'. Each string starts at a word. Keyed by (seed, global index).
+    """
+    parts: List[bytes] = []
+    for g in range(start, start + n):
+        rng = np.random.Generator(np.random.Philox(key=np.uint64(seed), counter=np.array([g, 0, 0, 0], dtype=np.uint64)))
+        L = int(np.clip(rng.normal(1200, 400), 64, 4096))
+        buf = bytearray()
+        nw = L // 4 + 8
+        wl = rng.geometric(1 / 6, size=nw)
+        letters = rng.choice(26, size=int(wl.sum()), p=_EN_FREQ)
+        extras = rng.random(size=(nw, 3))
+        k = 0
+        for w in range(nw):
+            word = bytes((97 + letters[k:k + wl[w]]).astype(np.uint8))
+            k += wl[w]
+            if extras[w, 0] < 0.08:
+                word = word[:1].upper() + word[1:]
+            if extras[w, 1] < 0.02:
+                word += b"0123456789.,;:()%-"[int(extras[w, 1] * 900) % 18:][:1]
+            if buf:
+                buf += b"\n" if extras[w, 2] < 0.01 else b" "
+            buf += word
+            if len(buf) >= L:
+                break
+        parts.append(bytes(buf[:L]))
+    return _pack(parts)
+
+
+def arabic_corpus(n: int, length: int = 256, seed: int = 5, start: int = 0) -> Tuple[np.ndarray, np.ndarray]:
+    """Config 5: Arabic-shaped UTF-8 (U+0621..U+064A, 2 bytes each), a space ~every 5 letters."""
+    parts: List[bytes] = []
+    for g in range(start, start + n):
+        rng = np.random.Generator(np.random.Philox(key=np.uint64(seed), counter=np.array([g, 0, 0, 0], dtype=np.uint64)))
+        cps = rng.integers(0x0621, 0x064B, size=length)
+        sp = rng.random(size=length) < 0.2
+        chars: List[str] = []
+        nb = 0
+        for i in range(length):
+            c = " " if (sp[i] and i > 0 and chars and chars[-1] != " ") else chr(int(cps[i]))
+            b = 1 if c == " " else 2
+            if nb + b > length:
+                break
+            chars.append(c)
+            nb += b
+        parts.append("".join(chars).encode("utf-8"))
+    return _pack(parts)
+
+
+def _pack(parts: List[bytes]) -> Tuple[np.ndarray, np.ndarray]:
+    offs = np.zeros(len(parts) + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([len(p) for p in parts], dtype=np.uint64)
+    text = np.frombuffer(b"".join(parts), dtype=np.uint8).copy()
+    return text, offs
+
+
+def unpack(text: np.ndarray, offs: np.ndarray) -> List[str]:
+    """CSR bytes -> list of Python strings (UTF-8)."""
+    raw = text.tobytes()
+    o = [int(x) for x in offs]
+    return [raw[o[i]:o[i + 1]].decode("utf-8", "surrogatepass") for i in range(len(o) - 1)]
