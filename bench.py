@@ -1,0 +1,238 @@
+#!/usr/bin/env python3
+"""bench.py -- BASELINE.json's headline metric on MI355X.
+
+metric: input bytes/sec (whole job, all GPUs) + exact-match rate vs the CPU DP,
+256-byte random printable-ASCII strings, synthetic Llama-shaped 32k vocab (no
+Llama-2 tokenizer file is available offline: SURVEY.md §0 finding 6).
+
+A step = one pass of the hot path (dpt_encode: tokenize kernel(s) + offset scan +
+CSR compaction, then the token-count histogram and, for N>1, ONE RCCL all-reduce
+of it) over the rank's resident shard of 1M strings (BASELINE.json configs[1];
+configs[2] at N=8).  Weak scaling: each rank owns 1M strings of a global corpus
+keyed by (seed, global index).
+
+Launch: python bench.py --gpus 1 --steps K --warmup W
+        python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import multiprocessing as mp
+import os
+import signal
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "dp-tokenization_amd"))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md chip table (spec)
+N_BINS = 258                # tokens-per-string histogram (<= 256 ids for 256-byte strings, + overflow)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--strings", type=int, default=1_000_000, help="strings per GPU")
+    ap.add_argument("--length", type=int, default=256)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--exact-sample", type=int, default=65536, help="strings checked against the C oracle (rank 0)")
+    ap.add_argument("--cpu-sample", type=int, default=2048, help="strings for the reference-port CPU baseline")
+    ap.add_argument("--cpu-budget", type=float, default=25.0, help="seconds of CPU-baseline wall time")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+# ------------------------------------------------------------------ CPU baseline (port of the reference)
+_PORT = {}
+
+
+def _port_init():
+    from dptok import synth
+    from oracle import ref_port
+    _PORT["t2i"] = synth.llama_shaped_vocab()
+    _PORT["f"] = ref_port.dp_tokenize_raw
+
+    def _alarm(signum, frame):
+        raise TimeoutError()
+    signal.signal(signal.SIGALRM, _alarm)
+
+
+def _port_one(text):
+    signal.alarm(10)
+    try:
+        _PORT["f"](text, _PORT["t2i"])
+        ok = True
+    except TimeoutError:
+        ok = False
+    finally:
+        signal.alarm(0)
+    return len(text.encode()), ok
+
+
+def cpu_baseline(texts, budget, cores):
+    """The reference's enumerate-then-select DP (oracle/ref_port.py) on `cores` processes."""
+    done_bytes, n_done, n_to = 0, 0, 0
+    ctx = mp.get_context("fork")
+    with ctx.Pool(cores, initializer=_port_init) as pool:
+        t0 = time.perf_counter()
+        it = pool.imap_unordered(_port_one, texts, chunksize=4)
+        for nb, ok in it:
+            if ok:
+                done_bytes += nb
+                n_done += 1
+            else:
+                n_to += 1
+            if time.perf_counter() - t0 > budget:
+                break
+        dt = time.perf_counter() - t0
+        pool.terminate()
+    return done_bytes / dt, n_done, n_to, dt
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from dptok import Encoder, Vocab, synth
+    t2i = synth.llama_shaped_vocab()
+    M, Lb = args.strings, args.length
+    text, offs = synth.random_ascii_corpus(M, Lb, seed=args.seed, start=rank * M)
+    cores = max(1, min(16, os.cpu_count() or 1))
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # before any GPU call: the pool forks plain CPU workers
+        texts = synth.unpack(text[: args.cpu_sample * Lb], offs[: args.cpu_sample + 1])
+        v, nd, nto, cdt = cpu_baseline(texts, args.cpu_budget, cores)
+        cpu = {"value": v, "unit": "bytes/s", "cores": cores, "kind": "port",
+               "sample": f"{nd} of the first {args.cpu_sample} cfg2 strings in {cdt:.1f}s "
+                         f"(enumerate-then-select, oracle/ref_port.py; {nto} hit the 10s per-string limit)"}
+
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    vocab = Vocab(t2i, device=local)
+    enc = Encoder(vocab)
+    n_bytes = len(text)
+    d_text = torch.from_numpy(text).to(dev)
+    d_off = torch.from_numpy(offs.view(np.int64)).to(dev)
+    d_ids = torch.empty(n_bytes, dtype=torch.int32, device=dev)
+    d_idoff = torch.empty(M + 1, dtype=torch.int64, device=dev)
+    d_status = torch.empty(M, dtype=torch.int32, device=dev)
+    d_hist = torch.zeros(N_BINS + 8, dtype=torch.int64, device=dev)
+    enc.reserve(n_bytes, M)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        enc.encode_device(d_text.data_ptr(), n_bytes, d_off.data_ptr(), M, d_ids.data_ptr(), n_bytes,
+                          d_idoff.data_ptr(), d_status.data_ptr(), stream=stream)
+        d_hist.zero_()
+        enc.histogram_device(d_idoff.data_ptr(), d_status.data_ptr(), M, d_hist.data_ptr(), N_BINS, stream=stream)
+        if world > 1:
+            dist.all_reduce(d_hist)       # the single RCCL collective
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    enc.profile(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    ms_stage, launches = enc.profile_read()
+    enc.profile(False)
+
+    hist = d_hist.cpu().numpy()
+    n_tok_rank = int(d_idoff[-1].item())
+    n_tok_all = int(hist[N_BINS])          # after the all-reduce: all ranks' ids
+    ok_strings = int(hist[N_BINS + 2])
+
+    # roofline of the dominant kernel (tokenize): algorithmic bytes per launch
+    k_ms = ms_stage[0] / max(launches, 1)
+    alg_bytes = n_bytes + 8 * (M + 1) + 4 * n_tok_rank + 8 * M + 4 * M
+    achieved = alg_bytes / (k_ms * 1e-3) / 1e9
+
+    # exact match vs the CPU DP (C oracle) and the CPU baseline -- rank 0 only
+    exact = None
+    if rank == 0:
+        from oracle import oracle
+        S = min(args.exact_sample, M)
+        ids_h = d_ids.cpu().numpy()
+        off_h = d_idoff.cpu().numpy().view(np.uint64)
+        st_h = d_status.cpu().numpy()
+        ov = oracle.OracleVocab(t2i)
+        sub_off = offs[: S + 1]
+        rids, roff, rst, _ = ov.encode_csr(text, sub_off, nthreads=cores)
+        same = 0
+        for i in range(S):
+            a = ids_h[int(off_h[i]):int(off_h[i + 1])]
+            b = rids[int(roff[i]):int(roff[i + 1])]
+            same += int(st_h[i] == rst[i] and np.array_equal(a, b))
+        exact = {"rate": same / S, "sample": S, "checker": "oracle/dp_oracle.c"}
+        if cpu is not None:
+            t0c = time.perf_counter()
+            ov.encode_csr(text, offs[: 65537], nthreads=cores)
+            cpu["c_restatement_bytes_per_s"] = 65536 * Lb / (time.perf_counter() - t0c)
+
+    if rank == 0:
+        value = world * n_bytes * args.steps / dt
+        line = {
+            "metric": "input bytes/sec/GPU + exact-match rate vs CPU DP, 256-byte strings",
+            "value": value,
+            "unit": "bytes/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic random printable ASCII (Philox keyed by seed+global index); synthetic Llama-shaped 32k vocab",
+            "config": {"workload": "cfg2: 1M x 256-byte random ASCII strings per GPU, raw pre-tokenization",
+                       "strings_per_gpu": M, "bytes_per_string": Lb, "vocab": "synthetic llama-shaped 32000",
+                       "parallelism": f"dp{world} (corpus shards, 1 RCCL all-reduce of the histogram per step)"},
+            "per_gpu_bytes_per_s": value / world,
+            "tokens_per_byte": n_tok_all / (world * n_bytes),
+            "ok_strings": ok_strings,
+            "exact_match": exact,
+            "stage_ms_per_step": {"tokenize": ms_stage[0] / max(launches, 1), "scan": ms_stage[1] / max(launches, 1),
+                                  "compact": ms_stage[2] / max(launches, 1)},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "tokenize_kernel<256,4>", "alg_bytes_per_launch": alg_bytes},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,369 @@
+// dpt_api.cpp -- the C-ABI declared in include/dpt.h.
+//
+// Owns: the device copy of the vocabulary (dpt_vocab), per-stream workspaces
+// (dpt_ctx), argument checking, the host-buffer convenience path and the
+// event-based kernel timing used by bench.py.  No C++ exception crosses the ABI.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/dpt.h"
+#include "dpt_internal.h"
+
+struct dpt_vocab {
+    int device = 0;
+    int2 *d_slots = nullptr;
+    int32_t *d_ids = nullptr;
+    int32_t root_base = 0;
+    dpt_vocab_stats stats{};
+};
+
+struct dpt_ctx {
+    int device = 0;
+    // workspace
+    int32_t *staging = nullptr;
+    uint64_t cap_bytes = 0;
+    uint64_t *counts = nullptr;
+    uint32_t *retry_list = nullptr;
+    uint64_t cap_str = 0;
+    uint32_t *retry_count = nullptr;
+    void *scan_temp = nullptr;
+    size_t scan_bytes = 0;
+    unsigned max_blocks = 0;
+    // host-path device buffers
+    uint8_t *h_text = nullptr;
+    uint64_t h_cap_bytes = 0;
+    uint8_t *h_cut = nullptr;
+    int32_t *h_ids = nullptr;
+    uint64_t *h_off = nullptr, *h_idoff = nullptr;
+    int32_t *h_status = nullptr, *h_capped = nullptr;
+    uint64_t h_cap_str = 0;
+    // profiling
+    bool profile = false;
+    std::vector<hipEvent_t> events;   // groups of 4 per call
+    uint64_t launches = 0;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char *what) {
+    return fail(DPT_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) hipSetDevice(prev);
+    }
+};
+
+template <typename T>
+hipError_t grow(T **p, uint64_t *cap, uint64_t need) {
+    if (need <= *cap && *p) return hipSuccess;
+    uint64_t n = need < 1024 ? 1024 : need + need / 4;
+    if (*p) hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    hipError_t e = hipMalloc((void **)p, n * sizeof(T));
+    if (e == hipSuccess) *cap = n;
+    return e;
+}
+
+int ensure_workspace(dpt_ctx *c, uint64_t n_bytes, uint64_t n_str) {
+    hipError_t e;
+    if (n_bytes > c->cap_bytes || !c->staging) {
+        e = grow(&c->staging, &c->cap_bytes, n_bytes);
+        if (e != hipSuccess) return hip_fail(e, "hipMalloc(staging)");
+    }
+    if (n_str > c->cap_str || !c->counts) {
+        uint64_t cap = c->cap_str, cap2 = c->cap_str;
+        e = grow(&c->counts, &cap, n_str);
+        if (e != hipSuccess) return hip_fail(e, "hipMalloc(counts)");
+        e = grow(&c->retry_list, &cap2, n_str);
+        if (e != hipSuccess) return hip_fail(e, "hipMalloc(retry_list)");
+        c->cap_str = cap < cap2 ? cap : cap2;
+        size_t tb = dpt::scan_temp_bytes(c->cap_str);
+        if (tb > c->scan_bytes) {
+            if (c->scan_temp) hipFree(c->scan_temp);
+            c->scan_temp = nullptr;
+            e = hipMalloc(&c->scan_temp, tb);
+            if (e != hipSuccess) return hip_fail(e, "hipMalloc(scan)");
+            c->scan_bytes = tb;
+        }
+    }
+    if (!c->retry_count) {
+        e = hipMalloc((void **)&c->retry_count, 16);
+        if (e != hipSuccess) return hip_fail(e, "hipMalloc(retry_count)");
+    }
+    return DPT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *dpt_last_error(void) { return g_err.c_str(); }
+
+int dpt_abi_version(void) { return DPT_ABI_VERSION; }
+
+int dpt_vocab_create(const uint8_t *utf8_blob, const uint64_t *tok_off, const int32_t *ids, uint32_t n_tok,
+                     int device, dpt_vocab **out) {
+    if (!out || !tok_off || (!utf8_blob && n_tok && tok_off[n_tok] != tok_off[0])) return fail(DPT_E_ARG, "null argument");
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(DPT_E_NODEV, "no HIP device");
+    if (device < 0 || device >= ndev) return fail(DPT_E_ARG, "bad device index");
+    for (uint32_t t = 0; t < n_tok; t++)
+        if (tok_off[t + 1] < tok_off[t]) return fail(DPT_E_ARG, "tok_off not monotone");
+    dpt::DoubleArray da;
+    const char *err = dpt::build_double_array(utf8_blob, tok_off, ids, n_tok, &da);
+    if (err) return fail(DPT_E_VOCAB, err);
+    if (da.max_cp > 64) {
+        dpt::free_double_array(&da);
+        return fail(DPT_E_VOCAB, "vocabulary has a token longer than 64 code points (engine span limit)");
+    }
+    DeviceGuard g(device);
+    hipError_t e = dpt::kernel_init();
+    if (e != hipSuccess) {
+        dpt::free_double_array(&da);
+        return hip_fail(e, "kernel_init");
+    }
+    dpt_vocab *v = new (std::nothrow) dpt_vocab();
+    if (!v) {
+        dpt::free_double_array(&da);
+        return fail(DPT_E_ARG, "out of host memory");
+    }
+    v->device = device;
+    std::vector<int2> slots(da.n_slots);
+    for (uint32_t t = 0; t < da.n_slots; t++) slots[t] = make_int2(da.base[t], da.check[t]);
+    e = hipMalloc((void **)&v->d_slots, sizeof(int2) * da.n_slots);
+    if (e == hipSuccess) e = hipMalloc((void **)&v->d_ids, sizeof(int32_t) * da.n_slots);
+    if (e == hipSuccess) e = hipMemcpy(v->d_slots, slots.data(), sizeof(int2) * da.n_slots, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(v->d_ids, da.id, sizeof(int32_t) * da.n_slots, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        dpt::free_double_array(&da);
+        if (v->d_slots) hipFree(v->d_slots);
+        if (v->d_ids) hipFree(v->d_ids);
+        delete v;
+        return hip_fail(e, "vocab upload");
+    }
+    v->root_base = da.root_base;
+    v->stats.n_tokens = da.n_tokens;
+    v->stats.n_nodes = da.n_nodes;
+    v->stats.n_slots = da.n_slots;
+    v->stats.max_bytes = da.max_bytes;
+    v->stats.max_cp = da.max_cp;
+    v->stats.device_bytes = (uint64_t)da.n_slots * (sizeof(int2) + sizeof(int32_t));
+    dpt::free_double_array(&da);
+    *out = v;
+    return DPT_OK;
+}
+
+int dpt_vocab_destroy(dpt_vocab *v) {
+    if (!v) return DPT_OK;
+    DeviceGuard g(v->device);
+    hipFree(v->d_slots);
+    hipFree(v->d_ids);
+    delete v;
+    return DPT_OK;
+}
+
+int dpt_vocab_stats_get(const dpt_vocab *v, dpt_vocab_stats *out) {
+    if (!v || !out) return fail(DPT_E_ARG, "null argument");
+    *out = v->stats;
+    return DPT_OK;
+}
+
+int dpt_ctx_create(int device, dpt_ctx **out) {
+    if (!out) return fail(DPT_E_ARG, "null argument");
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(DPT_E_NODEV, "no HIP device");
+    if (device < 0 || device >= ndev) return fail(DPT_E_ARG, "bad device index");
+    dpt_ctx *c = new (std::nothrow) dpt_ctx();
+    if (!c) return fail(DPT_E_ARG, "out of host memory");
+    c->device = device;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->max_blocks = (unsigned)prop.multiProcessorCount * 64u;
+    if (c->max_blocks == 0) c->max_blocks = 256u * 64u;
+    *out = c;
+    return DPT_OK;
+}
+
+int dpt_ctx_destroy(dpt_ctx *c) {
+    if (!c) return DPT_OK;
+    DeviceGuard g(c->device);
+    void *ps[] = {c->staging, c->counts, c->retry_list, c->retry_count, c->scan_temp, c->h_text, c->h_cut,
+                  c->h_ids, c->h_off, c->h_idoff, c->h_status, c->h_capped};
+    for (void *p : ps)
+        if (p) hipFree(p);
+    for (hipEvent_t e : c->events) hipEventDestroy(e);
+    delete c;
+    return DPT_OK;
+}
+
+int dpt_ctx_reserve(dpt_ctx *c, uint64_t n_bytes, uint64_t n_str) {
+    if (!c) return fail(DPT_E_ARG, "null ctx");
+    DeviceGuard g(c->device);
+    return ensure_workspace(c, n_bytes, n_str);
+}
+
+int dpt_encode(dpt_ctx *c, const dpt_vocab *v, int mode, const uint8_t *text, uint64_t n_bytes,
+               const uint64_t *str_off, const uint8_t *cut_mask, uint64_t n_str, int32_t *ids, uint64_t ids_cap,
+               uint64_t *id_off, int32_t *status, int32_t *capped_len, void *hip_stream) {
+    if (!c || !v) return fail(DPT_E_ARG, "null ctx or vocab");
+    if (mode != DPT_MODE_RAW && mode != DPT_MODE_PRESPLIT) return fail(DPT_E_ARG, "bad mode");
+    if (!str_off || !id_off || (n_str && !status)) return fail(DPT_E_ARG, "null output/offsets");
+    if (n_bytes && (!text || !ids)) return fail(DPT_E_ARG, "null text/ids");
+    if (mode == DPT_MODE_PRESPLIT && n_bytes && !cut_mask) return fail(DPT_E_ARG, "PRESPLIT needs cut_mask");
+    if (ids_cap < n_bytes) return fail(DPT_E_CAP, "ids_cap must be >= n_bytes");
+    if (n_str > 0x7FFFFFFFull) return fail(DPT_E_ARG, "too many strings for one call (max 2^31-1)");
+    if (c->device != v->device) return fail(DPT_E_ARG, "ctx and vocab on different devices");
+    DeviceGuard g(c->device);
+    int rc = ensure_workspace(c, n_bytes, n_str);
+    if (rc) return rc;
+    hipStream_t st = (hipStream_t)hip_stream;
+    dpt::EncodeLaunch p;
+    p.mode = mode;
+    p.text = text;
+    p.str_off = str_off;
+    p.cut_mask = cut_mask;
+    p.n_str = n_str;
+    p.ids = ids;
+    p.id_off = id_off;
+    p.status = status;
+    p.capped = capped_len;
+    p.staging = c->staging;
+    p.counts = c->counts;
+    p.retry_list = c->retry_list;
+    p.retry_count = c->retry_count;
+    p.scan_temp = c->scan_temp;
+    p.scan_temp_bytes = c->scan_bytes;
+    p.max_blocks = c->max_blocks;
+    p.slots = v->d_slots;
+    p.slot_ids = v->d_ids;
+    p.root_base = v->root_base;
+    hipEvent_t ev[6];
+    hipEvent_t *evp = nullptr;
+    if (c->profile) {
+        for (int k = 0; k < 4; k++) {
+            hipError_t e = hipEventCreate(&ev[k]);
+            if (e != hipSuccess) return hip_fail(e, "hipEventCreate");
+            c->events.push_back(ev[k]);
+        }
+        evp = ev;
+        c->launches++;
+    }
+    hipError_t e = dpt::launch_encode(p, st, evp);
+    if (e != hipSuccess) return hip_fail(e, "encode launch");
+    return DPT_OK;
+}
+
+int dpt_encode_host(dpt_ctx *c, const dpt_vocab *v, int mode, const uint8_t *text, uint64_t n_bytes,
+                    const uint64_t *str_off, const uint8_t *cut_mask, uint64_t n_str, int32_t *ids, uint64_t ids_cap,
+                    uint64_t *id_off, int32_t *status, int32_t *capped_len) {
+    if (!c || !v) return fail(DPT_E_ARG, "null ctx or vocab");
+    if (!str_off || !id_off || (n_str && !status)) return fail(DPT_E_ARG, "null output/offsets");
+    if (n_bytes && (!text || !ids)) return fail(DPT_E_ARG, "null text/ids");
+    if (ids_cap < n_bytes) return fail(DPT_E_CAP, "ids_cap must be >= n_bytes");
+    if (str_off[n_str] - str_off[0] != n_bytes) return fail(DPT_E_ARG, "n_bytes != str_off[n_str]-str_off[0]");
+    DeviceGuard g(c->device);
+    hipError_t e;
+    uint64_t cb = c->h_cap_bytes, cs = c->h_cap_str;
+    if (n_bytes + 1 > c->h_cap_bytes || !c->h_text) {
+        uint64_t c1 = cb, c2 = cb, c3 = cb;
+        if ((e = grow(&c->h_text, &c1, n_bytes + 1)) != hipSuccess) return hip_fail(e, "hipMalloc");
+        if ((e = grow(&c->h_cut, &c2, n_bytes + 1)) != hipSuccess) return hip_fail(e, "hipMalloc");
+        if ((e = grow(&c->h_ids, &c3, n_bytes + 1)) != hipSuccess) return hip_fail(e, "hipMalloc");
+        c->h_cap_bytes = c1 < c2 ? (c1 < c3 ? c1 : c3) : (c2 < c3 ? c2 : c3);
+    }
+    if (n_str + 2 > c->h_cap_str || !c->h_off) {
+        uint64_t c1 = cs, c2 = cs, c3 = cs, c4 = cs;
+        if ((e = grow(&c->h_off, &c1, n_str + 2)) != hipSuccess) return hip_fail(e, "hipMalloc");
+        if ((e = grow(&c->h_idoff, &c2, n_str + 2)) != hipSuccess) return hip_fail(e, "hipMalloc");
+        if ((e = grow(&c->h_status, &c3, n_str + 2)) != hipSuccess) return hip_fail(e, "hipMalloc");
+        if ((e = grow(&c->h_capped, &c4, n_str + 2)) != hipSuccess) return hip_fail(e, "hipMalloc");
+        uint64_t m = c1 < c2 ? c1 : c2;
+        m = m < c3 ? m : c3;
+        c->h_cap_str = m < c4 ? m : c4;
+    }
+    hipStream_t st = 0;
+    if (n_bytes && (e = hipMemcpyAsync(c->h_text, text, n_bytes, hipMemcpyHostToDevice, st)) != hipSuccess)
+        return hip_fail(e, "H2D text");
+    if (mode == DPT_MODE_PRESPLIT && n_bytes &&
+        (e = hipMemcpyAsync(c->h_cut, cut_mask, n_bytes, hipMemcpyHostToDevice, st)) != hipSuccess)
+        return hip_fail(e, "H2D cut");
+    // offsets rebased to 0 so that the device view is self-contained
+    std::vector<uint64_t> off(n_str + 1);
+    for (uint64_t i = 0; i <= n_str; i++) off[i] = str_off[i] - str_off[0];
+    if ((e = hipMemcpyAsync(c->h_off, off.data(), (n_str + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st)) != hipSuccess)
+        return hip_fail(e, "H2D offsets");
+    int rc = dpt_encode(c, v, mode, c->h_text, n_bytes, c->h_off, c->h_cut, n_str, c->h_ids, c->h_cap_bytes, c->h_idoff,
+                        c->h_status, c->h_capped, st);
+    if (rc) return rc;
+    if ((e = hipMemcpyAsync(id_off, c->h_idoff, (n_str + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, st)) != hipSuccess)
+        return hip_fail(e, "D2H id_off");
+    if (n_str && (e = hipMemcpyAsync(status, c->h_status, n_str * sizeof(int32_t), hipMemcpyDeviceToHost, st)) != hipSuccess)
+        return hip_fail(e, "D2H status");
+    if (capped_len && n_str &&
+        (e = hipMemcpyAsync(capped_len, c->h_capped, n_str * sizeof(int32_t), hipMemcpyDeviceToHost, st)) != hipSuccess)
+        return hip_fail(e, "D2H capped");
+    if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(e, "sync");
+    const uint64_t total = id_off[n_str];
+    if (total > ids_cap) return fail(DPT_E_CAP, "ids overflow");
+    if (total && (e = hipMemcpy(ids, c->h_ids, total * sizeof(int32_t), hipMemcpyDeviceToHost)) != hipSuccess)
+        return hip_fail(e, "D2H ids");
+    return DPT_OK;
+}
+
+int dpt_token_histogram(const uint64_t *id_off, const int32_t *status, uint64_t n_str, int64_t *hist, uint32_t n_bins,
+                        void *hip_stream) {
+    if (!id_off || !hist || (n_str && !status) || n_bins < 2) return fail(DPT_E_ARG, "bad histogram arguments");
+    hipError_t e = dpt::launch_histogram(id_off, status, n_str, hist, n_bins, (hipStream_t)hip_stream);
+    if (e != hipSuccess) return hip_fail(e, "histogram launch");
+    return DPT_OK;
+}
+
+int dpt_ctx_profile(dpt_ctx *c, int enable) {
+    if (!c) return fail(DPT_E_ARG, "null ctx");
+    c->profile = enable != 0;
+    return DPT_OK;
+}
+
+int dpt_ctx_profile_read(dpt_ctx *c, double *ms, uint64_t *launches) {
+    if (!c || !ms) return fail(DPT_E_ARG, "null argument");
+    DeviceGuard g(c->device);
+    ms[0] = ms[1] = ms[2] = 0.0;
+    for (size_t k = 0; k + 3 < c->events.size(); k += 4) {
+        hipError_t e = hipEventSynchronize(c->events[k + 3]);
+        if (e != hipSuccess) return hip_fail(e, "hipEventSynchronize");
+        for (int s = 0; s < 3; s++) {
+            float t = 0.f;
+            e = hipEventElapsedTime(&t, c->events[k + s], c->events[k + s + 1]);
+            if (e != hipSuccess) return hip_fail(e, "hipEventElapsedTime");
+            ms[s] += t;
+        }
+    }
+    for (hipEvent_t e : c->events) hipEventDestroy(e);
+    c->events.clear();
+    if (launches) *launches = c->launches;
+    c->launches = 0;
+    return DPT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,60 @@
+// Internal interface between the C-ABI (dpt_api.cpp) and the kernels (dpt_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace dpt {
+
+struct EncodeLaunch {
+    int mode;
+    const uint8_t *text;
+    const uint64_t *str_off;
+    const uint8_t *cut_mask;
+    uint64_t n_str;
+    int32_t *ids;
+    uint64_t *id_off;
+    int32_t *status;
+    int32_t *capped;
+    // workspace
+    int32_t *staging;
+    uint64_t *counts;
+    uint32_t *retry_list;
+    uint32_t *retry_count;
+    void *scan_temp;
+    size_t scan_temp_bytes;
+    unsigned max_blocks;
+    // vocabulary
+    const int2 *slots;
+    const int32_t *slot_ids;
+    int32_t root_base;
+};
+
+hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t ev[6]);
+size_t scan_temp_bytes(uint64_t n_str);
+hipError_t launch_histogram(const uint64_t *id_off, const int32_t *status, uint64_t n_str, int64_t *hist,
+                            uint32_t n_bins, hipStream_t stream);
+hipError_t kernel_init();
+int small_window_bytes();
+int big_window_bytes();
+
+// host double-array trie over token bytes (dpt_vocab.cpp)
+struct DoubleArray {
+    // slot t: base[t] (| TERM bit when a token ends here), check[t] = parent slot (-1 free)
+    int32_t *base = nullptr;
+    int32_t *check = nullptr;
+    int32_t *id = nullptr;
+    uint32_t n_slots = 0;
+    uint32_t n_nodes = 0;
+    uint32_t n_tokens = 0;
+    uint32_t max_bytes = 0;
+    uint32_t max_cp = 0;
+    int32_t root_base = 0;
+};
+
+// returns 0 or an error message
+const char *build_double_array(const uint8_t *blob, const uint64_t *off, const int32_t *ids, uint32_t n,
+                               DoubleArray *out);
+void free_double_array(DoubleArray *da);
+
+}  // namespace dpt

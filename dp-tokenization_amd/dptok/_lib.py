@@ -1,0 +1,72 @@
+"""ctypes binding of libdpt.so (include/dpt.h).
+
+The product path has NO CPU fallback: if the HIP library is missing or no GPU is
+visible, every call raises ``DptError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libdpt.so")
+
+DPT_OK = 0
+DPT_MODE_RAW = 0
+DPT_MODE_PRESPLIT = 1
+STATUS_OK, STATUS_NO_TOKENIZATION, STATUS_EMPTY_WORD, STATUS_TOO_LONG, STATUS_INTERNAL = range(5)
+
+
+class DptError(RuntimeError):
+    pass
+
+
+class VocabStats(ctypes.Structure):
+    _fields_ = [("n_tokens", ctypes.c_uint32), ("n_nodes", ctypes.c_uint32), ("n_slots", ctypes.c_uint32),
+                ("max_bytes", ctypes.c_uint32), ("max_cp", ctypes.c_uint32), ("device_bytes", ctypes.c_uint64)]
+
+
+_lib = None
+P = ctypes.c_void_p
+U64 = ctypes.c_uint64
+I32 = ctypes.c_int
+
+
+def lib():
+    """Load libdpt.so (raises DptError when the HIP extension is absent)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise DptError(f"HIP extension not built: {LIB_PATH} missing (run __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    L.dpt_last_error.restype = ctypes.c_char_p
+    L.dpt_abi_version.restype = I32
+    L.dpt_vocab_create.argtypes = [P, P, P, ctypes.c_uint32, I32, ctypes.POINTER(P)]
+    L.dpt_vocab_destroy.argtypes = [P]
+    L.dpt_vocab_stats_get.argtypes = [P, ctypes.POINTER(VocabStats)]
+    L.dpt_ctx_create.argtypes = [I32, ctypes.POINTER(P)]
+    L.dpt_ctx_destroy.argtypes = [P]
+    L.dpt_ctx_reserve.argtypes = [P, U64, U64]
+    L.dpt_encode.argtypes = [P, P, I32, P, U64, P, P, U64, P, U64, P, P, P, P]
+    L.dpt_encode_host.argtypes = [P, P, I32, P, U64, P, P, U64, P, U64, P, P, P]
+    L.dpt_token_histogram.argtypes = [P, P, U64, P, ctypes.c_uint32, P]
+    L.dpt_ctx_profile.argtypes = [P, I32]
+    L.dpt_ctx_profile_read.argtypes = [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(U64)]
+    for name in ("dpt_vocab_create", "dpt_vocab_destroy", "dpt_vocab_stats_get", "dpt_ctx_create", "dpt_ctx_destroy",
+                 "dpt_ctx_reserve", "dpt_encode", "dpt_encode_host", "dpt_token_histogram", "dpt_ctx_profile",
+                 "dpt_ctx_profile_read"):
+        getattr(L, name).restype = I32
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != DPT_OK:
+        msg = lib().dpt_last_error().decode("utf-8", "replace")
+        raise DptError(f"{what} failed ({rc}): {msg}")
+
+
+EXPORTED = ["dpt_last_error", "dpt_abi_version", "dpt_vocab_create", "dpt_vocab_destroy", "dpt_vocab_stats_get",
+            "dpt_ctx_create", "dpt_ctx_destroy", "dpt_ctx_reserve", "dpt_encode", "dpt_encode_host",
+            "dpt_token_histogram", "dpt_ctx_profile", "dpt_ctx_profile_read"]

@@ -1,0 +1,170 @@
+"""Host side of the engine: vocabulary upload, batch encode, status -> exception.
+
+This mirrors the reference's L2 adapter (packages/tokenizer_utils.py:52-96) one
+level down: a ``Vocab`` is the captured ``t2i``/``vocab`` of ``dp_tokenize_llama``
+(:53-57), an ``Encoder`` runs the per-word DP loop of the ``dp_tokenize`` closure
+(:66-80) for a whole batch on the GPU.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from ._lib import DPT_MODE_PRESPLIT, DPT_MODE_RAW, DptError, check
+
+MODES = {"raw": DPT_MODE_RAW, "presplit": DPT_MODE_PRESPLIT, DPT_MODE_RAW: DPT_MODE_RAW,
+         DPT_MODE_PRESPLIT: DPT_MODE_PRESPLIT}
+
+
+def _ptr(a: Optional[np.ndarray]):
+    return None if a is None else ctypes.c_void_p(a.ctypes.data)
+
+
+def encode_utf8(s: str) -> bytes:
+    return s.encode("utf-8", "surrogatepass")
+
+
+def pack_strings(texts: Sequence[str]) -> Tuple[np.ndarray, np.ndarray]:
+    enc = [encode_utf8(t) for t in texts]
+    offs = np.zeros(len(enc) + 1, dtype=np.uint64)
+    if enc:
+        offs[1:] = np.cumsum([len(e) for e in enc], dtype=np.uint64)
+    text = np.frombuffer(b"".join(enc) + b"\0", dtype=np.uint8)
+    return text, offs
+
+
+def raise_for_status(status: int, text: str = "") -> None:
+    """Re-raise the reference's exception for a per-string status."""
+    if status == _lib.STATUS_OK:
+        return
+    if status == _lib.STATUS_NO_TOKENIZATION:
+        # reference: ipdb.set_trace() then obtain_longest_token([]) -> max([]) (dp_tokenize.py:84)
+        raise ValueError("max() arg is an empty sequence (no tokenization of a word of %r)" % text[:60])
+    if status == _lib.STATUS_EMPTY_WORD:
+        # reference: segment_index_dp[-1] on an empty word (dp_tokenize.py:49)
+        raise IndexError("list index out of range (empty word)")
+    if status == _lib.STATUS_TOO_LONG:
+        raise DptError("a single word exceeds the engine window (2048 bytes)")
+    raise DptError("engine internal error (status %d)" % status)
+
+
+class Vocab:
+    """Device-resident vocabulary (double-array byte trie) built from ``t2i``."""
+
+    def __init__(self, t2i: Dict[str, int], device: int = 0):
+        L = _lib.lib()
+        toks = list(t2i.keys())
+        enc = [encode_utf8(t) for t in toks]
+        off = np.zeros(len(enc) + 1, dtype=np.uint64)
+        if enc:
+            off[1:] = np.cumsum([len(e) for e in enc], dtype=np.uint64)
+        blob = np.frombuffer(b"".join(enc) + b"\0", dtype=np.uint8)
+        ids = np.array([t2i[t] for t in toks], dtype=np.int32)
+        h = ctypes.c_void_p()
+        check(L.dpt_vocab_create(_ptr(blob), _ptr(off), _ptr(ids), len(toks), device, ctypes.byref(h)), "dpt_vocab_create")
+        self.handle = h
+        self.device = device
+        self.t2i = t2i
+        st = _lib.VocabStats()
+        check(L.dpt_vocab_stats_get(self.handle, ctypes.byref(st)), "dpt_vocab_stats_get")
+        self.stats = {f: getattr(st, f) for f, _ in st._fields_}
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h and _lib._lib is not None:
+            _lib._lib.dpt_vocab_destroy(h)
+            self.handle = None
+
+
+class Encoder:
+    """Batch shortest-tokenization on one GPU (one workspace; use from one stream at a time)."""
+
+    def __init__(self, vocab: Vocab):
+        L = _lib.lib()
+        self.vocab = vocab
+        h = ctypes.c_void_p()
+        check(L.dpt_ctx_create(vocab.device, ctypes.byref(h)), "dpt_ctx_create")
+        self.handle = h
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h and _lib._lib is not None:
+            _lib._lib.dpt_ctx_destroy(h)
+            self.handle = None
+
+    # ---------------------------------------------------------------- host buffers
+    def encode_csr(self, text: np.ndarray, offs: np.ndarray, mode="raw", cut_mask: Optional[np.ndarray] = None):
+        """CSR host arrays in -> (ids int32[], id_off u64[n+1], status int32[n], capped int32[n])."""
+        text = np.ascontiguousarray(text, dtype=np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        n = len(offs) - 1
+        n_bytes = int(offs[-1] - offs[0]) if n >= 0 else 0
+        ids = np.empty(max(n_bytes, 1), dtype=np.int32)
+        id_off = np.empty(n + 1, dtype=np.uint64)
+        status = np.empty(max(n, 1), dtype=np.int32)
+        capped = np.empty(max(n, 1), dtype=np.int32)
+        m = MODES[mode]
+        if m == DPT_MODE_PRESPLIT:
+            if cut_mask is None:
+                raise ValueError("presplit mode needs cut_mask")
+            cut_mask = np.ascontiguousarray(cut_mask, dtype=np.uint8)
+        base = int(offs[0])
+        tv = text[base:] if base else text
+        check(_lib.lib().dpt_encode_host(self.handle, self.vocab.handle, m, _ptr(tv), n_bytes, _ptr(offs),
+                                         _ptr(cut_mask[base:] if cut_mask is not None else None), n, _ptr(ids),
+                                         max(n_bytes, 1), _ptr(id_off), _ptr(status), _ptr(capped)), "dpt_encode_host")
+        return ids[: int(id_off[-1])], id_off, status[:n], capped[:n]
+
+    def encode_strs(self, texts: Sequence[str]) -> List[Tuple[List[int], int]]:
+        text, offs = pack_strings(texts)
+        ids, id_off, st, _ = self.encode_csr(text, offs)
+        return [(ids[int(id_off[i]):int(id_off[i + 1])].tolist(), int(st[i])) for i in range(len(texts))]
+
+    def encode_words(self, words: Sequence[str]) -> Tuple[List[int], int]:
+        """One string pre-split into words (llama mode, DPT_MODE_PRESPLIT): ids and status."""
+        enc = [encode_utf8(w) for w in words]
+        raw = b"".join(enc)
+        cut = np.zeros(len(raw) + 1, dtype=np.uint8)
+        o = 0
+        for e in enc:
+            if o < len(raw):
+                cut[o] = 1
+            o += len(e)
+        if any(len(e) == 0 for e in enc):
+            return [], _lib.STATUS_EMPTY_WORD
+        text = np.frombuffer(raw + b"\0", dtype=np.uint8)
+        offs = np.array([0, len(raw)], dtype=np.uint64)
+        ids, id_off, st, _ = self.encode_csr(text, offs, mode="presplit", cut_mask=cut)
+        return ids.tolist(), int(st[0])
+
+    # ---------------------------------------------------------------- device buffers
+    def encode_device(self, text_ptr: int, n_bytes: int, off_ptr: int, n_str: int, ids_ptr: int, ids_cap: int,
+                      idoff_ptr: int, status_ptr: int, capped_ptr: int = 0, cut_ptr: int = 0, stream: int = 0,
+                      mode="raw") -> None:
+        """All pointers are device addresses (e.g. ``torch.Tensor.data_ptr()``); stream-ordered, no sync."""
+        check(_lib.lib().dpt_encode(self.handle, self.vocab.handle, MODES[mode], ctypes.c_void_p(text_ptr), n_bytes,
+                                    ctypes.c_void_p(off_ptr), ctypes.c_void_p(cut_ptr or None), n_str,
+                                    ctypes.c_void_p(ids_ptr), ids_cap, ctypes.c_void_p(idoff_ptr),
+                                    ctypes.c_void_p(status_ptr), ctypes.c_void_p(capped_ptr or None),
+                                    ctypes.c_void_p(stream or None)), "dpt_encode")
+
+    def reserve(self, n_bytes: int, n_str: int) -> None:
+        check(_lib.lib().dpt_ctx_reserve(self.handle, n_bytes, n_str), "dpt_ctx_reserve")
+
+    def histogram_device(self, idoff_ptr: int, status_ptr: int, n_str: int, hist_ptr: int, n_bins: int,
+                         stream: int = 0) -> None:
+        check(_lib.lib().dpt_token_histogram(ctypes.c_void_p(idoff_ptr), ctypes.c_void_p(status_ptr), n_str,
+                                             ctypes.c_void_p(hist_ptr), n_bins, ctypes.c_void_p(stream or None)),
+              "dpt_token_histogram")
+
+    def profile(self, on: bool = True) -> None:
+        check(_lib.lib().dpt_ctx_profile(self.handle, 1 if on else 0), "dpt_ctx_profile")
+
+    def profile_read(self) -> Tuple[List[float], int]:
+        ms = (ctypes.c_double * 3)()
+        n = ctypes.c_uint64()
+        check(_lib.lib().dpt_ctx_profile_read(self.handle, ms, ctypes.byref(n)), "dpt_ctx_profile_read")
+        return [ms[0], ms[1], ms[2]], n.value

@@ -1,0 +1,132 @@
+/*
+ * dpt.h -- C-ABI of the MI355X shortest-tokenization engine (libdpt.so).
+ *
+ * Drop-in boundary for the reference's DP segmentation path.  The reference has
+ * no FFI (pure Python); these entry points are what its Python
+ * call surface binds through ctypes (dp-tokenization_amd/dptok/_lib.py):
+ *
+ *   dpt_vocab_create  <- dp_tokenize_llama's vocabulary capture,
+ *                        reference packages/tokenizer_utils.py:53-57
+ *                        (t2i = get_vocab(); vocab = set(t2i))
+ *   dpt_encode        <- the dp_tokenize closure's per-word loop,
+ *                        reference packages/tokenizer_utils.py:66-80, which calls
+ *                        compute_shortest_tokenizations (packages/dp_tokenize.py:6-70)
+ *                        and obtain_longest_token (packages/dp_tokenize.py:72-84)
+ *                        for every word produced by pretokenize_raw
+ *                        (packages/tokenizer_utils.py:33-50, DPT_MODE_RAW) or by
+ *                        pretokenize_with_llama + merge_tokens
+ *                        (packages/tokenizer_utils.py:7-31, DPT_MODE_PRESPLIT)
+ *   dpt_token_histogram <- the length comparison of the S2ORC probe,
+ *                        reference main_analyze_s2orc.py:269-297 (len(dp_tokenize(x)))
+ *
+ * Conventions: plain pointers and sizes, no C++ exceptions cross this boundary,
+ * every function returns an int (0 = DPT_OK, < 0 = error; message in
+ * dpt_last_error(), thread-local).  Device-pointer calls are stream-ordered and
+ * never synchronise.  A dpt_vocab is immutable after creation and may be shared
+ * by threads and streams; a dpt_ctx (workspace) must be used by one stream at a
+ * time.
+ */
+#ifndef DPT_H
+#define DPT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DPT_ABI_VERSION 1
+
+/* return codes */
+#define DPT_OK 0
+#define DPT_E_ARG (-1)      /* bad argument (null pointer, size) */
+#define DPT_E_HIP (-2)      /* HIP runtime error */
+#define DPT_E_VOCAB (-3)    /* vocabulary not supported (e.g. a token longer than 64 code points) */
+#define DPT_E_CAP (-4)      /* output capacity too small */
+#define DPT_E_NODEV (-5)    /* no HIP device */
+
+/* modes */
+#define DPT_MODE_RAW 0      /* pretokenize_raw semantics (tokenizer_utils.py:33-50) */
+#define DPT_MODE_PRESPLIT 1 /* words given by cut_mask; atoms = code points (llama mode) */
+
+/* per-string status (the reference's exceptions) */
+#define DPT_STATUS_OK 0
+#define DPT_STATUS_NO_TOKENIZATION 1 /* reference: ipdb.set_trace / ValueError (dp_tokenize.py:84) */
+#define DPT_STATUS_EMPTY_WORD 2      /* reference: IndexError (dp_tokenize.py:49) */
+#define DPT_STATUS_TOO_LONG 3        /* a single word longer than the engine's window (4096 bytes) */
+#define DPT_STATUS_INTERNAL 4        /* engine invariant violated (never expected) */
+
+typedef struct dpt_vocab dpt_vocab;
+typedef struct dpt_ctx dpt_ctx;
+
+typedef struct {
+    uint32_t n_tokens;     /* entries accepted (non-empty, duplicates collapsed) */
+    uint32_t n_nodes;      /* byte-trie nodes */
+    uint32_t n_slots;      /* double-array slots (incl. 256 padding) */
+    uint32_t max_bytes;    /* longest token, UTF-8 bytes */
+    uint32_t max_cp;       /* longest token, code points */
+    uint64_t device_bytes; /* device memory held by the vocab */
+} dpt_vocab_stats;
+
+const char *dpt_last_error(void);
+int dpt_abi_version(void);
+
+/*
+ * Build a vocabulary from n_tok UTF-8 strings: token t is
+ * utf8_blob[tok_off[t] .. tok_off[t+1]), its id is ids[t] (or t if ids == NULL).
+ * Later duplicates win (dict semantics); empty strings are ignored.  The library
+ * copies everything, builds a byte double-array trie on the host and uploads it
+ * to `device`.
+ */
+int dpt_vocab_create(const uint8_t *utf8_blob, const uint64_t *tok_off, const int32_t *ids,
+                     uint32_t n_tok, int device, dpt_vocab **out);
+int dpt_vocab_destroy(dpt_vocab *v);
+int dpt_vocab_stats_get(const dpt_vocab *v, dpt_vocab_stats *out);
+
+/* Workspace on `device` (grows on demand; dpt_ctx_reserve makes a later call capture-safe). */
+int dpt_ctx_create(int device, dpt_ctx **out);
+int dpt_ctx_destroy(dpt_ctx *c);
+int dpt_ctx_reserve(dpt_ctx *c, uint64_t n_bytes, uint64_t n_str);
+
+/*
+ * Tokenize n_str strings, CSR-packed: string s is text[str_off[s]-str_off[0] .. str_off[s+1]-str_off[0]),
+ * n_bytes = str_off[n_str] - str_off[0] (passed explicitly so the host never reads device memory).
+ * ALL pointers are DEVICE pointers on the ctx's device.  Outputs:
+ *   ids[id_off[s] .. id_off[s+1])  token ids of string s (none when status[s] != 0)
+ *   id_off[0..n_str]               id_off[0] = 0
+ *   status[s]                      DPT_STATUS_*
+ *   capped_len[s] (nullable)       sum over words of the reference's len_dp[-1] (dp_tokenize.py:70), -1 if unknown
+ * ids_cap must be >= n_bytes (a string never yields more ids than bytes).
+ * cut_mask (PRESPLIT only, n_bytes bytes): 1 where a word starts; byte 0 of every string always starts one.
+ * Stream-ordered on hip_stream (hipStream_t, NULL = default stream); no host synchronisation.
+ */
+int dpt_encode(dpt_ctx *c, const dpt_vocab *v, int mode, const uint8_t *text, uint64_t n_bytes,
+               const uint64_t *str_off, const uint8_t *cut_mask, uint64_t n_str, int32_t *ids,
+               uint64_t ids_cap, uint64_t *id_off, int32_t *status, int32_t *capped_len,
+               void *hip_stream);
+
+/* Same with HOST pointers: copies in, runs, copies out, synchronises. */
+int dpt_encode_host(dpt_ctx *c, const dpt_vocab *v, int mode, const uint8_t *text, uint64_t n_bytes,
+                    const uint64_t *str_off, const uint8_t *cut_mask, uint64_t n_str, int32_t *ids,
+                    uint64_t ids_cap, uint64_t *id_off, int32_t *status, int32_t *capped_len);
+
+/*
+ * Token-count histogram (device pointers): hist[0..n_bins) counts strings by
+ * #ids (last bin = overflow), then hist[n_bins+0] = total ids, hist[n_bins+1] =
+ * total strings, hist[n_bins+2+k] = strings with status k (k = 0..4).
+ * hist must hold n_bins + 8 int64 and is ACCUMULATED into (zero it first).
+ */
+int dpt_token_histogram(const uint64_t *id_off, const int32_t *status, uint64_t n_str,
+                        int64_t *hist, uint32_t n_bins, void *hip_stream);
+
+/* Per-ctx kernel timing with HIP events on the encode stream (for bench.py's roofline). */
+int dpt_ctx_profile(dpt_ctx *c, int enable);
+/* Sums over calls since the last read (synchronises on the recorded events):
+ * ms[0] tokenize kernel, ms[1] scan, ms[2] compact; *launches = tokenize launches. */
+int dpt_ctx_profile_read(dpt_ctx *c, double *ms, uint64_t *launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DPT_H */

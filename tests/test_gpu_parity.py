@@ -1,0 +1,146 @@
+"""GPU parity: the HIP engine (through the C-ABI) against the reference's golden
+vectors (bit-exact ids + status + capped lengths) and against the C oracle on
+seeded random inputs at larger sizes."""
+import numpy as np
+import pytest
+
+from conftest import CORPUS_FIXTURES, load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def engines(vocabs):
+    from dptok import Encoder, Vocab
+    return {k: Encoder(Vocab(v, 0)) for k, v in vocabs.items()}
+
+
+@pytest.fixture(scope="module")
+def oracles(vocabs):
+    from oracle import oracle
+    return {k: oracle.OracleVocab(v) for k, v in vocabs.items()}
+
+
+def _csr(texts):
+    from dptok import pack_strings
+    return pack_strings(texts)
+
+
+def _cmp_csr(a, b):
+    ids_a, off_a, st_a = a[:3]
+    ids_b, off_b, st_b = b[:3]
+    assert np.array_equal(st_a, st_b), np.nonzero(st_a != st_b)[0][:10]
+    assert np.array_equal(off_a, off_b), np.nonzero(off_a != off_b)[0][:10]
+    assert np.array_equal(ids_a, ids_b)
+
+
+@pytest.mark.parametrize("name", CORPUS_FIXTURES)
+def test_golden_vectors(name, engines):
+    g = load_golden(name)
+    cases = [c for c in g["cases"] if not c.get("skipped")]
+    text, offs = _csr([c["text"] for c in cases])
+    ids, id_off, st, capped = engines[g["vocab"]].encode_csr(text, offs)
+    for i, c in enumerate(cases):
+        got = ids[int(id_off[i]):int(id_off[i + 1])].tolist()
+        assert int(st[i]) == c["status"], (i, c["text"][:50])
+        assert got == c["ids"], (i, c["text"][:50])
+        if c.get("capped") is not None:
+            assert int(capped[i]) == c["capped"], (i, c["text"][:50])
+
+
+def test_small_random_vocab_cases():
+    from dptok import Encoder, Vocab
+    g = load_golden("small_random.json.gz")
+    bad = []
+    for c in g["cases"]:
+        t2i = {t: i for i, t in enumerate(c["vocab"])}
+        (ids, st), = Encoder(Vocab(t2i, 0)).encode_strs([c["text"]])
+        if (ids, st) != (c["ids"], c["status"]):
+            bad.append((c["text"], c["vocab"], ids, st, c["ids"], c["status"]))
+    assert not bad, bad[:3]
+
+
+@pytest.mark.parametrize("n,length,seed", [(131072, 256, 7), (20000, 64, 3), (4096, 1000, 9)])
+def test_random_ascii_vs_oracle(n, length, seed, engines, oracles):
+    from dptok import synth
+    text, offs = synth.random_ascii_corpus(n, length, seed=seed)
+    got = engines["llama32k"].encode_csr(text, offs)
+    ref = oracles["llama32k"].encode_csr(text, offs)
+    _cmp_csr(got, ref)
+    assert np.array_equal(got[3], ref[3])
+
+
+def test_s2orc_and_arabic_vs_oracle(engines, oracles):
+    from dptok import synth
+    for text, offs in (synth.s2orc_like_corpus(600, seed=44), synth.arabic_corpus(20000, seed=55)):
+        _cmp_csr(engines["llama32k"].encode_csr(text, offs), oracles["llama32k"].encode_csr(text, offs))
+
+
+def test_long_words_big_window(engines, oracles):
+    """Words longer than the 256-byte window take the 2048-byte pass; > 2048 -> status 3."""
+    rng = np.random.default_rng(5)
+    texts = []
+    for L in (255, 256, 257, 300, 700, 1500, 2047, 2048, 2049, 3000):
+        w = "".join(chr(c) for c in rng.integers(0x21, 0x7F, size=L))
+        texts.append(w)
+        texts.append("ab cd " + w + " ef")
+        texts.append(w + " " + w[: L // 2])
+    text, offs = _csr(texts)
+    ids, id_off, st, capped = engines["llama32k"].encode_csr(text, offs)
+    rids, roff, rst, rcap = oracles["llama32k"].encode_csr(text, offs)
+    for i, t in enumerate(texts):
+        longest = max(len(x.encode()) + (1 if k else 0) for k, x in enumerate(t.split(" ")))
+        if longest > 2048:
+            assert st[i] == 3, (i, len(t))
+            assert id_off[i + 1] == id_off[i]
+            continue
+        assert st[i] == rst[i], i
+        assert ids[int(id_off[i]):int(id_off[i + 1])].tolist() == rids[int(roff[i]):int(roff[i + 1])].tolist(), i
+        assert capped[i] == rcap[i]
+
+
+def test_empty_batch_and_empty_strings(engines):
+    enc = engines["llama32k"]
+    ids, id_off, st, _ = enc.encode_csr(np.zeros(1, np.uint8), np.zeros(1, np.uint64))
+    assert len(ids) == 0 and id_off.tolist() == [0]
+    text, offs = _csr(["", "a", "", " ", ""])
+    ids, id_off, st, _ = enc.encode_csr(text, offs)
+    assert st.tolist() == [2, 0, 2, 1, 2]
+
+
+def test_presplit_mode_vs_oracle(engines, oracles):
+    from dptok import synth
+    from oracle import oracle
+    text, offs = synth.random_ascii_corpus(5000, 200, seed=12)
+    rng = np.random.default_rng(0)
+    cut = (rng.random(len(text)) < 0.12).astype(np.uint8)
+    got = engines["llama32k"].encode_csr(text, offs, mode="presplit", cut_mask=cut)
+    ref = oracles["llama32k"].encode_csr(text, offs, mode=oracle.PRESPLIT, cut_mask=cut)
+    _cmp_csr(got, ref)
+
+
+def test_device_path_and_histogram(engines, oracles):
+    torch = pytest.importorskip("torch")
+    from dptok import synth
+    n = 50000
+    text, offs = synth.random_ascii_corpus(n, 256, seed=21)
+    enc = engines["llama32k"]
+    dt = torch.from_numpy(text).cuda()
+    do = torch.from_numpy(offs.view(np.int64)).cuda()
+    ids = torch.empty(len(text), dtype=torch.int32, device="cuda")
+    id_off = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    st = torch.empty(n, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    enc.encode_device(dt.data_ptr(), len(text), do.data_ptr(), n, ids.data_ptr(), len(text), id_off.data_ptr(),
+                      st.data_ptr(), stream=s)
+    hist = torch.zeros(258 + 8, dtype=torch.int64, device="cuda")
+    enc.histogram_device(id_off.data_ptr(), st.data_ptr(), n, hist.data_ptr(), 258, stream=s)
+    torch.cuda.synchronize()
+    rids, roff, rst, _ = oracles["llama32k"].encode_csr(text, offs)
+    off_h = id_off.cpu().numpy().view(np.uint64)
+    assert np.array_equal(off_h, roff)
+    assert np.array_equal(ids[: int(off_h[-1])].cpu().numpy(), rids)
+    h = hist.cpu().numpy()
+    counts = np.diff(roff.astype(np.int64))
+    assert h[258] == counts.sum() and h[259] == n and h[260] == n
+    assert np.array_equal(h[:257], np.bincount(np.minimum(counts, 257), minlength=258)[:257])
