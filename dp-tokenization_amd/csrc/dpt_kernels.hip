@@ -281,6 +281,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                     // tag of the last expanded byte of byte k
                     L.etag[ex] = (uint8_t)(((nf & 1) ? TAG_ATOM_END : 0) | ((nf & 2) ? TAG_WORD_END : 0));
                     ex++;
+                    cp += cpl[u];
                 }
                 n_ex += t1 & 0xFFFF; cp_tot += t1 >> 16;
                 n_atoms += t2 & 0xFFFF; n_words += t2 >> 16;

@@ -37,6 +37,14 @@ def lib():
     global _lib
     if _lib is not None:
         return _lib
+    if os.environ.get("DPT_NO_TORCH", "0") != "1":
+        # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64.so.7. Loading it
+        # first makes libdpt.so bind to that copy (same SONAME) instead of /opt/rocm's, so device
+        # pointers and streams from torch are valid for the engine.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
     if not os.path.exists(LIB_PATH):
         raise DptError(f"HIP extension not built: {LIB_PATH} missing (run __graft_entry__.build())")
     L = ctypes.CDLL(LIB_PATH)
