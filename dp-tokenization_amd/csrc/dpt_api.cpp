@@ -5,6 +5,7 @@
 // event-based kernel timing used by bench.py.  No C++ exception crosses the ABI.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -17,6 +18,7 @@ struct dpt_vocab {
     int device = 0;
     int2 *d_slots = nullptr;
     int32_t *d_ids = nullptr;
+    int4 *d_slots4 = nullptr;         // {base | TERM, check, id, 0} for the lane kernel
     int32_t root_base = 0;
     dpt_vocab_stats stats{};
 };
@@ -25,6 +27,7 @@ struct dpt_ctx {
     int device = 0;
     // workspace
     int32_t *staging = nullptr;
+    uint4 *rec = nullptr;             // lane kernel backtrace records (cap_bytes entries)
     uint64_t cap_bytes = 0;
     uint64_t *counts = nullptr;
     uint32_t *retry_list = nullptr;
@@ -87,8 +90,12 @@ hipError_t grow(T **p, uint64_t *cap, uint64_t need) {
 int ensure_workspace(dpt_ctx *c, uint64_t n_bytes, uint64_t n_str) {
     hipError_t e;
     if (n_bytes > c->cap_bytes || !c->staging) {
-        e = grow(&c->staging, &c->cap_bytes, n_bytes);
+        uint64_t cap1 = c->cap_bytes, cap2 = c->cap_bytes;
+        e = grow(&c->staging, &cap1, n_bytes);
         if (e != hipSuccess) return hip_fail(e, "hipMalloc(staging)");
+        e = grow(&c->rec, &cap2, n_bytes);
+        if (e != hipSuccess) return hip_fail(e, "hipMalloc(rec)");
+        c->cap_bytes = cap1 < cap2 ? cap1 : cap2;
     }
     if (n_str > c->cap_str || !c->counts) {
         uint64_t cap = c->cap_str, cap2 = c->cap_str;
@@ -111,6 +118,21 @@ int ensure_workspace(dpt_ctx *c, uint64_t n_bytes, uint64_t n_str) {
         if (e != hipSuccess) return hip_fail(e, "hipMalloc(retry_count)");
     }
     return DPT_OK;
+}
+
+// First-pass kernel: 16-lane rows (4 strings per wave) when every token has <= 16 code
+// points, else 64-lane rows.  DPT_KERNEL=lane|rows16|rows64 overrides (A/B measurements; the
+// lane kernel measured slower on cfg2: 2x the VALU count and ~30 GB of scratch traffic per
+// 1M strings, profiles/r01_pmc_*).
+int kernel_variant(uint32_t max_cp) {
+    int v = max_cp <= 16 ? dpt::KERNEL_ROWS16 : dpt::KERNEL_ROWS64;
+    if (const char *e = getenv("DPT_KERNEL")) {
+        if (!strcmp(e, "rows16")) v = dpt::KERNEL_ROWS16;
+        else if (!strcmp(e, "rows64")) v = dpt::KERNEL_ROWS64;
+        else if (!strcmp(e, "lane")) v = dpt::KERNEL_LANE;
+    }
+    if (max_cp > 16) v = dpt::KERNEL_ROWS64;
+    return v;
 }
 
 }  // namespace
@@ -150,8 +172,14 @@ int dpt_vocab_create(const uint8_t *utf8_blob, const uint64_t *tok_off, const in
     }
     v->device = device;
     std::vector<int2> slots(da.n_slots);
-    for (uint32_t t = 0; t < da.n_slots; t++) slots[t] = make_int2(da.base[t], da.check[t]);
+    std::vector<int4> slots4(da.n_slots);
+    for (uint32_t t = 0; t < da.n_slots; t++) {
+        slots[t] = make_int2(da.base[t], da.check[t]);
+        slots4[t] = make_int4(da.base[t], da.check[t], da.id[t], 0);
+    }
     e = hipMalloc((void **)&v->d_slots, sizeof(int2) * da.n_slots);
+    if (e == hipSuccess) e = hipMalloc((void **)&v->d_slots4, sizeof(int4) * da.n_slots);
+    if (e == hipSuccess) e = hipMemcpy(v->d_slots4, slots4.data(), sizeof(int4) * da.n_slots, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc((void **)&v->d_ids, sizeof(int32_t) * da.n_slots);
     if (e == hipSuccess) e = hipMemcpy(v->d_slots, slots.data(), sizeof(int2) * da.n_slots, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(v->d_ids, da.id, sizeof(int32_t) * da.n_slots, hipMemcpyHostToDevice);
@@ -159,6 +187,7 @@ int dpt_vocab_create(const uint8_t *utf8_blob, const uint64_t *tok_off, const in
         dpt::free_double_array(&da);
         if (v->d_slots) hipFree(v->d_slots);
         if (v->d_ids) hipFree(v->d_ids);
+        if (v->d_slots4) hipFree(v->d_slots4);
         delete v;
         return hip_fail(e, "vocab upload");
     }
@@ -168,7 +197,7 @@ int dpt_vocab_create(const uint8_t *utf8_blob, const uint64_t *tok_off, const in
     v->stats.n_slots = da.n_slots;
     v->stats.max_bytes = da.max_bytes;
     v->stats.max_cp = da.max_cp;
-    v->stats.device_bytes = (uint64_t)da.n_slots * (sizeof(int2) + sizeof(int32_t));
+    v->stats.device_bytes = (uint64_t)da.n_slots * (sizeof(int2) + sizeof(int32_t) + sizeof(int4));
     dpt::free_double_array(&da);
     *out = v;
     return DPT_OK;
@@ -179,6 +208,7 @@ int dpt_vocab_destroy(dpt_vocab *v) {
     DeviceGuard g(v->device);
     hipFree(v->d_slots);
     hipFree(v->d_ids);
+    hipFree(v->d_slots4);
     delete v;
     return DPT_OK;
 }
@@ -208,7 +238,7 @@ int dpt_ctx_create(int device, dpt_ctx **out) {
 int dpt_ctx_destroy(dpt_ctx *c) {
     if (!c) return DPT_OK;
     DeviceGuard g(c->device);
-    void *ps[] = {c->staging, c->counts, c->retry_list, c->retry_count, c->scan_temp, c->h_text, c->h_cut,
+    void *ps[] = {c->staging, c->rec, c->counts, c->retry_list, c->retry_count, c->scan_temp, c->h_text, c->h_cut,
                   c->h_ids, c->h_off, c->h_idoff, c->h_status, c->h_capped};
     for (void *p : ps)
         if (p) hipFree(p);
@@ -255,8 +285,12 @@ int dpt_encode(dpt_ctx *c, const dpt_vocab *v, int mode, const uint8_t *text, ui
     p.scan_temp = c->scan_temp;
     p.scan_temp_bytes = c->scan_bytes;
     p.max_blocks = c->max_blocks;
+    p.rec = c->rec;
+    p.variant = kernel_variant(v->stats.max_cp);
     p.slots = v->d_slots;
     p.slot_ids = v->d_ids;
+    p.n_slots = v->stats.n_slots;
+    p.slots4 = v->d_slots4;
     p.root_base = v->root_base;
     hipEvent_t ev[6];
     hipEvent_t *evp = nullptr;

@@ -24,13 +24,23 @@ struct EncodeLaunch {
     void *scan_temp;
     size_t scan_temp_bytes;
     unsigned max_blocks;
+    int variant;             // KERNEL_* below
+    uint4 *rec;              // lane kernel: per-atom backtrace records (n_bytes entries)
     // vocabulary
     const int2 *slots;
     const int32_t *slot_ids;
+    const int4 *slots4;      // lane kernel: {base | TERM<<31, check, id, 0}
+    uint32_t n_slots;
     int32_t root_base;
 };
 
+// kernel variants for the first pass (the 2048-byte window pass always follows for retries)
+constexpr int KERNEL_LANE = 0;    // lane per string, register ring of 16 walks (vocab max_cp <= 16)
+constexpr int KERNEL_ROWS16 = 1;  // 4 strings per wave in 16-lane DPP rows, LDS windows (max_cp <= 16)
+constexpr int KERNEL_ROWS64 = 2;  // 1 string per wave, 64-lane DPP (max_cp <= 64)
+
 hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t ev[6]);
+void launch_lane(const EncodeLaunch &p, unsigned blocks, hipStream_t stream);
 size_t scan_temp_bytes(uint64_t n_str);
 hipError_t launch_histogram(const uint64_t *id_off, const int32_t *status, uint64_t n_str, int64_t *hist,
                             uint32_t n_bins, hipStream_t stream);

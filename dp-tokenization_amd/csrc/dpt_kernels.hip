@@ -1,35 +1,40 @@
 // dpt_kernels.hip -- CDNA4 (gfx950) kernels of the shortest-tokenization engine.
 //
-// One input string per wavefront (64 lanes).  Per window of <= CH input bytes
-// (windows end at word boundaries; words are independent DP problems,
-// reference packages/tokenizer_utils.py:70):
+// A wavefront holds NG = 64/G independent strings ("slots"), each in a G-lane
+// group (G = 16 when every vocabulary token has <= 16 code points -- Llama-2 --
+// else G = 64, one string per wave).  Per window of <= CH input bytes (windows
+// end at word boundaries; words are independent DP problems, reference
+// packages/tokenizer_utils.py:70):
 //
 //   prep   atomise the window like pretokenize_raw (tokenizer_utils.py:33-50) into
 //          an atom-expanded UTF-8 byte string in LDS ('▁'+c first, ' '->'▁',
 //          '\n'->'<0x0A>'), with atom/word-end tags, atom offsets, code-point
 //          prefix sums (cp(span) = cpos[i]-cpos[j], the len(t) of dp_tokenize.py:82)
-//          and the word-start list -- two packed DPP wave scans.
+//          and word starts -- packed DPP wave scans.
 //   A      match discovery: lanes walk the byte double-array trie (L2-resident)
-//          from every atom start; a bit (L-1) of smask[j] records that the L-atom
-//          span from atom j is a vocabulary token ("join(atoms[j:i]) in vocabulary",
-//          dp_tokenize.py:39).  Lanes that finish pick up the next start (ballot +
-//          mbcnt), so the wave stays busy.
-//   B      forward recurrence, sequential over end positions i with lanes = back
-//          distances d (j = i-1-d): per lane one 32-bit key
+//          from every atom start of every slot; bit (L-1) of smask[j] records that
+//          the L-atom span from atom j is a vocabulary token ("join(atoms[j:i]) in
+//          vocabulary", dp_tokenize.py:39).  Lanes that finish take the next start
+//          (ballot + mbcnt), so the wave stays busy.
+//   B      forward recurrence, sequential over end positions i; lane d of a group
+//          holds candidate j = i-1-d and forms ONE 32-bit key
 //              (cost[j]+1) << 16 | invalid[j] << 15 | (0x7FFF - max(G[j], cp(span)))
-//          and ONE DPP wave-min gives cost[i] (capped at the atom index within the
-//          word, dp_tokenize.py:28), reachability and the max-of-max token length
-//          G[i].  The per-lane state (state, cpos,
-//          smask of j) is shifted one lane per step with DPP wave_shr:1 -- no LDS
-//          traffic on the critical path.
-//   C1     selection: per word, right to left, lanes = back distances, ballot of
-//          "j in E(i), valid, max(A, cp, G[j]) == G[n]", the LOWEST set lane is
-//          the LARGEST j -- the reference's first argmax in DFS order
-//          (dp_tokenize.py:58 pops the largest j first, :84 takes the first max).
-//   C2     id resolution: lanes re-walk each selected span through the trie and
-//          write t2i[token] (tokenizer_utils.py:76-79) to a staging row.
+//          a DPP group-min gives cost[i] (capped at the atom index within the word,
+//          dp_tokenize.py:28), reachability and the max-of-max token length G[i]
+//          (SURVEY.md Appendix A 1-3).  Two ballots record, per end i, the lanes in
+//          E(i) (dp_tokenize.py:40-46) that are reachable (em) and those that attain
+//          G[i] (gm).  The per-lane state (state, cpos, smask of j) moves one lane per
+//          step by DPP row_shr:1 / wave_shr:1 -- no LDS on the recurrence.
+//   C1     selection, one lane per word: walking right to left, pick the LOWEST set
+//          bit (= LARGEST j) of gm[i] while the longest token so far is below G[n],
+//          of em[i] once it is reached.  That is the reference's first argmax in DFS
+//          order (dp_tokenize.py:58 pops the largest j first; :84 takes the first max).
+//   C2     id resolution: lanes re-walk each selected span through the trie and write
+//          t2i[token] (tokenizer_utils.py:76-79) to the slot's staging row.
 //
-// A separate scan + compaction turns the staging rows into CSR ids.
+// Strings whose single word exceeds CH bytes (or whose atom expansion exceeds the LDS
+// budget) are re-run by the 2048-byte, one-string-per-wave instantiation.  A scan +
+// compaction turns the staging rows into CSR ids.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include <stdint.h>
@@ -53,12 +58,19 @@ __device__ __forceinline__ unsigned wave_incl_scan_add(unsigned v) {
     return v;
 }
 
+// min within each row of 16 lanes, result in every lane of the row
+// (mov_dpp with bound_ctrl lets hipcc fold each step into one v_min_u32_dpp)
+__device__ __forceinline__ unsigned row_min_u32(unsigned v) {
+    v = min(v, (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true));   // quad_perm [1,0,3,2]
+    v = min(v, (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, true));   // quad_perm [2,3,0,1]
+    v = min(v, (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, true));  // row_half_mirror
+    v = min(v, (unsigned)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, true));  // row_mirror
+    return v;
+}
+
 // min over 64 lanes, result uniform (SGPR)
 __device__ __forceinline__ unsigned wave_min_u32(unsigned v) {
-    v = min(v, (unsigned)__builtin_amdgcn_update_dpp(v, v, 0xB1, 0xF, 0xF, false));  // quad_perm [1,0,3,2]
-    v = min(v, (unsigned)__builtin_amdgcn_update_dpp(v, v, 0x4E, 0xF, 0xF, false));  // quad_perm [2,3,0,1]
-    v = min(v, (unsigned)__builtin_amdgcn_update_dpp(v, v, 0x141, 0xF, 0xF, false)); // row_half_mirror
-    v = min(v, (unsigned)__builtin_amdgcn_update_dpp(v, v, 0x140, 0xF, 0xF, false)); // row_mirror
+    v = row_min_u32(v);
     v = min(v, (unsigned)__builtin_amdgcn_update_dpp(v, v, 0x142, 0xA, 0xF, false)); // row_bcast:15
     v = min(v, (unsigned)__builtin_amdgcn_update_dpp(v, v, 0x143, 0xC, 0xF, false)); // row_bcast:31
     return __builtin_amdgcn_readlane(v, 63);
@@ -74,14 +86,49 @@ __device__ __forceinline__ unsigned wave_max_u32(unsigned v) {
     return __builtin_amdgcn_readlane(v, 63);
 }
 
-// lane l receives x[l-1]; lane 0 receives `in` (DPP wave_shr:1, bound_ctrl off)
-__device__ __forceinline__ unsigned shift_in(unsigned x, unsigned in) {
+// lane l receives x[l-1]; the first lane of each row (row_shr:1) / of the wave (wave_shr:1) receives `in`
+__device__ __forceinline__ unsigned row_shift_in(unsigned x, unsigned in) {
+    return (unsigned)__builtin_amdgcn_update_dpp((int)in, (int)x, 0x111, 0xF, 0xF, false);
+}
+__device__ __forceinline__ unsigned wave_shift_in(unsigned x, unsigned in) {
     return (unsigned)__builtin_amdgcn_update_dpp((int)in, (int)x, 0x138, 0xF, 0xF, false);
 }
 
 __device__ __forceinline__ unsigned uni(unsigned x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ uint64_t uni64(uint64_t x) {
+    return ((uint64_t)uni((unsigned)(x >> 32)) << 32) | uni((unsigned)x);
+}
 
 __device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// ------------------------------------------------------------------ group geometry
+
+template <int G> struct Group;
+
+// G = 16: four strings per wave, one per DPP row.  Per atom: {cpos, span mask} in one
+// dword; per end position: {gm, em} in one dword.
+template <> struct Group<16> {
+    using M = uint16_t;  // span mask: bit L-1 = an L-atom token starts here
+    struct Rec { uint16_t cpos; uint16_t smask; };
+    struct Gem { uint32_t v; };
+    static __device__ __forceinline__ unsigned gm(const Gem &x) { return x.v & 0xFFFFu; }
+    static __device__ __forceinline__ unsigned em(const Gem &x) { return x.v >> 16; }
+};
+
+// G = 64: one string per wave (vocabularies with tokens of 17..64 code points).
+template <> struct Group<64> {
+    using M = uint64_t;
+    struct Rec { uint64_t smask; uint16_t cpos; uint16_t pad[3]; };
+    struct Gem { uint64_t gm, em; };
+    static __device__ __forceinline__ uint64_t gm(const Gem &x) { return x.gm; }
+    static __device__ __forceinline__ uint64_t em(const Gem &x) { return x.em; }
+};
 
 // ------------------------------------------------------------------ LDS layout
 
@@ -91,25 +138,38 @@ constexpr uint8_t TAG_WORD_END = 2;
 
 constexpr unsigned ST_VALID = 0x8000u;
 constexpr unsigned ST_RESET = ST_VALID;   // cost 0, reachable, G 0
-constexpr unsigned MAXD = 64;             // longest span in atoms (vocab max_cp <= 64 enforced on the host)
+constexpr uint16_t CP_WS = 0x8000;        // cpos bit: atom starts a word
 
-template <int CH>
-struct WaveLDS {
+template <int CH, int G, int EXP>
+struct GroupLDS {
+    using M = typename Group<G>::M;
     static constexpr int NA = CH + 2;            // atoms + sentinel
-    static constexpr int NE = 6 * CH + 8;        // expanded bytes ('\n' -> 6 bytes; first atom +3)
-    uint64_t smask[NA];
-    uint32_t state[NA];
-    uint32_t tok[NA];
-    uint32_t wfin[NA];
-    uint16_t aoff[NA];
-    uint16_t cpos[NA];
-    uint16_t wsl[NA];
+    static constexpr int NE = EXP * CH + 8;      // expanded bytes
+    // rec[j]: code-point prefix of atom j (| CP_WS at word starts and at the window end)
+    //         and the span mask of tokens of 1..G atoms starting at j
+    typename Group<G>::Rec rec[NA];
+    // gem[i]: lanes d (j = i-1-d) in E(i) that are reachable (em) and that attain G[i] (gm)
+    typename Group<G>::Gem gem[NA];
+    uint32_t wfin[NA];  // per word: the final group-min key (cost<<16 | invalid<<15 | 0x7FFF-G)
+    uint16_t aoff[NA];  // atom -> expanded byte offset
+    uint16_t wsl[NA];   // word -> first atom
+    uint16_t tok[NA];   // selected token -> first atom (tokens tile the window)
     uint8_t ebyte[NE];
     uint8_t etag[NE];
 };
 
-template <int CH>
-constexpr int wave_lds_bytes() { return (int)((sizeof(WaveLDS<CH>) + 15) & ~size_t(15)); }
+struct SlotState {
+    uint64_t s, sb, slen, pos;
+    uint32_t active, status, ntok, capsum;
+    uint32_t wlen, n_atoms, n_words, wtok;
+    uint32_t inval, pad0, pad1, pad2;
+};
+
+template <int CH, int G, int EXP>
+constexpr int group_lds_bytes() { return (int)((sizeof(GroupLDS<CH, G, EXP>) + 15) & ~size_t(15)); }
+
+template <int CH, int G, int EXP>
+constexpr int block_lds_bytes() { return (64 / G) * (group_lds_bytes<CH, G, EXP>() + (int)sizeof(SlotState)); }
 
 // ------------------------------------------------------------------ trie access
 
@@ -121,334 +181,491 @@ struct TrieView {
 
 constexpr int32_t TERM_BIT = (int32_t)0x80000000;
 
-// ------------------------------------------------------------------ the tokenize kernel
+// ------------------------------------------------------------------ arguments
 
 struct EncodeArgs {
     const uint8_t *text;
     const uint64_t *str_off;
     const uint8_t *cut_mask;    // PRESPLIT only
     uint64_t n_str;
-    uint64_t base_off;          // str_off[0] (read on device)
     int32_t *staging;           // ids staged at (str_off[s]-str_off[0]) + k
     uint64_t *counts;           // per string
     int32_t *status;
     int32_t *capped;            // nullable
-    uint32_t *retry_list;       // strings that overflowed the window (status TOO_LONG) for the big pass
+    uint32_t *retry_list;       // strings for the 2048-byte pass
     uint32_t *retry_count;
-    const uint32_t *work_list;  // big pass: list of string indices (nullable => all strings)
+    const uint32_t *work_list;  // 2048-byte pass: the retry list
     const uint32_t *work_count;
     int mode;
 };
 
-template <int CH, int WPB, bool BIG>
-__global__ void __launch_bounds__(WPB * 64)
-tokenize_kernel(EncodeArgs a, TrieView tv) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const unsigned wid = threadIdx.x >> 6;
-    const unsigned lane = lane_id();
-    WaveLDS<CH> &L = *reinterpret_cast<WaveLDS<CH> *>(smem + wid * wave_lds_bytes<CH>());
+#ifdef DPT_STAMPS
+// diagnostic build only: cycles per phase summed over waves (never in the product build)
+__device__ unsigned long long g_stamps[8];
+#define STAMP_DECL unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}; unsigned long long st_prev = __builtin_amdgcn_s_memtime();
+#define STAMP(k) do { const unsigned long long _t = __builtin_amdgcn_s_memtime(); st_acc[k] += _t - st_prev; st_prev = _t; } while (0)
+#define STAMP_FLUSH do { if (lane == 0) for (int _k = 0; _k < 6; _k++) atomicAdd(&g_stamps[_k], st_acc[_k]); } while (0)
+#else
+#define STAMP_DECL
+#define STAMP(k)
+#define STAMP_FLUSH
+#endif
 
+// ------------------------------------------------------------------ prep: one slot's window
+
+// Finds the window [pos, pos+wlen) (ends at a word start or at the string end).
+// Returns false when a single word does not fit in CH bytes.
+template <int CH>
+__device__ bool window_bounds(const uint8_t *str, const uint8_t *cut, uint64_t slen, uint64_t pos, bool raw,
+                              unsigned lane, unsigned &wlen) {
+    const uint64_t rem = slen - pos;
+    if (rem <= (uint64_t)CH) {
+        wlen = (unsigned)rem;
+        return true;
+    }
+    int best = -1;
+    for (int k = lane; k <= CH; k += 64) {
+        if (k == 0) continue;
+        const uint64_t p = pos + k;
+        const uint8_t b = str[p];
+        const bool ws = raw ? (b == ' ') : (cut[p] != 0 && (b & 0xC0) != 0x80);
+        if (ws) best = k;
+    }
+    const unsigned q = wave_max_u32((unsigned)(best + 1));
+    if (q == 0) return false;
+    wlen = q - 1;
+    return true;
+}
+
+// Atomise window bytes [pos, pos+wlen) into L.  Returns false if the expansion
+// does not fit the LDS budget.  Whole wave cooperates.
+template <int CH, int G, int EXP>
+__device__ bool prep_window(GroupLDS<CH, G, EXP> &L, const uint8_t *str, const uint8_t *cut, uint64_t pos,
+                            unsigned wlen, bool raw, unsigned lane, unsigned &n_atoms_o, unsigned &n_words_o) {
+    constexpr unsigned EX_BUDGET = GroupLDS<CH, G, EXP>::NE - 8;
+    unsigned n_atoms = 0, n_ex = 0, cp_tot = 0, n_words = 0;
+    for (unsigned c0 = 0; c0 < wlen; c0 += 256) {
+        uint8_t bt[4];
+        unsigned cpl[4];
+        bool ast[4], wst[4];
+        unsigned ex_sum = 0, cp_sum = 0, a_sum = 0, w_sum = 0;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const unsigned k = c0 + lane * 4 + u;
+            const bool in = k < wlen;
+            const uint64_t p = pos + k;
+            const uint8_t b = in ? str[p] : 0;
+            const bool first = in && p == 0;
+            const bool cont = in && !first && (b & 0xC0) == 0x80;
+            const bool as = in && !cont;
+            bool wsf;
+            unsigned el, cl;
+            if (raw) {
+                wsf = as && (k == 0 || b == ' ');
+                el = !in ? 0 : first ? 4 : (b == ' ' ? 3 : (b == '\n' ? 6 : 1));
+                cl = !in ? 0 : first ? 2 : (b == '\n' ? 6 : (cont ? 0 : 1));
+            } else {
+                wsf = as && (k == 0 || cut[p] != 0);
+                el = in ? 1 : 0;
+                cl = as ? 1 : 0;
+            }
+            bt[u] = b; cpl[u] = cl; ast[u] = as; wst[u] = wsf;
+            ex_sum += el; cp_sum += cl; a_sum += as; w_sum += wsf;
+        }
+        // packed scans: (ex | cp<<16), (atoms | words<<16); every field < 65536
+        const unsigned v1 = ex_sum | (cp_sum << 16);
+        const unsigned v2 = a_sum | (w_sum << 16);
+        const unsigned i1 = wave_incl_scan_add(v1);
+        const unsigned i2 = wave_incl_scan_add(v2);
+        const unsigned t1 = __builtin_amdgcn_readlane(i1, 63);
+        const unsigned t2 = __builtin_amdgcn_readlane(i2, 63);
+        if (n_ex + (t1 & 0xFFFF) > EX_BUDGET) return false;
+        unsigned ex = n_ex + ((i1 - v1) & 0xFFFF);
+        unsigned cp = cp_tot + ((i1 - v1) >> 16);
+        unsigned ai = n_atoms + ((i2 - v2) & 0xFFFF);
+        unsigned wi = n_words + ((i2 - v2) >> 16);
+        // does the byte after each of mine start an atom / a word?
+        const unsigned my_first_flags = (ast[0] ? 1u : 0u) | (wst[0] ? 2u : 0u);
+        unsigned next_flags = (unsigned)__shfl_down((int)my_first_flags, 1);
+        const unsigned kn = c0 + 256;
+        unsigned chunk_next = 3;  // end of window: atom end + word end
+        if (kn < wlen) {
+            const uint64_t p = pos + kn;
+            const uint8_t b = str[p];
+            const bool as = (b & 0xC0) != 0x80;
+            const bool wsf = as && (raw ? b == ' ' : cut[p] != 0);
+            chunk_next = (as ? 1u : 0u) | (wsf ? 2u : 0u);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const unsigned k = c0 + lane * 4 + u;
+            if (k >= wlen) break;
+            const uint64_t p = pos + k;
+            unsigned nf;
+            if (k + 1 >= wlen) nf = 3;
+            else if (u < 3) nf = (ast[u + 1] ? 1u : 0u) | (wst[u + 1] ? 2u : 0u);
+            else nf = (lane == 63) ? chunk_next : next_flags;
+            if (ast[u]) {
+                L.aoff[ai] = (uint16_t)ex;
+                L.rec[ai].cpos = (uint16_t)(cp | (wst[u] ? CP_WS : 0));
+                if (wst[u]) { L.wsl[wi] = (uint16_t)ai; wi++; }
+                ai++;
+            }
+            const uint8_t b = bt[u];
+            if (raw && p == 0) {
+                L.ebyte[ex] = 0xE2; L.ebyte[ex + 1] = 0x96; L.ebyte[ex + 2] = 0x81; L.ebyte[ex + 3] = b;
+                L.etag[ex] = 0; L.etag[ex + 1] = 0; L.etag[ex + 2] = 0;
+                ex += 3;
+            } else if (raw && b == ' ') {
+                L.ebyte[ex] = 0xE2; L.ebyte[ex + 1] = 0x96; L.ebyte[ex + 2] = 0x81;
+                L.etag[ex] = 0; L.etag[ex + 1] = 0;
+                ex += 2;
+            } else if (raw && b == '\n') {
+                L.ebyte[ex] = '<'; L.ebyte[ex + 1] = '0'; L.ebyte[ex + 2] = 'x';
+                L.ebyte[ex + 3] = '0'; L.ebyte[ex + 4] = 'A'; L.ebyte[ex + 5] = '>';
+                L.etag[ex] = 0; L.etag[ex + 1] = 0; L.etag[ex + 2] = 0; L.etag[ex + 3] = 0; L.etag[ex + 4] = 0;
+                ex += 5;
+            } else {
+                L.ebyte[ex] = b;
+            }
+            L.etag[ex] = (uint8_t)(((nf & 1) ? TAG_ATOM_END : 0) | ((nf & 2) ? TAG_WORD_END : 0));
+            ex++;
+            cp += cpl[u];
+        }
+        n_ex += t1 & 0xFFFF; cp_tot += t1 >> 16;
+        n_atoms += t2 & 0xFFFF; n_words += t2 >> 16;
+    }
+    if (lane == 0) {
+        L.aoff[n_atoms] = (uint16_t)n_ex;
+        L.rec[n_atoms].cpos = (uint16_t)(cp_tot | CP_WS);
+        L.wsl[n_words] = (uint16_t)n_atoms;
+    }
+    n_atoms_o = n_atoms;
+    n_words_o = n_words;
+    return true;
+}
+
+// ------------------------------------------------------------------ the tokenize kernel
+
+template <int CH, int G, int EXP, bool BIG>
+__global__ void __launch_bounds__(64)
+tokenize_kernel(EncodeArgs a, TrieView tv) {
+    constexpr int NG = 64 / G;
+    using GL = GroupLDS<CH, G, EXP>;
+    using GR = Group<G>;
+    using M = typename GR::M;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    SlotState *const SS = reinterpret_cast<SlotState *>(smem + NG * group_lds_bytes<CH, G, EXP>());
+    auto grp = [&](unsigned g) -> GL & { return *reinterpret_cast<GL *>(smem + g * group_lds_bytes<CH, G, EXP>()); };
+
+    const unsigned lane = lane_id();
+    const unsigned mg = lane / G;        // my group
+    const unsigned d = lane % G;         // my back distance - 1
     const uint64_t n_work = BIG ? (uint64_t)(*a.work_count) : a.n_str;
-    const uint64_t wave_global = (uint64_t)blockIdx.x * WPB + wid;
-    const uint64_t wave_stride = (uint64_t)gridDim.x * WPB;
     const uint64_t base_off = a.str_off[0];
     const bool raw = a.mode == 0;
+    uint64_t next = blockIdx.x;          // one wave per block
+    const uint64_t stride = gridDim.x;
+    STAMP_DECL
 
-    for (uint64_t w = wave_global; w < n_work; w += wave_stride) {
-        const uint64_t s = BIG ? (uint64_t)a.work_list[w] : w;
-        const uint64_t sb = a.str_off[s] - base_off;
-        const uint64_t slen = a.str_off[s + 1] - a.str_off[s];
-        const uint8_t *str = a.text + sb;
-        const uint8_t *cut = raw ? nullptr : a.cut_mask + sb;
-        int32_t *out = a.staging + sb;
+    if (lane < (unsigned)NG) SS[lane].active = 0;
+    wave_sync();
 
-        unsigned status = 0;
-        unsigned ntok = 0;        // ids emitted so far
-        unsigned capsum = 0;      // sum of capped word lengths
-        bool capped_known = true;
-        if (slen == 0) status = 2;  // pretokenize_raw('') == [[]] -> IndexError
-
-        uint64_t pos = 0;
-        while (status != 2 && status != 3 && pos < slen) {
-            // ---------------------------------------------------------- window bounds
-            const uint64_t rem = slen - pos;
-            unsigned wlen;
-            if (rem <= (uint64_t)CH) {
-                wlen = (unsigned)rem;
-            } else {
-                // last word start q in [1, CH]: the window is [pos, pos+q)
-                int best = -1;
-                for (int k = lane; k <= CH; k += 64) {
-                    if (k == 0) continue;
-                    const uint64_t p = pos + k;
-                    const uint8_t b = str[p];
-                    bool ws = raw ? (b == ' ') : (cut[p] != 0 && (b & 0xC0) != 0x80);
-                    if (ws) best = k;
+    for (;;) {
+        // ---------------------------------------------------------- slots: fetch strings, find windows, prep
+        unsigned busy = 0;
+        for (unsigned g = 0; g < (unsigned)NG; g++) {
+            GL &L = grp(g);
+            SlotState &S = SS[g];
+            for (;;) {
+                if (!uni(S.active)) {
+                    if (next >= n_work) break;
+                    const uint64_t s = BIG ? (uint64_t)a.work_list[next] : next;
+                    next += stride;
+                    const uint64_t sb = a.str_off[s] - base_off;
+                    const uint64_t sl = a.str_off[s + 1] - a.str_off[s];
+                    if (lane == 0) {
+                        S.s = s; S.sb = sb; S.slen = sl; S.pos = 0; S.active = 1;
+                        S.status = sl == 0 ? 2u : 0u;  // pretokenize_raw('') == [[]] -> IndexError
+                        S.ntok = 0; S.capsum = 0;
+                    }
+                    wave_sync();
                 }
-                const unsigned q = wave_max_u32((unsigned)(best + 1));
-                if (q == 0) { status = 3; break; }  // one word longer than the window
-                wlen = q - 1;
+                const uint64_t sb = uni64(S.sb), slen = uni64(S.slen), pos = uni64(S.pos);
+                unsigned status = uni(S.status);
+                const uint8_t *str = a.text + sb;
+                const uint8_t *cut = raw ? nullptr : a.cut_mask + sb;
+                unsigned wlen = 0, na = 0, nw = 0;
+                bool ok = status != 2;
+                if (ok) ok = window_bounds<CH>(str, cut, slen, pos, raw, lane, wlen);
+                if (ok) ok = prep_window<CH, G, EXP>(L, str, cut, pos, wlen, raw, lane, na, nw);
+                if (ok) {
+                    if (lane == 0) { S.wlen = wlen; S.n_atoms = na; S.n_words = nw; }
+                    busy++;
+                    break;
+                }
+                // the string ends here: empty, or a word too long for this pass
+                if (status != 2) status = 3;
+                if (lane == 0) {
+                    const uint64_t s = S.s;
+                    if (status == 3 && !BIG) {
+                        const unsigned slot = atomicAdd(a.retry_count, 1u);
+                        a.retry_list[slot] = (uint32_t)s;
+                    }
+                    a.status[s] = (int32_t)status;
+                    a.counts[s] = 0;
+                    if (a.capped) a.capped[s] = status == 2 ? 0 : -1;
+                    S.active = 0;
+                }
+                wave_sync();
             }
+            if (lane == 0 && !S.active) { S.n_atoms = 0; S.n_words = 0; }
+        }
+        wave_sync();
+        if (busy == 0) break;
+        STAMP(0);
 
-            // ---------------------------------------------------------- prep: atomise
-            // lane l owns bytes 4l..4l+3 of each 256-byte chunk of the window
-            unsigned n_atoms = 0, n_ex = 0, cp_tot = 0, n_words = 0;
-            for (unsigned c0 = 0; c0 < wlen; c0 += 256) {
-                uint8_t bt[4];
-                unsigned exl[4], cpl[4];
-                bool ast[4], wst[4];
-                unsigned ex_sum = 0, cp_sum = 0, a_sum = 0, w_sum = 0;
+        // ---------------------------------------------------------- A: match discovery (all slots)
+        {
+            unsigned pre[NG + 1];
+            pre[0] = 0;
 #pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const unsigned k = c0 + lane * 4 + u;
-                    const bool in = k < wlen;
-                    const uint64_t p = pos + k;
-                    const uint8_t b = in ? str[p] : 0;
-                    const bool first = in && p == 0;
-                    const bool cont = in && !first && (b & 0xC0) == 0x80;
-                    const bool as = in && !cont;
-                    bool wsf;
-                    unsigned el, cl;
-                    if (raw) {
-                        wsf = as && (k == 0 || b == ' ');
-                        el = !in ? 0 : first ? 4 : (b == ' ' ? 3 : (b == '\n' ? 6 : 1));
-                        cl = !in ? 0 : first ? 2 : (b == '\n' ? 6 : (cont ? 0 : 1));
-                    } else {
-                        wsf = as && (k == 0 || cut[p] != 0);
-                        el = in ? 1 : 0;
-                        cl = as ? 1 : 0;
-                    }
-                    bt[u] = b; exl[u] = el; cpl[u] = cl; ast[u] = as; wst[u] = wsf;
-                    ex_sum += el; cp_sum += cl; a_sum += as; w_sum += wsf;
-                }
-                // packed scans: (ex | cp<<16), (atoms | words<<16); all fields < 65536
-                const unsigned v1 = ex_sum | (cp_sum << 16);
-                const unsigned v2 = a_sum | (w_sum << 16);
-                const unsigned i1 = wave_incl_scan_add(v1);
-                const unsigned i2 = wave_incl_scan_add(v2);
-                const unsigned t1 = __builtin_amdgcn_readlane(i1, 63);
-                const unsigned t2 = __builtin_amdgcn_readlane(i2, 63);
-                unsigned ex = n_ex + ((i1 - v1) & 0xFFFF);
-                unsigned cp = cp_tot + ((i1 - v1) >> 16);
-                unsigned ai = n_atoms + ((i2 - v2) & 0xFFFF);
-                unsigned wi = n_words + ((i2 - v2) >> 16);
-                // does the byte after each of mine start an atom / word?
-                const unsigned my_first_flags = (ast[0] ? 1u : 0u) | (wst[0] ? 2u : 0u);
-                unsigned next_flags = (unsigned)__shfl_down((int)my_first_flags, 1);
-                if (lane == 63) next_flags = 0;
-                // the next chunk's first byte (crossing a 256-byte chunk inside the window)
-                const unsigned kn = c0 + 256;
-                unsigned chunk_next = 3;  // end of window: atom end + word end
-                if (kn < wlen) {
-                    const uint64_t p = pos + kn;
-                    const uint8_t b = str[p];
-                    const bool as = (b & 0xC0) != 0x80;
-                    const bool wsf = as && (raw ? b == ' ' : cut[p] != 0);
-                    chunk_next = (as ? 1u : 0u) | (wsf ? 2u : 0u);
-                }
+            for (int g = 0; g < NG; g++) pre[g + 1] = pre[g] + uni(SS[g].n_atoms);
+            const unsigned total = pre[NG];
+            unsigned gsel = 0, j = 0;
+            auto locate = [&](unsigned uu) {
+                gsel = 0;
 #pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const unsigned k = c0 + lane * 4 + u;
-                    if (k >= wlen) break;
-                    const uint64_t p = pos + k;
-                    unsigned nf;
-                    if (k + 1 >= wlen) nf = 3;
-                    else if (u < 3) nf = (ast[u + 1] ? 1u : 0u) | (wst[u + 1] ? 2u : 0u);
-                    else nf = (lane == 63) ? chunk_next : next_flags;
-                    if (ast[u]) {
-                        L.aoff[ai] = (uint16_t)ex;
-                        L.cpos[ai] = (uint16_t)cp;
-                        if (wst[u]) { L.wsl[wi] = (uint16_t)ai; wi++; }
-                        ai++;
-                    }
-                    const uint8_t b = bt[u];
-                    if (raw && p == 0) {
-                        L.ebyte[ex] = 0xE2; L.ebyte[ex + 1] = 0x96; L.ebyte[ex + 2] = 0x81; L.ebyte[ex + 3] = b;
-                        L.etag[ex] = 0; L.etag[ex + 1] = 0; L.etag[ex + 2] = 0;
-                        ex += 3;
-                    } else if (raw && b == ' ') {
-                        L.ebyte[ex] = 0xE2; L.ebyte[ex + 1] = 0x96; L.ebyte[ex + 2] = 0x81;
-                        L.etag[ex] = 0; L.etag[ex + 1] = 0;
-                        ex += 2;
-                    } else if (raw && b == '\n') {
-                        L.ebyte[ex] = '<'; L.ebyte[ex + 1] = '0'; L.ebyte[ex + 2] = 'x';
-                        L.ebyte[ex + 3] = '0'; L.ebyte[ex + 4] = 'A'; L.ebyte[ex + 5] = '>';
-                        L.etag[ex] = 0; L.etag[ex + 1] = 0; L.etag[ex + 2] = 0; L.etag[ex + 3] = 0; L.etag[ex + 4] = 0;
-                        ex += 5;
+                for (int g = 1; g < NG; g++) gsel += uu >= pre[g] ? 1u : 0u;
+                unsigned base = 0;
+#pragma unroll
+                for (int g = 0; g < NG; g++) base = (gsel == (unsigned)g) ? pre[g] : base;
+                j = uu - base;
+            };
+            unsigned u = lane;
+            bool active = u < total;
+            unsigned e = 0;
+            int32_t nb = tv.root_base, node = 0;
+            unsigned len = 0, mask = 0;
+            uint64_t mask64 = 0;
+            if (active) { locate(u); e = grp(gsel).aoff[j]; }
+            unsigned nxt = 64;
+            while (ballot(active)) {
+                bool done = false;
+                if (active) {
+                    GL &L = grp(gsel);
+                    const uint8_t b = L.ebyte[e];
+                    const uint8_t tg = L.etag[e];
+                    const int32_t t = nb + (int32_t)b;
+                    const int2 ent = tv.slots[t];
+                    if (ent.y != node) {
+                        done = true;
                     } else {
-                        L.ebyte[ex] = b;
-                    }
-                    // tag of the last expanded byte of byte k
-                    L.etag[ex] = (uint8_t)(((nf & 1) ? TAG_ATOM_END : 0) | ((nf & 2) ? TAG_WORD_END : 0));
-                    ex++;
-                    cp += cpl[u];
-                }
-                n_ex += t1 & 0xFFFF; cp_tot += t1 >> 16;
-                n_atoms += t2 & 0xFFFF; n_words += t2 >> 16;
-            }
-            if (lane == 0) {
-                L.aoff[n_atoms] = (uint16_t)n_ex;
-                L.cpos[n_atoms] = (uint16_t)cp_tot;
-                L.wsl[n_words] = (uint16_t)n_atoms;
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-
-            // ---------------------------------------------------------- A: match discovery
-            {
-                unsigned j = lane;
-                unsigned e = j < n_atoms ? L.aoff[j] : 0;
-                int32_t nb = tv.root_base;     // base of the current node
-                int32_t node = 0;              // current slot (root = 0)
-                unsigned len = 0;
-                uint64_t mask = 0;
-                unsigned next = 64;
-                bool active = j < n_atoms;
-                while (ballot(active)) {
-                    bool done = false;
-                    if (active) {
-                        const uint8_t b = L.ebyte[e];
-                        const uint8_t tg = L.etag[e];
-                        const int32_t t = nb + (int32_t)b;
-                        const int2 ent = tv.slots[t];
-                        if (ent.y != node) {
-                            done = true;
-                        } else {
-                            node = t;
-                            nb = ent.x & 0x7FFFFFFF;
-                            e++;
-                            if (tg & TAG_ATOM_END) {
-                                len++;
-                                if (ent.x & TERM_BIT) mask |= 1ull << (len - 1);
-                                if ((tg & TAG_WORD_END) || len == MAXD) done = true;
+                        node = t;
+                        nb = ent.x & 0x7FFFFFFF;
+                        e++;
+                        if (tg & TAG_ATOM_END) {
+                            len++;
+                            if (ent.x & TERM_BIT) {
+                                if (G == 64) mask64 |= 1ull << (len - 1);
+                                else mask |= 1u << (len - 1);
                             }
+                            if ((tg & TAG_WORD_END) || len == (unsigned)G) done = true;
                         }
                     }
-                    const uint64_t dm = ballot(done);
-                    if (done) {
-                        L.smask[j] = mask;
-                        const unsigned rank = __builtin_amdgcn_mbcnt_hi((unsigned)(dm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)dm, 0u));
-                        j = next + rank;
-                        active = j < n_atoms;
-                        if (active) { e = L.aoff[j]; nb = tv.root_base; node = 0; len = 0; mask = 0; }
+                }
+                const uint64_t dm = ballot(done);
+                if (done) {
+                    if (G == 64) grp(gsel).rec[j].smask = (M)mask64;
+                    else grp(gsel).rec[j].smask = (M)mask;
+                    const unsigned rank = __builtin_amdgcn_mbcnt_hi((unsigned)(dm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)dm, 0u));
+                    u = nxt + rank;
+                    active = u < total;
+                    if (active) { locate(u); e = grp(gsel).aoff[j]; nb = tv.root_base; node = 0; len = 0; mask = 0; mask64 = 0; }
+                }
+                nxt += (unsigned)__builtin_popcountll(dm);
+            }
+        }
+        wave_sync();
+        STAMP(1);
+
+        // ---------------------------------------------------------- B: forward recurrence
+        {
+            GL &L = grp(mg);
+            const unsigned na = SS[mg].n_atoms;
+            unsigned imax = 0;
+#pragma unroll
+            for (int g = 0; g < NG; g++) imax = max(imax, uni(SS[g].n_atoms));
+            // st (lane d, candidate j = i-1-d) = (cost[j]+1) << 16 | invalid[j] << 15 | G[j]
+            constexpr unsigned ST0 = 0x10000u;   // word start: cost 0, reachable, G 0
+            unsigned ws = 0, w = 0, wsum = 0, winv = 0;
+            if constexpr (G == 16) {
+                const uint32_t *rec32 = reinterpret_cast<const uint32_t *>(L.rec);
+                const uint32_t r0 = rec32[0];
+                unsigned st = d == 0 ? ST0 : 0u;
+                unsigned cpj = 0;
+                unsigned m = (d == 0 && na > 0) ? (r0 >> 16) : 0u;
+                uint32_t nx = rec32[1];
+                for (unsigned i = 1; i <= imax; i++) {
+                    const uint32_t cur = nx;
+                    nx = rec32[i + 1];                         // i+1 <= CH+1 < NA: always in bounds
+                    const unsigned cpi = cur & 0x7FFFu;
+                    const unsigned span = cpi - cpj;
+                    const unsigned gj = st & 0x7FFFu;
+                    const unsigned kv = (st | 0x7FFFu) - (gj > span ? gj : span);
+                    const unsigned key = ((m >> d) & 1u) ? kv : 0xFFFFFFFFu;
+                    unsigned r = row_min_u32(key);
+                    const unsigned capkey = ((i - ws) << 16) | 0xFFFFu;
+                    r = r < capkey ? r : capkey;
+                    const uint64_t gmb = ballot(key == r);
+                    const uint64_t emb = ballot((key ^ r) < 0x8000u);
+                    const bool live = i <= na;
+                    const bool wend = live && (cur & CP_WS);  // CP_WS marks word starts and the window end
+                    const bool boundary = wend && i < na;
+                    if (d == 0 && live) {
+                        const unsigned sh = 16u * mg;
+                        L.gem[i].v = ((unsigned)(gmb >> sh) & 0xFFFFu) | ((unsigned)(emb >> sh) << 16);
+                        if (wend) L.wfin[w] = r;
                     }
-                    next += (unsigned)__builtin_popcountll(dm);
+                    wsum += wend ? (r >> 16) : 0u;
+                    winv |= wend ? (r & 0x8000u) : 0u;
+                    w += boundary ? 1u : 0u;
+                    ws = boundary ? i : ws;
+                    const unsigned sin = boundary ? ST0 : ((r ^ 0x7FFFu) + 0x10000u);
+                    st = row_shift_in(st, sin);
+                    cpj = row_shift_in(cpj, cpi);
+                    m = row_shift_in(m, cur >> 16);
+                }
+            } else {
+                unsigned st = d == 0 ? ST0 : 0u;
+                unsigned cpj = 0;
+                const uint64_t m0 = na > 0 ? L.rec[0].smask : 0ull;
+                unsigned mlo = d == 0 ? (unsigned)m0 : 0u, mhi = d == 0 ? (unsigned)(m0 >> 32) : 0u;
+                for (unsigned i = 1; i <= imax; i++) {
+                    const unsigned cur = L.rec[i].cpos;
+                    const uint64_t mi = L.rec[i].smask;
+                    const unsigned cpi = cur & 0x7FFFu;
+                    const unsigned span = cpi - cpj;
+                    const unsigned gj = st & 0x7FFFu;
+                    const unsigned kv = (st | 0x7FFFu) - (gj > span ? gj : span);
+                    const unsigned bit = (d < 32 ? (mlo >> d) : (mhi >> (d - 32))) & 1u;
+                    const unsigned key = bit ? kv : 0xFFFFFFFFu;
+                    unsigned r = wave_min_u32(key);
+                    const unsigned capkey = ((i - ws) << 16) | 0xFFFFu;
+                    r = r < capkey ? r : capkey;
+                    const uint64_t gmb = ballot(key == r);
+                    const uint64_t emb = ballot((key ^ r) < 0x8000u);
+                    const bool wend = (cur & CP_WS) != 0;
+                    const bool boundary = wend && i < na;
+                    if (lane == 0) {
+                        L.gem[i].gm = gmb;
+                        L.gem[i].em = emb;
+                        if (wend) L.wfin[w] = r;
+                    }
+                    wsum += wend ? (r >> 16) : 0u;
+                    winv |= wend ? (r & 0x8000u) : 0u;
+                    w += boundary ? 1u : 0u;
+                    ws = boundary ? i : ws;
+                    const unsigned sin = boundary ? ST0 : ((r ^ 0x7FFFu) + 0x10000u);
+                    st = wave_shift_in(st, sin);
+                    cpj = wave_shift_in(cpj, cpi);
+                    mlo = wave_shift_in(mlo, (unsigned)mi);
+                    mhi = wave_shift_in(mhi, (unsigned)(mi >> 32));
                 }
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (d == 0 && na > 0) {
+                SlotState &S = SS[mg];
+                S.capsum += wsum;
+                S.inval = winv ? 1u : 0u;
+                S.wtok = wsum;
+            }
+        }
+        wave_sync();
+        STAMP(2);
 
-            // ---------------------------------------------------------- B: forward recurrence
-            {
-                unsigned st = 0, cpj = 0, mlo = 0, mhi = 0;
-                // position 0 (the first word start) enters lane 0
-                {
-                    const uint64_t m0 = L.smask[0];
-                    st = shift_in(st, ST_RESET);
-                    cpj = shift_in(cpj, 0u);
-                    mlo = shift_in(mlo, uni((unsigned)m0));
-                    mhi = shift_in(mhi, uni((unsigned)(m0 >> 32)));
-                }
-                if (lane == 0) L.state[0] = ST_RESET;
-                unsigned wcur = 0, ws = 0;
-                unsigned next_ws = n_words > 1 ? uni(L.wsl[1]) : n_atoms;
-                const unsigned d = lane;
-                for (unsigned i0 = 1; i0 <= n_atoms; i0 += 64) {
-                    // preload the uniform per-position inputs of 64 steps
-                    const unsigned pi = i0 + lane;
-                    const unsigned pcp = pi <= n_atoms ? L.cpos[pi] : 0u;
-                    const uint64_t pm = pi < n_atoms ? L.smask[pi] : 0ull;
-                    const unsigned pml = (unsigned)pm, pmh = (unsigned)(pm >> 32);
-                    const unsigned iend = min(n_atoms, i0 + 63);
-                    for (unsigned i = i0; i <= iend; i++) {
-                        const unsigned k = i - i0;
-                        const unsigned cpi = __builtin_amdgcn_readlane(pcp, k);
-                        const unsigned bit = (d < 32 ? (mlo >> d) : (mhi >> (d - 32))) & 1u;
-                        const unsigned span = cpi - cpj;
-                        const unsigned gj = st & 0x7FFFu;
-                        const unsigned g = gj > span ? gj : span;
-                        const unsigned key = bit ? ((((st >> 16) + 1u) << 16) | ((st & ST_VALID) ^ ST_VALID) | (0x7FFFu - g))
-                                                 : 0xFFFFFFFFu;
-                        unsigned r = wave_min_u32(key);
-                        const unsigned capkey = ((i - ws) << 16) | 0xFFFFu;
-                        r = r < capkey ? r : capkey;
-                        const bool v = (r & ST_VALID) == 0;
-                        const unsigned si = (r & 0xFFFF0000u) | (v ? (ST_VALID | (0x7FFFu - (r & 0x7FFFu))) : 0u);
-                        unsigned sin = si;
-                        if (i == next_ws && i < n_atoms) {
-                            if (lane == 0) L.wfin[wcur] = si;
-                            wcur++;
-                            ws = i;
-                            next_ws = (wcur + 1 < n_words) ? uni(L.wsl[wcur + 1]) : n_atoms;
-                            sin = ST_RESET;
-                        }
-                        if (i == n_atoms && lane == 0) L.wfin[wcur] = si;
-                        if (lane == 0) L.state[i] = sin;
-                        st = shift_in(st, sin);
-                        cpj = shift_in(cpj, cpi);
-                        mlo = shift_in(mlo, __builtin_amdgcn_readlane(pml, k));
-                        mhi = shift_in(mhi, __builtin_amdgcn_readlane(pmh, k));
+        // ---------------------------------------------------------- C1: selection, one lane per word
+        {
+            unsigned pre[NG + 1], tokpre[NG + 1], inv_g[NG];
+            pre[0] = 0; tokpre[0] = 0;
+#pragma unroll
+            for (int g = 0; g < NG; g++) {
+                const unsigned nwg = uni(SS[g].n_atoms) > 0 ? uni(SS[g].n_words) : 0u;
+                inv_g[g] = uni(SS[g].inval) | (uni(SS[g].status) != 0 ? 1u : 0u);
+                pre[g + 1] = pre[g] + nwg;
+                tokpre[g + 1] = tokpre[g] + (nwg ? uni(SS[g].wtok) : 0u);
+            }
+            const unsigned total = pre[NG];
+            unsigned carry = 0;
+            for (unsigned u0 = 0; u0 < total; u0 += 64) {
+                const unsigned u = u0 + lane;
+                const bool in = u < total;
+                unsigned g = 0;
+#pragma unroll
+                for (int k = 1; k < NG; k++) g += u >= pre[k] ? 1u : 0u;
+                unsigned wbase = 0, tbase = 0, ginv = 0;
+#pragma unroll
+                for (int k = 0; k < NG; k++)
+                    if (g == (unsigned)k) { wbase = pre[k]; tbase = tokpre[k]; ginv = inv_g[k]; }
+                GL &L = grp(g);
+                const unsigned w = u - wbase;
+                const unsigned F = in ? L.wfin[w] : 0u;
+                const unsigned cost = in ? (F >> 16) : 0u;
+                const unsigned incl = wave_incl_scan_add(cost);
+                const unsigned tok_base = carry + incl - cost - tbase;
+                carry += __builtin_amdgcn_readlane(incl, 63);
+                if (in && !ginv) {
+                    const unsigned ws = L.wsl[w];
+                    unsigned i = L.wsl[w + 1];
+                    const unsigned Ls = 0x7FFFu - (F & 0x7FFFu);   // G of the word = the longest token to reach
+                    unsigned c = cost, A = 0;
+                    unsigned pend = L.rec[i].cpos & 0x7FFFu;
+                    while (i > ws) {
+                        const typename GR::Gem gem = L.gem[i];
+                        const unsigned cpi = L.rec[i].cpos & 0x7FFFu;
+                        const unsigned sp = pend - cpi;
+                        A = A > sp ? A : sp;                 // the token emitted last step ended at pend
+                        const M sel = (M)(A < Ls ? GR::gm(gem) : GR::em(gem));
+                        const unsigned dd = (G == 64) ? (unsigned)__builtin_ctzll((uint64_t)sel | (1ull << 63))
+                                                      : (unsigned)__builtin_ctz((unsigned)sel | 0x80000000u);
+                        if (sel == 0 || dd + 1 > i - ws || c == 0) break;   // unreachable by Appendix A
+                        const unsigned j = i - 1 - dd;
+                        c--;
+                        L.tok[tok_base + c] = (uint16_t)j;
+                        pend = cpi;
+                        i = j;
                     }
                 }
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        wave_sync();
+        STAMP(3);
 
-            // ---------------------------------------------------------- C1: selection
-            unsigned wtok = 0;   // tokens of this window
-            for (unsigned w = 0; w < n_words; w++) {
-                const unsigned F = uni(L.wfin[w]);
-                capsum += F >> 16;
-                if (status) continue;                 // keep summing capped lengths only
-                if (!(F & ST_VALID)) { status = 1; continue; }
-                const unsigned ws = uni(L.wsl[w]);
-                unsigned i = uni(L.wsl[w + 1]);
-                unsigned c = F >> 16;
-                const unsigned Ls = F & 0x7FFFu;
-                unsigned A = 0;
-                unsigned cpi = uni(L.cpos[i]);
-                const unsigned base = wtok;
-                while (i > ws) {
-                    const unsigned d = lane;
-                    const int j = (int)i - 1 - (int)d;
-                    bool cond = false;
-                    unsigned cj = 0;
-                    if (j >= (int)ws && d < MAXD) {
-                        const uint64_t m = L.smask[j];
-                        const unsigned sj = L.state[j];
-                        cj = L.cpos[j];
-                        const unsigned span = cpi - cj;
-                        unsigned mx = A > span ? A : span;
-                        const unsigned gj = sj & 0x7FFFu;
-                        mx = mx > gj ? mx : gj;
-                        cond = ((m >> d) & 1ull) && (sj >> 16) + 1u == c && (sj & ST_VALID) && mx == Ls;
-                    }
-                    const uint64_t bal = ballot(cond);
-                    if (bal == 0) { status = 4; break; }
-                    const unsigned dd = (unsigned)__builtin_ctzll(bal);
-                    const unsigned jj = i - 1 - dd;
-                    const unsigned cjj = __builtin_amdgcn_readlane(cj, dd);
-                    c--;
-                    if (lane == 0) L.tok[base + c] = jj | (i << 16);
-                    const unsigned span = cpi - cjj;
-                    A = A > span ? A : span;
-                    i = jj;
-                    cpi = cjj;
-                }
-                if (!status) wtok += F >> 16;
+        // ---------------------------------------------------------- C2: ids (lanes over all slots' tokens)
+        {
+            unsigned pre[NG + 1], na_g[NG];
+            pre[0] = 0;
+#pragma unroll
+            for (int g = 0; g < NG; g++) {
+                const bool gv = uni(SS[g].inval) == 0 && uni(SS[g].status) == 0 && uni(SS[g].n_atoms) > 0;
+                pre[g + 1] = pre[g] + (gv ? uni(SS[g].wtok) : 0u);
+                na_g[g] = uni(SS[g].n_atoms);
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-
-            // ---------------------------------------------------------- C2: ids
-            if (!status) {
-                for (unsigned t = lane; t < wtok; t += 64) {
-                    const unsigned ji = L.tok[t];
-                    const unsigned e0 = L.aoff[ji & 0xFFFF], e1 = L.aoff[ji >> 16];
+            const unsigned total = pre[NG];
+            for (unsigned t0 = 0; t0 < total; t0 += 64) {
+                const unsigned t = t0 + lane;
+                if (t < total) {
+                    unsigned g = 0;
+#pragma unroll
+                    for (int k = 1; k < NG; k++) g += t >= pre[k] ? 1u : 0u;
+                    unsigned base = 0, na = 0, ntk = 0;
+#pragma unroll
+                    for (int k = 0; k < NG; k++)
+                        if (g == (unsigned)k) { base = pre[k]; na = na_g[k]; ntk = pre[k + 1] - pre[k]; }
+                    GL &L = grp(g);
+                    const unsigned k = t - base;
+                    const unsigned j0 = L.tok[k];
+                    const unsigned j1 = k + 1 < ntk ? L.tok[k + 1] : na;
+                    const unsigned e0 = L.aoff[j0], e1 = L.aoff[j1];
                     int32_t node = 0, nb = tv.root_base;
                     bool ok = true;
                     for (unsigned e = e0; e < e1; e++) {
@@ -458,26 +675,33 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                         node = sl;
                         nb = ent.x & 0x7FFFFFFF;
                     }
-                    out[ntok + t] = ok ? tv.ids[node] : -1;
+                    const SlotState &S = SS[g];
+                    a.staging[S.sb + S.ntok + k] = ok ? tv.ids[node] : -1;
                 }
-                ntok += wtok;
             }
-            pos += wlen;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-        if (status == 3) capped_known = false;
-        if (lane == 0) {
-            if (status == 3 && !BIG) {
-                const unsigned slot = atomicAdd(a.retry_count, 1u);
-                a.retry_list[slot] = (uint32_t)s;
+        wave_sync();
+
+        // ---------------------------------------------------------- advance slots, finish strings
+        if (lane < (unsigned)NG) {
+            SlotState &S = SS[lane];
+            if (S.active && S.n_atoms > 0) {
+                if (S.inval && S.status == 0) S.status = 1;
+                if (S.status == 0) S.ntok += S.wtok;
+                S.pos += S.wlen;
+                if (S.pos >= S.slen) {
+                    const uint64_t s = S.s;
+                    a.status[s] = (int32_t)S.status;
+                    a.counts[s] = S.status == 0 ? (uint64_t)S.ntok : 0ull;
+                    if (a.capped) a.capped[s] = (int32_t)S.capsum;
+                    S.active = 0;
+                }
             }
-            a.status[s] = (int32_t)status;
-            a.counts[s] = status == 0 ? (uint64_t)ntok : 0ull;
-            if (a.capped) a.capped[s] = capped_known ? (int32_t)capsum : -1;
         }
+        wave_sync();
+        STAMP(4);
     }
+    STAMP_FLUSH;
 }
 
 // ------------------------------------------------------------------ compaction
@@ -525,15 +749,22 @@ __global__ void __launch_bounds__(256) hist_kernel(const uint64_t *__restrict__ 
 
 // ------------------------------------------------------------------ launchers
 
-constexpr int SMALL_CH = 256, SMALL_WPB = 4;
-constexpr int BIG_CH = 2048, BIG_WPB = 1;
+constexpr int SMALL_CH = 256, SMALL_EXP = 2;
+constexpr int BIG_CH = 2048, BIG_EXP = 6;
 
-static_assert(wave_lds_bytes<SMALL_CH>() * SMALL_WPB <= 64 * 1024, "small LDS");
-static_assert(wave_lds_bytes<BIG_CH>() * BIG_WPB <= 160 * 1024, "big LDS");
+static_assert(block_lds_bytes<SMALL_CH, 16, SMALL_EXP>() <= 64 * 1024, "small LDS");
+static_assert(block_lds_bytes<SMALL_CH, 64, SMALL_EXP>() <= 64 * 1024, "small LDS");
+static_assert(block_lds_bytes<BIG_CH, 64, BIG_EXP>() <= 160 * 1024, "big LDS");
+
+template <int CH, int G, int EXP, bool BIG>
+static void launch_tok(const EncodeArgs &a, const TrieView &tv, unsigned blocks, hipStream_t stream) {
+    constexpr int lds = block_lds_bytes<CH, G, EXP>();
+    hipLaunchKernelGGL((tokenize_kernel<CH, G, EXP, BIG>), dim3(blocks), dim3(64), lds, stream, a, tv);
+}
 
 hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t ev[6]) {
     EncodeArgs a;
-    a.text = p.text; a.str_off = p.str_off; a.cut_mask = p.cut_mask; a.n_str = p.n_str; a.base_off = 0;
+    a.text = p.text; a.str_off = p.str_off; a.cut_mask = p.cut_mask; a.n_str = p.n_str;
     a.staging = p.staging; a.counts = p.counts; a.status = p.status; a.capped = p.capped;
     a.retry_list = p.retry_list; a.retry_count = p.retry_count; a.work_list = nullptr; a.work_count = nullptr;
     a.mode = p.mode;
@@ -542,16 +773,21 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     hipLaunchKernelGGL(zero_first, dim3(1), dim3(64), 0, stream, p.id_off, p.retry_count);
     if (ev) hipEventRecord(ev[0], stream);
     if (p.n_str > 0) {
-        const uint64_t waves = p.n_str;
-        uint64_t blocks = (waves + SMALL_WPB - 1) / SMALL_WPB;
-        if (blocks > (uint64_t)p.max_blocks) blocks = p.max_blocks;
-        hipLaunchKernelGGL((tokenize_kernel<SMALL_CH, SMALL_WPB, false>), dim3((unsigned)blocks), dim3(SMALL_WPB * 64),
-                           wave_lds_bytes<SMALL_CH>() * SMALL_WPB, stream, a, tv);
-        // second pass over the strings whose single word did not fit a 256-byte window
+        if (p.variant == KERNEL_LANE) {
+            uint64_t blocks = (p.n_str + 63) / 64;
+            if (blocks > (uint64_t)p.max_blocks) blocks = p.max_blocks;
+            launch_lane(p, (unsigned)blocks, stream);
+        } else {
+            const unsigned ng = p.variant == KERNEL_ROWS16 ? 4u : 1u;
+            uint64_t blocks = (p.n_str + ng - 1) / ng;
+            if (blocks > (uint64_t)p.max_blocks) blocks = p.max_blocks;
+            if (p.variant == KERNEL_ROWS16) launch_tok<SMALL_CH, 16, SMALL_EXP, false>(a, tv, (unsigned)blocks, stream);
+            else launch_tok<SMALL_CH, 64, SMALL_EXP, false>(a, tv, (unsigned)blocks, stream);
+        }
+        // second pass over the strings whose single word (or expansion) did not fit the small window
         EncodeArgs b = a;
         b.work_list = p.retry_list; b.work_count = p.retry_count;
-        hipLaunchKernelGGL((tokenize_kernel<BIG_CH, BIG_WPB, true>), dim3(256), dim3(BIG_WPB * 64),
-                           wave_lds_bytes<BIG_CH>() * BIG_WPB, stream, b, tv);
+        launch_tok<BIG_CH, 64, BIG_EXP, true>(b, tv, 256, stream);
     }
     if (ev) hipEventRecord(ev[1], stream);
     if (p.n_str > 0) {
@@ -588,16 +824,24 @@ hipError_t launch_histogram(const uint64_t *id_off, const int32_t *status, uint6
 hipError_t kernel_init() {
     static bool done = false;
     if (done) return hipSuccess;
-    hipError_t e = hipFuncSetAttribute((const void *)tokenize_kernel<BIG_CH, BIG_WPB, true>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, wave_lds_bytes<BIG_CH>() * BIG_WPB);
-    if (e != hipSuccess) return e;
-    e = hipFuncSetAttribute((const void *)tokenize_kernel<SMALL_CH, SMALL_WPB, false>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, wave_lds_bytes<SMALL_CH>() * SMALL_WPB);
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&tokenize_kernel<BIG_CH, 64, BIG_EXP, true>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, block_lds_bytes<BIG_CH, 64, BIG_EXP>());
     if (e == hipSuccess) done = true;
     return e;
 }
 
 int small_window_bytes() { return SMALL_CH; }
 int big_window_bytes() { return BIG_CH; }
+
+#ifdef DPT_STAMPS
+extern "C" int dpt_debug_stamps(unsigned long long *out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[8] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
 
 }  // namespace dpt

@@ -9,7 +9,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libdpt.so")
+LIB_PATH = os.environ.get("DPT_LIB") or os.path.join(HERE, "libdpt.so")
 
 DPT_OK = 0
 DPT_MODE_RAW = 0

@@ -1,0 +1,28 @@
+"""Diagnostic: per-phase cycle shares of the tokenize kernel (libdpt_stamps.so build)."""
+import ctypes, os, sys, time
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["DPT_LIB"] = os.path.join(ROOT, "dp-tokenization_amd/csrc/build/libdpt_stamps.so")
+sys.path[:0] = [ROOT, os.path.join(ROOT, "dp-tokenization_amd")]
+import numpy as np
+from dptok import Encoder, Vocab, synth, _lib
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 200000
+L = int(sys.argv[2]) if len(sys.argv) > 2 else 256
+gen = sys.argv[3] if len(sys.argv) > 3 else "ascii"
+enc = Encoder(Vocab(synth.llama_shaped_vocab(), 0))
+if gen == "ascii":
+    text, offs = synth.random_ascii_corpus(n, L, seed=1)
+elif gen == "s2orc":
+    text, offs = synth.s2orc_like_corpus(n, seed=4)
+else:
+    text, offs = synth.arabic_corpus(n, L, seed=5)
+enc.encode_csr(text, offs)
+buf = (ctypes.c_ulonglong * 8)()
+lib = _lib.lib()
+lib.dpt_debug_stamps(buf, 1)
+t0 = time.time(); enc.encode_csr(text, offs); dt = time.time() - t0
+lib.dpt_debug_stamps(buf, 0)
+names = ["prep", "A_match", "B_forward", "C1_select", "C2_ids+win", "tail"]
+tot = sum(buf[k] for k in range(6))
+print(f"{gen} n={n} wall={dt*1e3:.1f} ms (host path incl. copies)")
+for k in range(6):
+    print(f"  {names[k]:12s} {buf[k]/tot*100:6.2f}%  {buf[k]/n:10.0f} cycles/string(wave)")
