@@ -44,6 +44,8 @@ struct dpt_ctx {
     uint64_t *h_off = nullptr, *h_idoff = nullptr;
     int32_t *h_status = nullptr, *h_capped = nullptr;
     uint64_t h_cap_str = 0;
+    uint64_t *h_edges = nullptr;
+    uint64_t h_cap_edges = 0;
     // profiling
     bool profile = false;
     std::vector<hipEvent_t> events;   // groups of 4 per call
@@ -239,7 +241,7 @@ int dpt_ctx_destroy(dpt_ctx *c) {
     if (!c) return DPT_OK;
     DeviceGuard g(c->device);
     void *ps[] = {c->staging, c->rec, c->counts, c->retry_list, c->retry_count, c->scan_temp, c->h_text, c->h_cut,
-                  c->h_ids, c->h_off, c->h_idoff, c->h_status, c->h_capped};
+                  c->h_ids, c->h_off, c->h_idoff, c->h_status, c->h_capped, c->h_edges};
     for (void *p : ps)
         if (p) hipFree(p);
     for (hipEvent_t e : c->events) hipEventDestroy(e);
@@ -253,14 +255,16 @@ int dpt_ctx_reserve(dpt_ctx *c, uint64_t n_bytes, uint64_t n_str) {
     return ensure_workspace(c, n_bytes, n_str);
 }
 
-int dpt_encode(dpt_ctx *c, const dpt_vocab *v, int mode, const uint8_t *text, uint64_t n_bytes,
-               const uint64_t *str_off, const uint8_t *cut_mask, uint64_t n_str, int32_t *ids, uint64_t ids_cap,
-               uint64_t *id_off, int32_t *status, int32_t *capped_len, void *hip_stream) {
+static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uint8_t *text, uint64_t n_bytes,
+                       const uint64_t *str_off, const uint8_t *cut_mask, uint64_t n_str, int32_t *ids, uint64_t ids_cap,
+                       uint64_t *id_off, int32_t *status, int32_t *capped_len, uint64_t *edges, void *hip_stream) {
+    const int mode = mode_flags & DPT_MODE_MASK;
     if (!c || !v) return fail(DPT_E_ARG, "null ctx or vocab");
-    if (mode != DPT_MODE_RAW && mode != DPT_MODE_PRESPLIT) return fail(DPT_E_ARG, "bad mode");
+    if (mode != DPT_MODE_RAW && mode != DPT_MODE_PRESPLIT && mode != DPT_MODE_ATOMS) return fail(DPT_E_ARG, "bad mode");
+    if (mode_flags & ~(DPT_MODE_MASK | DPT_FLAG_UNCAPPED | DPT_FLAG_LEN_ONLY)) return fail(DPT_E_ARG, "bad flags");
     if (!str_off || !id_off || (n_str && !status)) return fail(DPT_E_ARG, "null output/offsets");
     if (n_bytes && (!text || !ids)) return fail(DPT_E_ARG, "null text/ids");
-    if (mode == DPT_MODE_PRESPLIT && n_bytes && !cut_mask) return fail(DPT_E_ARG, "PRESPLIT needs cut_mask");
+    if (mode != DPT_MODE_RAW && n_bytes && !cut_mask) return fail(DPT_E_ARG, "PRESPLIT/ATOMS need cut_mask");
     if (ids_cap < n_bytes) return fail(DPT_E_CAP, "ids_cap must be >= n_bytes");
     if (n_str > 0x7FFFFFFFull) return fail(DPT_E_ARG, "too many strings for one call (max 2^31-1)");
     if (c->device != v->device) return fail(DPT_E_ARG, "ctx and vocab on different devices");
@@ -269,7 +273,8 @@ int dpt_encode(dpt_ctx *c, const dpt_vocab *v, int mode, const uint8_t *text, ui
     if (rc) return rc;
     hipStream_t st = (hipStream_t)hip_stream;
     dpt::EncodeLaunch p;
-    p.mode = mode;
+    p.mode = mode_flags;
+    p.edges = edges;
     p.text = text;
     p.str_off = str_off;
     p.cut_mask = cut_mask;
@@ -287,6 +292,9 @@ int dpt_encode(dpt_ctx *c, const dpt_vocab *v, int mode, const uint8_t *text, ui
     p.max_blocks = c->max_blocks;
     p.rec = c->rec;
     p.variant = kernel_variant(v->stats.max_cp);
+    // the lane kernel implements the plain raw / pre-split encode only
+    if (p.variant == dpt::KERNEL_LANE && (mode_flags != DPT_MODE_RAW && mode_flags != DPT_MODE_PRESPLIT || edges))
+        p.variant = v->stats.max_cp <= 16 ? dpt::KERNEL_ROWS16 : dpt::KERNEL_ROWS64;
     p.slots = v->d_slots;
     p.slot_ids = v->d_ids;
     p.n_slots = v->stats.n_slots;
@@ -308,9 +316,18 @@ int dpt_encode(dpt_ctx *c, const dpt_vocab *v, int mode, const uint8_t *text, ui
     return DPT_OK;
 }
 
-int dpt_encode_host(dpt_ctx *c, const dpt_vocab *v, int mode, const uint8_t *text, uint64_t n_bytes,
-                    const uint64_t *str_off, const uint8_t *cut_mask, uint64_t n_str, int32_t *ids, uint64_t ids_cap,
-                    uint64_t *id_off, int32_t *status, int32_t *capped_len) {
+int dpt_encode(dpt_ctx *c, const dpt_vocab *v, int mode, const uint8_t *text, uint64_t n_bytes,
+               const uint64_t *str_off, const uint8_t *cut_mask, uint64_t n_str, int32_t *ids, uint64_t ids_cap,
+               uint64_t *id_off, int32_t *status, int32_t *capped_len, void *hip_stream) {
+    if (mode & ~DPT_MODE_MASK) return fail(DPT_E_ARG, "flags are for dpt_dp_host");
+    return encode_impl(c, v, mode, text, n_bytes, str_off, cut_mask, n_str, ids, ids_cap, id_off, status, capped_len,
+                       nullptr, hip_stream);
+}
+
+static int encode_host_impl(dpt_ctx *c, const dpt_vocab *v, int mode, const uint8_t *text, uint64_t n_bytes,
+                            const uint64_t *str_off, const uint8_t *cut_mask, uint64_t n_str, int32_t *ids,
+                            uint64_t ids_cap, uint64_t *id_off, int32_t *status, int32_t *capped_len,
+                            uint64_t *edges) {
     if (!c || !v) return fail(DPT_E_ARG, "null ctx or vocab");
     if (!str_off || !id_off || (n_str && !status)) return fail(DPT_E_ARG, "null output/offsets");
     if (n_bytes && (!text || !ids)) return fail(DPT_E_ARG, "null text/ids");
@@ -339,7 +356,7 @@ int dpt_encode_host(dpt_ctx *c, const dpt_vocab *v, int mode, const uint8_t *tex
     hipStream_t st = 0;
     if (n_bytes && (e = hipMemcpyAsync(c->h_text, text, n_bytes, hipMemcpyHostToDevice, st)) != hipSuccess)
         return hip_fail(e, "H2D text");
-    if (mode == DPT_MODE_PRESPLIT && n_bytes &&
+    if ((mode & DPT_MODE_MASK) != DPT_MODE_RAW && n_bytes &&
         (e = hipMemcpyAsync(c->h_cut, cut_mask, n_bytes, hipMemcpyHostToDevice, st)) != hipSuccess)
         return hip_fail(e, "H2D cut");
     // offsets rebased to 0 so that the device view is self-contained
@@ -347,9 +364,19 @@ int dpt_encode_host(dpt_ctx *c, const dpt_vocab *v, int mode, const uint8_t *tex
     for (uint64_t i = 0; i <= n_str; i++) off[i] = str_off[i] - str_off[0];
     if ((e = hipMemcpyAsync(c->h_off, off.data(), (n_str + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st)) != hipSuccess)
         return hip_fail(e, "H2D offsets");
-    int rc = dpt_encode(c, v, mode, c->h_text, n_bytes, c->h_off, c->h_cut, n_str, c->h_ids, c->h_cap_bytes, c->h_idoff,
-                        c->h_status, c->h_capped, st);
+    uint64_t *d_edges = nullptr;
+    if (edges) {
+        uint64_t cap = c->h_cap_edges;
+        if ((e = grow(&c->h_edges, &cap, n_bytes + 1)) != hipSuccess) return hip_fail(e, "hipMalloc(edges)");
+        c->h_cap_edges = cap;
+        d_edges = c->h_edges;
+    }
+    int rc = encode_impl(c, v, mode, c->h_text, n_bytes, c->h_off, c->h_cut, n_str, c->h_ids, c->h_cap_bytes, c->h_idoff,
+                         c->h_status, c->h_capped, d_edges, st);
     if (rc) return rc;
+    if (edges && n_bytes &&
+        (e = hipMemcpyAsync(edges, d_edges, n_bytes * sizeof(uint64_t), hipMemcpyDeviceToHost, st)) != hipSuccess)
+        return hip_fail(e, "D2H edges");
     if ((e = hipMemcpyAsync(id_off, c->h_idoff, (n_str + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, st)) != hipSuccess)
         return hip_fail(e, "D2H id_off");
     if (n_str && (e = hipMemcpyAsync(status, c->h_status, n_str * sizeof(int32_t), hipMemcpyDeviceToHost, st)) != hipSuccess)
@@ -363,6 +390,26 @@ int dpt_encode_host(dpt_ctx *c, const dpt_vocab *v, int mode, const uint8_t *tex
     if (total && (e = hipMemcpy(ids, c->h_ids, total * sizeof(int32_t), hipMemcpyDeviceToHost)) != hipSuccess)
         return hip_fail(e, "D2H ids");
     return DPT_OK;
+}
+
+int dpt_encode_host(dpt_ctx *c, const dpt_vocab *v, int mode, const uint8_t *text, uint64_t n_bytes,
+                    const uint64_t *str_off, const uint8_t *cut_mask, uint64_t n_str, int32_t *ids, uint64_t ids_cap,
+                    uint64_t *id_off, int32_t *status, int32_t *capped_len) {
+    if (mode & ~DPT_MODE_MASK) return fail(DPT_E_ARG, "flags are for dpt_dp_host");
+    return encode_host_impl(c, v, mode, text, n_bytes, str_off, cut_mask, n_str, ids, ids_cap, id_off, status,
+                            capped_len, nullptr);
+}
+
+int dpt_dp_host(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uint8_t *text, uint64_t n_bytes,
+                const uint64_t *str_off, const uint8_t *cut_mask, uint64_t n_str, int32_t *status, int32_t *lengths,
+                uint64_t *edges) {
+    if (!lengths && !edges) return fail(DPT_E_ARG, "nothing to compute");
+    if (!(mode_flags & (DPT_FLAG_UNCAPPED | DPT_FLAG_LEN_ONLY))) mode_flags |= DPT_FLAG_LEN_ONLY;
+    std::vector<uint64_t> id_off(n_str + 1);
+    std::vector<int32_t> len_tmp(lengths ? 0 : n_str + 1);
+    int32_t dummy_ids[1];
+    return encode_host_impl(c, v, mode_flags, text, n_bytes, str_off, cut_mask, n_str, dummy_ids, n_bytes ? n_bytes : 1,
+                            id_off.data(), status, lengths ? lengths : len_tmp.data(), edges);
 }
 
 int dpt_token_histogram(const uint64_t *id_off, const int32_t *status, uint64_t n_str, int64_t *hist, uint32_t n_bins,

@@ -4,10 +4,13 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "../../include/dpt.h"
+
 namespace dpt {
 
 struct EncodeLaunch {
-    int mode;
+    int mode;                // DPT_MODE_* | DPT_FLAG_*
+    uint64_t *edges;         // nullable: per atom end E(i)&reachable masks (n_bytes entries)
     const uint8_t *text;
     const uint64_t *str_off;
     const uint8_t *cut_mask;

@@ -162,7 +162,7 @@ struct SlotState {
     uint64_t s, sb, slen, pos;
     uint32_t active, status, ntok, capsum;
     uint32_t wlen, n_atoms, n_words, wtok;
-    uint32_t inval, pad0, pad1, pad2;
+    uint32_t inval, abase, pad1, pad2;   // abase: atoms of the string's earlier windows
 };
 
 template <int CH, int G, int EXP>
@@ -196,7 +196,8 @@ struct EncodeArgs {
     uint32_t *retry_count;
     const uint32_t *work_list;  // 2048-byte pass: the retry list
     const uint32_t *work_count;
-    int mode;
+    uint64_t *edges;            // nullable: per atom end, the E(i) & reachable back-distance mask
+    int mode;                   // DPT_MODE_* | DPT_FLAG_*
 };
 
 #ifdef DPT_STAMPS
@@ -216,7 +217,7 @@ __device__ unsigned long long g_stamps[8];
 // Finds the window [pos, pos+wlen) (ends at a word start or at the string end).
 // Returns false when a single word does not fit in CH bytes.
 template <int CH>
-__device__ bool window_bounds(const uint8_t *str, const uint8_t *cut, uint64_t slen, uint64_t pos, bool raw,
+__device__ bool window_bounds(const uint8_t *str, const uint8_t *cut, uint64_t slen, uint64_t pos, int mode,
                               unsigned lane, unsigned &wlen) {
     const uint64_t rem = slen - pos;
     if (rem <= (uint64_t)CH) {
@@ -228,7 +229,7 @@ __device__ bool window_bounds(const uint8_t *str, const uint8_t *cut, uint64_t s
         if (k == 0) continue;
         const uint64_t p = pos + k;
         const uint8_t b = str[p];
-        const bool ws = raw ? (b == ' ') : (cut[p] != 0 && (b & 0xC0) != 0x80);
+        const bool ws = mode == 0 ? (b == ' ') : (mode == 1 ? (cut[p] != 0 && (b & 0xC0) != 0x80) : (cut[p] & 1) != 0);
         if (ws) best = k;
     }
     const unsigned q = wave_max_u32((unsigned)(best + 1));
@@ -241,8 +242,9 @@ __device__ bool window_bounds(const uint8_t *str, const uint8_t *cut, uint64_t s
 // does not fit the LDS budget.  Whole wave cooperates.
 template <int CH, int G, int EXP>
 __device__ bool prep_window(GroupLDS<CH, G, EXP> &L, const uint8_t *str, const uint8_t *cut, uint64_t pos,
-                            unsigned wlen, bool raw, unsigned lane, unsigned &n_atoms_o, unsigned &n_words_o) {
+                            unsigned wlen, int mode, unsigned lane, unsigned &n_atoms_o, unsigned &n_words_o) {
     constexpr unsigned EX_BUDGET = GroupLDS<CH, G, EXP>::NE - 8;
+    const bool raw = mode == 0;
     unsigned n_atoms = 0, n_ex = 0, cp_tot = 0, n_words = 0;
     for (unsigned c0 = 0; c0 < wlen; c0 += 256) {
         uint8_t bt[4];
@@ -256,7 +258,9 @@ __device__ bool prep_window(GroupLDS<CH, G, EXP> &L, const uint8_t *str, const u
             const uint64_t p = pos + k;
             const uint8_t b = in ? str[p] : 0;
             const bool first = in && p == 0;
-            const bool cont = in && !first && (b & 0xC0) == 0x80;
+            const uint8_t cm = (in && !raw) ? cut[p] : 0;
+            // mode 2 (ATOMS): atom starts come from the mask (bit 1), word starts from bit 0
+            const bool cont = in && !first && (mode == 2 ? (cm & 3) == 0 : (b & 0xC0) == 0x80);
             const bool as = in && !cont;
             bool wsf;
             unsigned el, cl;
@@ -265,9 +269,9 @@ __device__ bool prep_window(GroupLDS<CH, G, EXP> &L, const uint8_t *str, const u
                 el = !in ? 0 : first ? 4 : (b == ' ' ? 3 : (b == '\n' ? 6 : 1));
                 cl = !in ? 0 : first ? 2 : (b == '\n' ? 6 : (cont ? 0 : 1));
             } else {
-                wsf = as && (k == 0 || cut[p] != 0);
+                wsf = as && (k == 0 || (mode == 1 ? cm != 0 : (cm & 1) != 0));
                 el = in ? 1 : 0;
-                cl = as ? 1 : 0;
+                cl = (in && (b & 0xC0) != 0x80) ? 1 : 0;   // code points, whatever the atoms
             }
             bt[u] = b; cpl[u] = cl; ast[u] = as; wst[u] = wsf;
             ex_sum += el; cp_sum += cl; a_sum += as; w_sum += wsf;
@@ -292,8 +296,9 @@ __device__ bool prep_window(GroupLDS<CH, G, EXP> &L, const uint8_t *str, const u
         if (kn < wlen) {
             const uint64_t p = pos + kn;
             const uint8_t b = str[p];
-            const bool as = (b & 0xC0) != 0x80;
-            const bool wsf = as && (raw ? b == ' ' : cut[p] != 0);
+            const uint8_t cm = raw ? 0 : cut[p];
+            const bool as = mode == 2 ? (cm & 3) != 0 : (b & 0xC0) != 0x80;
+            const bool wsf = as && (raw ? b == ' ' : (mode == 1 ? cm != 0 : (cm & 1) != 0));
             chunk_next = (as ? 1u : 0u) | (wsf ? 2u : 0u);
         }
 #pragma unroll
@@ -363,7 +368,10 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
     const unsigned d = lane % G;         // my back distance - 1
     const uint64_t n_work = BIG ? (uint64_t)(*a.work_count) : a.n_str;
     const uint64_t base_off = a.str_off[0];
-    const bool raw = a.mode == 0;
+    const int mode = a.mode & DPT_MODE_MASK;
+    const bool raw = mode == 0;
+    const bool uncapped = (a.mode & DPT_FLAG_UNCAPPED) != 0;   // f2: inspect_tokenizer's inf-initialised DP
+    const bool len_only = (a.mode & (DPT_FLAG_UNCAPPED | DPT_FLAG_LEN_ONLY)) != 0;
     uint64_t next = blockIdx.x;          // one wave per block
     const uint64_t stride = gridDim.x;
     STAMP_DECL
@@ -387,7 +395,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                     if (lane == 0) {
                         S.s = s; S.sb = sb; S.slen = sl; S.pos = 0; S.active = 1;
                         S.status = sl == 0 ? 2u : 0u;  // pretokenize_raw('') == [[]] -> IndexError
-                        S.ntok = 0; S.capsum = 0;
+                        S.ntok = 0; S.capsum = 0; S.abase = 0;
                     }
                     wave_sync();
                 }
@@ -397,8 +405,8 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 const uint8_t *cut = raw ? nullptr : a.cut_mask + sb;
                 unsigned wlen = 0, na = 0, nw = 0;
                 bool ok = status != 2;
-                if (ok) ok = window_bounds<CH>(str, cut, slen, pos, raw, lane, wlen);
-                if (ok) ok = prep_window<CH, G, EXP>(L, str, cut, pos, wlen, raw, lane, na, nw);
+                if (ok) ok = window_bounds<CH>(str, cut, slen, pos, mode, lane, wlen);
+                if (ok) ok = prep_window<CH, G, EXP>(L, str, cut, pos, wlen, mode, lane, na, nw);
                 if (ok) {
                     if (lane == 0) { S.wlen = wlen; S.n_atoms = na; S.n_words = nw; }
                     busy++;
@@ -515,11 +523,13 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                     const unsigned kv = (st | 0x7FFFu) - (gj > span ? gj : span);
                     const unsigned key = ((m >> d) & 1u) ? kv : 0xFFFFFFFFu;
                     unsigned r = row_min_u32(key);
-                    const unsigned capkey = ((i - ws) << 16) | 0xFFFFu;
+                    const unsigned capkey = uncapped ? 0xFFFFFFFFu : (((i - ws) << 16) | 0xFFFFu);
                     r = r < capkey ? r : capkey;
                     const uint64_t gmb = ballot(key == r);
                     const uint64_t emb = ballot((key ^ r) < 0x8000u);
                     const bool live = i <= na;
+                    if (a.edges && d == 0 && live)
+                        a.edges[SS[mg].sb + SS[mg].abase + i - 1] = (unsigned)(emb >> (16u * mg)) & 0xFFFFu;
                     const bool wend = live && (cur & CP_WS);  // CP_WS marks word starts and the window end
                     const bool boundary = wend && i < na;
                     if (d == 0 && live) {
@@ -531,7 +541,8 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                     winv |= wend ? (r & 0x8000u) : 0u;
                     w += boundary ? 1u : 0u;
                     ws = boundary ? i : ws;
-                    const unsigned sin = boundary ? ST0 : ((r ^ 0x7FFFu) + 0x10000u);
+                    // (uncapped DP: an unreachable position saturates at cost 0xFFFF = inf)
+                    const unsigned sin = boundary ? ST0 : (r >= 0xFFFE0000u ? 0xFFFF8000u : ((r ^ 0x7FFFu) + 0x10000u));
                     st = row_shift_in(st, sin);
                     cpj = row_shift_in(cpj, cpi);
                     m = row_shift_in(m, cur >> 16);
@@ -551,10 +562,11 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                     const unsigned bit = (d < 32 ? (mlo >> d) : (mhi >> (d - 32))) & 1u;
                     const unsigned key = bit ? kv : 0xFFFFFFFFu;
                     unsigned r = wave_min_u32(key);
-                    const unsigned capkey = ((i - ws) << 16) | 0xFFFFu;
+                    const unsigned capkey = uncapped ? 0xFFFFFFFFu : (((i - ws) << 16) | 0xFFFFu);
                     r = r < capkey ? r : capkey;
                     const uint64_t gmb = ballot(key == r);
                     const uint64_t emb = ballot((key ^ r) < 0x8000u);
+                    if (a.edges && lane == 0) a.edges[SS[0].sb + SS[0].abase + i - 1] = emb;
                     const bool wend = (cur & CP_WS) != 0;
                     const bool boundary = wend && i < na;
                     if (lane == 0) {
@@ -566,7 +578,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                     winv |= wend ? (r & 0x8000u) : 0u;
                     w += boundary ? 1u : 0u;
                     ws = boundary ? i : ws;
-                    const unsigned sin = boundary ? ST0 : ((r ^ 0x7FFFu) + 0x10000u);
+                    const unsigned sin = boundary ? ST0 : (r >= 0xFFFE0000u ? 0xFFFF8000u : ((r ^ 0x7FFFu) + 0x10000u));
                     st = wave_shift_in(st, sin);
                     cpj = wave_shift_in(cpj, cpi);
                     mlo = wave_shift_in(mlo, (unsigned)mi);
@@ -613,7 +625,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 const unsigned incl = wave_incl_scan_add(cost);
                 const unsigned tok_base = carry + incl - cost - tbase;
                 carry += __builtin_amdgcn_readlane(incl, 63);
-                if (in && !ginv) {
+                if (in && !ginv && !len_only) {
                     const unsigned ws = L.wsl[w];
                     unsigned i = L.wsl[w + 1];
                     const unsigned Ls = 0x7FFFu - (F & 0x7FFFu);   // G of the word = the longest token to reach
@@ -646,7 +658,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
             pre[0] = 0;
 #pragma unroll
             for (int g = 0; g < NG; g++) {
-                const bool gv = uni(SS[g].inval) == 0 && uni(SS[g].status) == 0 && uni(SS[g].n_atoms) > 0;
+                const bool gv = !len_only && uni(SS[g].inval) == 0 && uni(SS[g].status) == 0 && uni(SS[g].n_atoms) > 0;
                 pre[g + 1] = pre[g] + (gv ? uni(SS[g].wtok) : 0u);
                 na_g[g] = uni(SS[g].n_atoms);
             }
@@ -687,8 +699,9 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
             SlotState &S = SS[lane];
             if (S.active && S.n_atoms > 0) {
                 if (S.inval && S.status == 0) S.status = 1;
-                if (S.status == 0) S.ntok += S.wtok;
+                if (S.status == 0 && !len_only) S.ntok += S.wtok;
                 S.pos += S.wlen;
+                S.abase += S.n_atoms;
                 if (S.pos >= S.slen) {
                     const uint64_t s = S.s;
                     a.status[s] = (int32_t)S.status;
@@ -768,6 +781,7 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     a.staging = p.staging; a.counts = p.counts; a.status = p.status; a.capped = p.capped;
     a.retry_list = p.retry_list; a.retry_count = p.retry_count; a.work_list = nullptr; a.work_count = nullptr;
     a.mode = p.mode;
+    a.edges = p.edges;
     TrieView tv{p.slots, p.slot_ids, p.root_base};
 
     hipLaunchKernelGGL(zero_first, dim3(1), dim3(64), 0, stream, p.id_off, p.retry_count);

@@ -13,10 +13,33 @@ from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import _lib
-from ._lib import DPT_MODE_PRESPLIT, DPT_MODE_RAW, DptError, check
+from ._lib import (DPT_FLAG_LEN_ONLY, DPT_FLAG_UNCAPPED, DPT_MODE_ATOMS, DPT_MODE_PRESPLIT, DPT_MODE_RAW, DptError,
+                   check)
 
-MODES = {"raw": DPT_MODE_RAW, "presplit": DPT_MODE_PRESPLIT, DPT_MODE_RAW: DPT_MODE_RAW,
-         DPT_MODE_PRESPLIT: DPT_MODE_PRESPLIT}
+MODES = {"raw": DPT_MODE_RAW, "presplit": DPT_MODE_PRESPLIT, "atoms": DPT_MODE_ATOMS, DPT_MODE_RAW: DPT_MODE_RAW,
+         DPT_MODE_PRESPLIT: DPT_MODE_PRESPLIT, DPT_MODE_ATOMS: DPT_MODE_ATOMS}
+
+
+def atoms_to_csr(atom_lists: Sequence[Sequence[str]]):
+    """Lists of atom strings -> (text, offsets, cut mask) for DPT_MODE_ATOMS (one word per list:
+    bit 1 marks every atom start, bit 0 the first).  Empty atoms are not representable."""
+    parts, cuts = [], []
+    for atoms in atom_lists:
+        for k, a in enumerate(atoms):
+            e = encode_utf8(a)
+            if not e:
+                raise ValueError("empty atom")
+            parts.append(e)
+            c = bytearray(len(e))
+            c[0] = 3 if k == 0 else 2
+            cuts.append(bytes(c))
+    lens = [sum(len(encode_utf8(a)) for a in atoms) for atoms in atom_lists]
+    offs = np.zeros(len(atom_lists) + 1, dtype=np.uint64)
+    if lens:
+        offs[1:] = np.cumsum(lens, dtype=np.uint64)
+    text = np.frombuffer(b"".join(parts) + b"\0", dtype=np.uint8)
+    cut = np.frombuffer(b"".join(cuts) + b"\0", dtype=np.uint8)
+    return text, offs, cut
 
 
 def _ptr(a: Optional[np.ndarray]):
@@ -107,9 +130,9 @@ class Encoder:
         status = np.empty(max(n, 1), dtype=np.int32)
         capped = np.empty(max(n, 1), dtype=np.int32)
         m = MODES[mode]
-        if m == DPT_MODE_PRESPLIT:
+        if m != DPT_MODE_RAW:
             if cut_mask is None:
-                raise ValueError("presplit mode needs cut_mask")
+                raise ValueError("presplit/atoms mode needs cut_mask")
             cut_mask = np.ascontiguousarray(cut_mask, dtype=np.uint8)
         base = int(offs[0])
         tv = text[base:] if base else text
@@ -139,6 +162,27 @@ class Encoder:
         offs = np.array([0, len(raw)], dtype=np.uint64)
         ids, id_off, st, _ = self.encode_csr(text, offs, mode="presplit", cut_mask=cut)
         return ids.tolist(), int(st[0])
+
+    def dp(self, text: np.ndarray, offs: np.ndarray, mode="atoms", cut_mask: Optional[np.ndarray] = None,
+           uncapped: bool = False, edges: bool = False):
+        """DP by-products without ids (dpt_dp_host): (status, lengths, edges or None).  lengths are
+        the capped len_dp[-1] sums (reference dp_tokenize.py:70) or, with ``uncapped``, the minimum
+        token counts (65535 per impossible word, inspect_tokenizer.py:77-86)."""
+        text = np.ascontiguousarray(text, dtype=np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        if len(offs) and int(offs[0]) != 0:
+            raise ValueError("dp(): offsets must start at 0")
+        n = len(offs) - 1
+        n_bytes = int(offs[-1] - offs[0])
+        status = np.empty(max(n, 1), dtype=np.int32)
+        lengths = np.empty(max(n, 1), dtype=np.int32)
+        ed = np.zeros(max(n_bytes, 1), dtype=np.uint64) if edges else None
+        m = MODES[mode] | (DPT_FLAG_UNCAPPED if uncapped else DPT_FLAG_LEN_ONLY)
+        if cut_mask is not None:
+            cut_mask = np.ascontiguousarray(cut_mask, dtype=np.uint8)
+        check(_lib.lib().dpt_dp_host(self.handle, self.vocab.handle, m, _ptr(text), n_bytes, _ptr(offs), _ptr(cut_mask),
+                                     n, _ptr(status), _ptr(lengths), _ptr(ed)), "dpt_dp_host")
+        return status[:n], lengths[:n], ed
 
     # ---------------------------------------------------------------- device buffers
     def encode_device(self, text_ptr: int, n_bytes: int, off_ptr: int, n_str: int, ids_ptr: int, ids_cap: int,

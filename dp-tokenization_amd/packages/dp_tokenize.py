@@ -1,0 +1,102 @@
+"""Drop-in for the reference's ``packages/dp_tokenize.py`` (L1 DP core), GPU-backed.
+
+* ``compute_shortest_tokenizations(base_representation_s, vocabulary,
+  disregard_word_initial_marker, word_initial_marker) -> (List[List[str]], int)``
+  (reference dp_tokenize.py:6-70): the forward DP runs on the GPU over the caller's
+  atoms (DPT_MODE_ATOMS) and returns, per atom end i, the reachable part of the
+  optimal-predecessor set ``segment_index_dp[i-1]``; the host then lists every shortest
+  tokenization in the reference's DFS order (largest predecessor popped first, a subtree
+  finished before its siblings, dp_tokenize.py:49-69).  Dead ends (unreachable
+  predecessors, which the reference explores and drops) are never entered, so the list
+  and its order are the reference's.  The second value is ``len_dp[-1]`` (capped DP).
+  Raises IndexError on an empty input like the reference (dp_tokenize.py:49).
+* ``obtain_longest_token(tokenizations)`` (dp_tokenize.py:72-84): the first tokenization
+  whose longest token (code points) is longest; ValueError on an empty list.
+
+The enumeration is exponential in the worst case (SURVEY.md §0 finding 4) -- for the
+tokenizer use case call ``dp_tokenize`` (packages.tokenizer_utils), which selects the
+same tokenization on the GPU without enumerating.
+"""
+from __future__ import annotations
+
+import os
+import sys
+from collections import OrderedDict
+from typing import List, Sequence
+
+_HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if _HERE not in sys.path:
+    sys.path.insert(0, _HERE)
+
+from dptok import DptError, Encoder, Vocab  # noqa: E402
+from dptok.engine import atoms_to_csr  # noqa: E402
+
+_CACHE: "OrderedDict[frozenset, Encoder]" = OrderedDict()
+
+
+def _engine_for(vocabulary) -> Encoder:
+    key = frozenset(vocabulary)
+    enc = _CACHE.get(key)
+    if enc is None:
+        t2i = {tok: i for i, tok in enumerate(sorted(key))}
+        enc = Encoder(Vocab(t2i, int(os.environ.get("LOCAL_RANK", "0"))))
+        _CACHE[key] = enc
+        if len(_CACHE) > 4:
+            _CACHE.popitem(last=False)
+    else:
+        _CACHE.move_to_end(key)
+    return enc
+
+
+def _dp_edges(atoms: Sequence[str], vocabulary, uncapped: bool = False):
+    """GPU DP over one atom list: (status, length, per-end reachable-predecessor masks)."""
+    enc = _engine_for(vocabulary)
+    text, offs, cut = atoms_to_csr([atoms])
+    status, lengths, edges = enc.dp(text, offs, mode="atoms", cut_mask=cut, uncapped=uncapped, edges=True)
+    # edges are indexed by the byte offset of the string + atom end - 1; one string at offset 0
+    return int(status[0]), int(lengths[0]), edges
+
+
+def compute_shortest_tokenizations(base_representation_s, vocabulary, disregard_word_initial_marker,
+                                   word_initial_marker):
+    if disregard_word_initial_marker:
+        # dp_tokenize.py:24-25 (str.lstrip strips any leading characters of the marker string)
+        vocabulary = {token.lstrip(word_initial_marker) for token in vocabulary}
+    atoms = list(base_representation_s)
+    n = len(atoms)
+    if n == 0:
+        raise IndexError("list index out of range")
+    vocab = {t for t in vocabulary if t}
+    status, length, edges = _dp_edges(atoms, vocab)
+    if status == 3:
+        raise DptError("input longer than the engine's 2048-byte window")
+    if status not in (0, 1):
+        raise DptError("engine status %d" % status)
+    if status == 1:
+        return [], length
+    # preds[i]: reachable optimal predecessors of end i, ascending (= segment_index_dp[i-1] order)
+    def preds(i: int) -> List[int]:
+        m = int(edges[i - 1])
+        out = []
+        while m:
+            d = (m & -m).bit_length() - 1
+            out.append(i - 1 - d)
+            m &= m - 1
+        return sorted(out)
+
+    stack = [(j, n, []) for j in preds(n)]
+    done: List[List[str]] = []
+    while stack:
+        j, i, partial = stack.pop()
+        toks = ["".join(atoms[j:i])] + partial
+        if j == 0:
+            done.append(toks)
+        else:
+            for jj in preds(j):
+                stack.append((jj, j, list(toks)))
+    return done, length
+
+
+def obtain_longest_token(tokenizations: List[List[str]]) -> List[str]:
+    tokenization_lengths = [max([len(t) for t in tokenization]) for tokenization in tokenizations]
+    return tokenizations[tokenization_lengths.index(max(tokenization_lengths))]

@@ -1,0 +1,143 @@
+"""Drop-in for the reference's ``packages/tokenizer_utils.py`` (L2 adapters) backed by the
+MI355X engine.  Same names, argument meaning and error behaviour:
+
+* ``dp_tokenize_llama(llama_tokenizer, pretokenize_option='llama')`` -> ``(dp_tokenize,
+  decode_dp_tokenization)`` (reference :52-96).  ``dp_tokenize(str) -> List[int]`` runs the
+  per-word shortest-tokenization DP + longest-token selection on the GPU:
+  - ``'raw'``: the pre-tokenizer runs inside the kernel (pretokenize_raw semantics, :33-50);
+  - ``'llama'``: SentencePiece pieces from ``llama_tokenizer.encode`` are merged into words on
+    the host (pretokenize_with_llama + merge_tokens, :7-31) and the GPU runs in pre-split mode.
+  The DP call is the evident-intent 4-argument call; the shipped 5-argument call at :71 raises
+  TypeError (SURVEY.md §0 finding 3), which this drop-in does not reproduce.
+  Failures re-raise the reference's exceptions: a word with no tokenization -> ValueError
+  (reference: ipdb.set_trace then max([]) at dp_tokenize.py:84), an empty word -> IndexError
+  (dp_tokenize.py:49).  An unknown ``pretokenize_option`` fails at call time with NameError,
+  like the reference's unbound ``pretokenize_func``.
+* ``dp_tokenize.batch(List[str]) -> List[List[int]]``: the batched form (one GPU launch).
+* ``merge_tokens``, ``pretokenize_with_llama``, ``pretokenize_raw``: the reference's host-side
+  string utilities with identical behaviour (pre-tokenization, not the DP).
+"""
+from __future__ import annotations
+
+import os
+import sys
+from typing import Dict, List, Sequence
+
+_HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if _HERE not in sys.path:
+    sys.path.insert(0, _HERE)
+
+from dptok import Encoder, Vocab, raise_for_status  # noqa: E402
+
+SPACE_TOKEN = "▁"
+
+
+class _InverseDict(dict):
+    """Minimal stand-in for ``bidict`` (reference uses ``.inverse``)."""
+
+    @property
+    def inverse(self):
+        return {v: k for k, v in self.items()}
+
+
+def merge_tokens(tokens, sep="Ġ"):
+    """Join runs of pieces that do not start with ``sep`` (reference tokenizer_utils.py:7-22)."""
+    merged_tokens = []
+    i = 0
+    n = len(tokens)
+    while i < n:
+        cur = tokens[i]
+        while i + 1 < n and not tokens[i + 1].startswith(sep):
+            cur = cur + tokens[i + 1]
+            i += 1
+        merged_tokens.append(cur)
+        i += 1
+    return merged_tokens
+
+
+def pretokenize_with_llama(tokenizer, vocab_bidict):
+    """SentencePiece pieces merged into words (reference tokenizer_utils.py:24-31)."""
+    inverse = vocab_bidict.inverse
+
+    def pretokenize(input_str):
+        pieces = [inverse[t] for t in tokenizer.encode(input_str)]
+        return merge_tokens(pieces, sep=SPACE_TOKEN)
+
+    return pretokenize
+
+
+def pretokenize_raw(manual_mapping) -> callable:
+    """Raw character pre-tokenizer (reference tokenizer_utils.py:33-50): first char gets the
+    '▁' prefix, ' ' opens a word as '▁', characters in ``manual_mapping.inverse`` are replaced
+    (``'\\n' -> '<0x0A>'``).  The GPU engine applies the same rules in-kernel."""
+    inverse = manual_mapping.inverse
+
+    def pretokenize(input_str):
+        atoms = list(input_str)
+        words = []
+        start = 0
+        for i, ch in enumerate(atoms):
+            if i == 0:
+                atoms[i] = SPACE_TOKEN + ch
+            elif ch == " ":
+                atoms[i] = SPACE_TOKEN
+                words.append(atoms[start:i])
+                start = i
+            elif ch in inverse:
+                atoms[i] = inverse[ch]
+        words.append(atoms[start:])
+        return words
+
+    return pretokenize
+
+
+def _device() -> int:
+    return int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def dp_tokenize_llama(llama_tokenizer, pretokenize_option="llama"):
+    t2i: Dict[str, int] = dict(llama_tokenizer.get_vocab())
+    vocab_bidict = _InverseDict(t2i)
+    engine = Encoder(Vocab(t2i, _device()))
+    manual_mapping = _InverseDict({"<0x0A>": "\n"})
+    if manual_mapping.inverse != {"\n": "<0x0A>"}:  # the raw kernel hard-codes this mapping
+        raise AssertionError("unexpected manual mapping")
+
+    if pretokenize_option == "raw":
+        def encode_many(texts: Sequence[str]) -> List[List[int]]:
+            out = []
+            for t, (ids, st) in zip(texts, engine.encode_strs(list(texts))):
+                raise_for_status(st, t)
+                out.append(ids)
+            return out
+    elif pretokenize_option == "llama":
+        pretokenize = pretokenize_with_llama(llama_tokenizer, vocab_bidict)
+
+        def encode_many(texts: Sequence[str]) -> List[List[int]]:
+            out = []
+            for t in texts:
+                ids, st = engine.encode_words(pretokenize(t))
+                raise_for_status(st, t)
+                out.append(ids)
+            return out
+    else:
+        def encode_many(texts):
+            raise NameError("name 'pretokenize_func' is not defined")
+
+    def dp_tokenize(input_str) -> List[int]:
+        return encode_many([input_str])[0]
+
+    def decode_dp_tokenization(encoding: List[int]):
+        # reference tokenizer_utils.py:82-84: drop the 4-character "<s> " prefix
+        return llama_tokenizer.decode(encoding)[4:]
+
+    dp_tokenize.batch = encode_many
+    dp_tokenize.engine = engine
+    return dp_tokenize, decode_dp_tokenization
+
+
+def dp_tokenize_bloom(bloom_tokenizer, HF_CACHE_DIR):
+    """BLOOM byte-level adapter (reference tokenizer_utils.py:98-181): SURVEY.md §8f row f3,
+    not part of this round's hot path."""
+    raise NotImplementedError("dp_tokenize_bloom: BLOOM byte-level path is row f3 (next); "
+                              "use dp_tokenize_llama or dptok.Encoder with a t2i vocabulary")

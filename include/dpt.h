@@ -46,9 +46,15 @@ extern "C" {
 #define DPT_E_CAP (-4)      /* output capacity too small */
 #define DPT_E_NODEV (-5)    /* no HIP device */
 
-/* modes */
+/* modes (low 4 bits) */
 #define DPT_MODE_RAW 0      /* pretokenize_raw semantics (tokenizer_utils.py:33-50) */
-#define DPT_MODE_PRESPLIT 1 /* words given by cut_mask; atoms = code points (llama mode) */
+#define DPT_MODE_PRESPLIT 1 /* words start where cut_mask != 0; atoms = code points (llama mode) */
+#define DPT_MODE_ATOMS 2    /* caller-defined atoms: cut_mask bit 1 = an atom starts, bit 0 = a word
+                               starts (compute_shortest_tokenizations over an arbitrary atom list) */
+#define DPT_MODE_MASK 0x0F
+/* flags (dpt_dp_host only) */
+#define DPT_FLAG_UNCAPPED 0x10 /* inf-initialised DP (inspect_tokenizer.py:77-86): lengths only */
+#define DPT_FLAG_LEN_ONLY 0x20 /* capped DP lengths (dp_tokenize.py:70 len_dp[-1]), no ids */
 
 /* per-string status (the reference's exceptions) */
 #define DPT_STATUS_OK 0
@@ -110,6 +116,20 @@ int dpt_encode(dpt_ctx *c, const dpt_vocab *v, int mode, const uint8_t *text, ui
 int dpt_encode_host(dpt_ctx *c, const dpt_vocab *v, int mode, const uint8_t *text, uint64_t n_bytes,
                     const uint64_t *str_off, const uint8_t *cut_mask, uint64_t n_str, int32_t *ids,
                     uint64_t ids_cap, uint64_t *id_off, int32_t *status, int32_t *capped_len);
+
+/*
+ * DP by-products without ids (HOST pointers; synchronises).  mode_flags = DPT_MODE_* |
+ * DPT_FLAG_LEN_ONLY (capped len_dp[-1] per string, summed over words) or DPT_FLAG_UNCAPPED
+ * (minimum token count, 65535 per word that has no tokenization).  status[s] as dpt_encode.
+ * edges (nullable, n_bytes entries): for string s and atom end i (1-based atom index within
+ * the string) edges[str_off[s]-str_off[0] + i - 1] has bit d set iff atom i-1-d .. i-1 is a
+ * token, cost[i-1-d] + 1 == cost[i] and i-1-d is reachable -- the reference's
+ * segment_index_dp[i-1] restricted to reachable starts (dp_tokenize.py:40-46), from which the
+ * host enumerates every shortest tokenization in the reference's DFS order.
+ */
+int dpt_dp_host(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uint8_t *text, uint64_t n_bytes,
+                const uint64_t *str_off, const uint8_t *cut_mask, uint64_t n_str, int32_t *status,
+                int32_t *lengths, uint64_t *edges);
 
 /*
  * Token-count histogram (device pointers): hist[0..n_bins) counts strings by

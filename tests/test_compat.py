@@ -1,0 +1,154 @@
+"""The reference-compatible surface (dp-tokenization_amd/packages, inspect_tokenizer.py) against
+fixtures produced by the reference itself (tests/golden/make_golden.py).
+
+CPU tests cover the host-side string utilities; ``gpu`` tests cover every DP-backed name."""
+import math
+
+import numpy as np
+import pytest
+
+from conftest import load_golden
+
+
+@pytest.fixture(scope="module")
+def compat():
+    return load_golden("compat_cases.json.gz")
+
+
+# ------------------------------------------------------------------ host utilities (CPU)
+
+def test_merge_tokens_matches_reference(compat):
+    from packages.tokenizer_utils import merge_tokens
+    for c in compat["merge_tokens"]:
+        assert merge_tokens(c["tokens"], sep=c["sep"]) == c["out"], c
+
+
+def test_pretokenize_raw_matches_reference(compat):
+    from packages.tokenizer_utils import _InverseDict, pretokenize_raw
+    pre = pretokenize_raw(_InverseDict({"<0x0A>": "\n"}))
+    for c in compat["pretokenize_raw"]:
+        assert pre(c["text"]) == c["out"], c["text"]
+
+
+def test_pretokenize_with_llama_matches_reference(compat):
+    from dptok import synth
+    from fake_llama import FakeLlamaTokenizer
+    from packages.tokenizer_utils import _InverseDict, pretokenize_with_llama
+    t2i = synth.llama_shaped_vocab()
+    pre = pretokenize_with_llama(FakeLlamaTokenizer(t2i), _InverseDict(t2i))
+    for c in compat["llama_mode"]:
+        assert pre(c["text"]) == c["words"], c["text"]
+
+
+def test_obtain_longest_token_semantics():
+    from packages.dp_tokenize import obtain_longest_token
+    assert obtain_longest_token([["ab", "c"], ["a", "bc"], ["abc"]]) == ["abc"]
+    assert obtain_longest_token([["ab", "c"], ["a", "bc"]]) == ["ab", "c"]   # first argmax
+    with pytest.raises(ValueError):
+        obtain_longest_token([])
+
+
+def test_inspect_obtain_token_compositions():
+    import inspect_tokenizer as it
+    vocab = {"a": 0, "b": 1, "c": 2, "ab": 3, "bc": 4, "abc": 5}
+    merges = ["a b", "b c", "ab c"]
+    assert it.obtain_token_compositions("abc", vocab, merges) == [["ab", "c"], ["a", "b", "c"]]
+    assert it.obtain_token_compositions("a", vocab, merges) == [["a"]]
+
+
+# ------------------------------------------------------------------ DP-backed names (GPU)
+
+@pytest.mark.gpu
+def test_dp_tokenize_llama_raw_mode(vocabs):
+    from fake_llama import FakeLlamaTokenizer
+    from packages.tokenizer_utils import dp_tokenize_llama
+    g = load_golden("cfg2_llama32k.json.gz")
+    dp_tokenize, decode = dp_tokenize_llama(FakeLlamaTokenizer(vocabs["llama32k"]), "raw")
+    for c in g["cases"][:100]:
+        assert dp_tokenize(c["text"]) == c["ids"]
+    assert dp_tokenize.batch([c["text"] for c in g["cases"]]) == [c["ids"] for c in g["cases"]]
+    e = load_golden("edge_llama32k.json.gz")
+    for c in e["cases"]:
+        if c["status"] == 0:
+            assert dp_tokenize(c["text"]) == c["ids"]
+        else:
+            with pytest.raises(ValueError if c["status"] == 1 else IndexError):
+                dp_tokenize(c["text"])
+
+
+@pytest.mark.gpu
+def test_dp_tokenize_llama_llama_mode(vocabs, compat):
+    from fake_llama import FakeLlamaTokenizer
+    from packages.tokenizer_utils import dp_tokenize_llama
+    dp_tokenize, decode = dp_tokenize_llama(FakeLlamaTokenizer(vocabs["llama32k"]))   # default 'llama'
+    for c in compat["llama_mode"]:
+        if c["status"] == 0:
+            ids = dp_tokenize(c["text"])
+            assert ids == c["ids"], c["text"]
+            assert isinstance(decode(ids), str)   # tokenizer.decode(ids)[4:] (fake decode, not Llama's)
+        else:
+            with pytest.raises((ValueError, IndexError)):
+                dp_tokenize(c["text"])
+
+
+@pytest.mark.gpu
+def test_unknown_pretokenize_option_fails_at_call_time(vocabs):
+    from fake_llama import FakeLlamaTokenizer
+    from packages.tokenizer_utils import dp_tokenize_llama
+    dp_tokenize, _ = dp_tokenize_llama(FakeLlamaTokenizer(vocabs["llama32k"]), "bogus")
+    with pytest.raises(NameError):
+        dp_tokenize("abc")
+
+
+@pytest.mark.gpu
+def test_compute_shortest_tokenizations_enumeration_order():
+    """Every optimal tokenization, in the reference's DFS order, for 2000 tie-heavy words."""
+    from packages.dp_tokenize import compute_shortest_tokenizations, obtain_longest_token
+    g = load_golden("small_random.json.gz")
+    n = 0
+    for c in g["cases"]:
+        for w in c["words"]:
+            toks, length = compute_shortest_tokenizations(w["atoms"], set(c["vocab"]), False, None)
+            assert toks == w["tokenizations"], (w["atoms"], c["vocab"])
+            assert length == w["len"]
+            if toks:
+                obtain_longest_token(toks)
+            n += 1
+    assert n > 1000
+    with pytest.raises(IndexError):
+        compute_shortest_tokenizations([], {"a"}, False, None)
+
+
+@pytest.mark.gpu
+def test_reference_kats_through_drop_in():
+    import inspect_tokenizer as it
+    from packages.dp_tokenize import compute_shortest_tokenizations, obtain_longest_token
+    k = load_golden("reference_kats.json")
+    for t in k["lengths"]:
+        assert it.min_tokens_for_string(t["text"], set(t["vocab"])) == t["expected"]
+        toks, n = compute_shortest_tokenizations(list(t["text"]), set(t["vocab"]), False, None)
+        assert toks == t["ref_tokenizations"] and n == t["ref_capped_len"]
+    for t in k["membership"]:
+        toks, n = compute_shortest_tokenizations(t["text"], t["vocab"], False, "")
+        assert toks == t["ref_tokenizations"] and n == t["ref_len"]
+        for m in t["must_contain"]:
+            assert m in toks
+        assert obtain_longest_token(toks) == t["ref_selected"]
+
+
+@pytest.mark.gpu
+def test_inspect_min_tokens_uncapped(compat):
+    import inspect_tokenizer as it
+    for c in compat["inspect_min_tokens"]:
+        got = it.min_tokens_for_string(c["text"], set(c["vocab"]))
+        want = math.inf if c["min"] == "inf" else c["min"]
+        assert got == want, c
+        assert it.compute_length_of_most_efficient_tokenization(list(c["text"]), set(c["vocab"])) == want
+
+
+@pytest.mark.gpu
+def test_disregard_word_initial_marker():
+    from packages.dp_tokenize import compute_shortest_tokenizations
+    V = {"##ab", "##c", "a", "b"}
+    toks, n = compute_shortest_tokenizations(list("abc"), V, True, "##")
+    assert n == 2 and toks == [["ab", "c"]]
