@@ -105,6 +105,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     from dptok import Encoder, Vocab, synth
+    from dptok import dist as ddist
     t2i = synth.llama_shaped_vocab()
     M, Lb = args.strings, args.length
     text, offs = synth.random_ascii_corpus(M, Lb, seed=args.seed, start=rank * M)
@@ -118,12 +119,8 @@ def main():
                "sample": f"{nd} of the first {args.cpu_sample} cfg2 strings in {cdt:.1f}s "
                          f"(enumerate-then-select, oracle/ref_port.py; {nto} hit the 10s per-string limit)"}
 
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
+    ddist.init_from_env("nccl")
+    torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     vocab = Vocab(t2i, device=local)
     enc = Encoder(vocab)
@@ -142,8 +139,7 @@ def main():
                           d_idoff.data_ptr(), d_status.data_ptr(), stream=stream)
         d_hist.zero_()
         enc.histogram_device(d_idoff.data_ptr(), d_status.data_ptr(), M, d_hist.data_ptr(), N_BINS, stream=stream)
-        if world > 1:
-            dist.all_reduce(d_hist)       # the single RCCL collective
+        ddist.allreduce_histogram(d_hist)  # the single RCCL collective; no-op at N=1
 
     for _ in range(args.warmup):
         step()
