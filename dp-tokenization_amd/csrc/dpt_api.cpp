@@ -132,6 +132,7 @@ int kernel_variant(uint32_t max_cp) {
         if (!strcmp(e, "rows16")) v = dpt::KERNEL_ROWS16;
         else if (!strcmp(e, "rows64")) v = dpt::KERNEL_ROWS64;
         else if (!strcmp(e, "lane")) v = dpt::KERNEL_LANE;
+        else if (!strcmp(e, "rows16w128")) v = dpt::KERNEL_ROWS16_128;
     }
     if (max_cp > 16) v = dpt::KERNEL_ROWS64;
     return v;
@@ -293,7 +294,7 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
     p.rec = c->rec;
     p.variant = kernel_variant(v->stats.max_cp);
     // the lane kernel implements the plain raw / pre-split encode only
-    if (p.variant == dpt::KERNEL_LANE && (mode_flags != DPT_MODE_RAW && mode_flags != DPT_MODE_PRESPLIT || edges))
+    if (p.variant == dpt::KERNEL_LANE && ((mode_flags != DPT_MODE_RAW && mode_flags != DPT_MODE_PRESPLIT) || edges))
         p.variant = v->stats.max_cp <= 16 ? dpt::KERNEL_ROWS16 : dpt::KERNEL_ROWS64;
     p.slots = v->d_slots;
     p.slot_ids = v->d_ids;

@@ -38,6 +38,9 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include <stdint.h>
+#include <stdlib.h>
+
+#include <type_traits>
 
 #include "dpt_internal.h"
 
@@ -132,30 +135,42 @@ template <> struct Group<64> {
 
 // ------------------------------------------------------------------ LDS layout
 
-// tags on the LAST expanded byte of an atom
-constexpr uint8_t TAG_ATOM_END = 1;
-constexpr uint8_t TAG_WORD_END = 2;
-
-constexpr unsigned ST_VALID = 0x8000u;
-constexpr unsigned ST_RESET = ST_VALID;   // cost 0, reachable, G 0
 constexpr uint16_t CP_WS = 0x8000;        // cpos bit: atom starts a word
+constexpr unsigned MAX_ATOM_BYTES = 8;    // expanded atom = one u64 (raw: '▁'+4-byte code point = 7)
 
-template <int CH, int G, int EXP>
+// final state at a word end: G = 16 packs cost (<= 1023) | invalid | 31-G (G <= 16) in 16 bits
+// (straight from the key: its low 5 bits are 31-G, bit 15 the invalid flag)
+template <int G> struct Wfin;
+template <> struct Wfin<16> {
+    using T = uint16_t;
+    static __device__ __forceinline__ T pack(unsigned r) { return (T)(((r >> 10) & 0xFFE0u) | (r & 31u)); }
+    // 1023 = the uncapped DP's "inf" (0xFFFF, inspect_tokenizer.py:80); capped costs stay <= CH
+    static __device__ __forceinline__ unsigned cost(T x) { return (x >> 6) == 1023u ? 0xFFFFu : (x >> 6); }
+    static __device__ __forceinline__ bool invalid(T x) { return (x >> 5) & 1u; }
+    static __device__ __forceinline__ unsigned gmax(T x) { return 31u - (x & 31u); }
+};
+template <> struct Wfin<64> {
+    using T = uint32_t;   // the group-min key itself: cost<<16 | invalid<<15 | 0x7FFF-G
+    static __device__ __forceinline__ T pack(unsigned r) { return r; }
+    static __device__ __forceinline__ unsigned cost(T x) { return x >> 16; }
+    static __device__ __forceinline__ bool invalid(T x) { return (x >> 15) & 1u; }
+    static __device__ __forceinline__ unsigned gmax(T x) { return 0x7FFFu - (x & 0x7FFFu); }
+};
+
+template <int CH, int G>
 struct GroupLDS {
     using M = typename Group<G>::M;
     static constexpr int NA = CH + 2;            // atoms + sentinel
-    static constexpr int NE = EXP * CH + 8;      // expanded bytes
-    // rec[j]: code-point prefix of atom j (| CP_WS at word starts and at the window end)
-    //         and the span mask of tokens of 1..G atoms starting at j
+    // rec[j]: code-point prefix of atom j (| CP_WS at word starts and at the window end) and the
+    //         span mask of tokens of 1..G atoms starting at j; after phase B the mask field holds
+    //         the first atom of selected token j (tokens tile the window)
     typename Group<G>::Rec rec[NA];
     // gem[i]: lanes d (j = i-1-d) in E(i) that are reachable (em) and that attain G[i] (gm)
     typename Group<G>::Gem gem[NA];
-    uint32_t wfin[NA];  // per word: the final group-min key (cost<<16 | invalid<<15 | 0x7FFF-G)
-    uint16_t aoff[NA];  // atom -> expanded byte offset
-    uint16_t wsl[NA];   // word -> first atom
-    uint16_t tok[NA];   // selected token -> first atom (tokens tile the window)
-    uint8_t ebyte[NE];
-    uint8_t etag[NE];
+    typename Wfin<G>::T wfin[NA];   // per end position: final state (read at word ends)
+    uint16_t aoff[NA];              // atom -> byte offset in the window
+    uint16_t wsl[NA];               // word -> first atom
+    uint8_t bytes[CH + 16];         // the window's input bytes (expanded on the fly)
 };
 
 struct SlotState {
@@ -165,11 +180,11 @@ struct SlotState {
     uint32_t inval, abase, pad1, pad2;   // abase: atoms of the string's earlier windows
 };
 
-template <int CH, int G, int EXP>
-constexpr int group_lds_bytes() { return (int)((sizeof(GroupLDS<CH, G, EXP>) + 15) & ~size_t(15)); }
+template <int CH, int G>
+constexpr int group_lds_bytes() { return (int)((sizeof(GroupLDS<CH, G>) + 15) & ~size_t(15)); }
 
-template <int CH, int G, int EXP>
-constexpr int block_lds_bytes() { return (64 / G) * (group_lds_bytes<CH, G, EXP>() + (int)sizeof(SlotState)); }
+template <int CH, int G>
+constexpr int block_lds_bytes() { return (64 / G) * (group_lds_bytes<CH, G>() + (int)sizeof(SlotState)); }
 
 // ------------------------------------------------------------------ trie access
 
@@ -186,7 +201,7 @@ constexpr int32_t TERM_BIT = (int32_t)0x80000000;
 struct EncodeArgs {
     const uint8_t *text;
     const uint64_t *str_off;
-    const uint8_t *cut_mask;    // PRESPLIT only
+    const uint8_t *cut_mask;    // PRESPLIT / ATOMS only
     uint64_t n_str;
     int32_t *staging;           // ids staged at (str_off[s]-str_off[0]) + k
     uint64_t *counts;           // per string
@@ -196,6 +211,7 @@ struct EncodeArgs {
     uint32_t *retry_count;
     const uint32_t *work_list;  // 2048-byte pass: the retry list
     const uint32_t *work_count;
+    uint32_t *work_next;        // dynamic work distribution counter (zeroed per launch)
     uint64_t *edges;            // nullable: per atom end, the E(i) & reachable back-distance mask
     int mode;                   // DPT_MODE_* | DPT_FLAG_*
 };
@@ -211,6 +227,34 @@ __device__ unsigned long long g_stamps[8];
 #define STAMP(k)
 #define STAMP_FLUSH
 #endif
+
+// phase A's per-atom descriptor lives in the (not yet written) gem[] entry of the atom
+template <int CH, int G>
+__device__ __forceinline__ uint32_t &ainfo(GroupLDS<CH, G> &L, unsigned j) {
+    return *reinterpret_cast<uint32_t *>(&L.gem[j]);
+}
+
+// la (<= 8) window bytes from offset p: three aligned dword reads and a funnel shift
+__device__ __forceinline__ uint64_t load_bytes(const uint8_t *bytes, unsigned p, unsigned la) {
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(bytes) + (p >> 2);
+    const unsigned sh = (p & 3u) * 8u;
+    const uint64_t lo = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+    const uint64_t hi = w[2];
+    uint64_t v = sh ? ((lo >> sh) | (hi << (64u - sh))) : lo;
+    return la >= 8 ? v : (v & ((1ull << (8u * la)) - 1ull));
+}
+
+// expanded bytes of the atom described by `info` (see prep_window)
+__device__ __forceinline__ uint64_t atom_from_info(const uint8_t *bytes, uint32_t info, bool raw, unsigned &cnt) {
+    const unsigned p = info & 0xFFFu, la = (info >> 12) & 0xFu;
+    const uint64_t v = load_bytes(bytes, p, la);
+    const unsigned b0 = (unsigned)(v & 0xFFu);
+    if (raw && (info & (1u << 17))) { cnt = 3 + la; return 0x8196E2ull | (v << 24); }
+    if (raw && b0 == ' ') { cnt = 3; return 0x8196E2ull; }
+    if (raw && b0 == '\n') { cnt = 6; return 0x3E413078303Cull; }
+    cnt = la;
+    return v;
+}
 
 // ------------------------------------------------------------------ prep: one slot's window
 
@@ -238,130 +282,101 @@ __device__ bool window_bounds(const uint8_t *str, const uint8_t *cut, uint64_t s
     return true;
 }
 
-// Atomise window bytes [pos, pos+wlen) into L.  Returns false if the expansion
-// does not fit the LDS budget.  Whole wave cooperates.
-template <int CH, int G, int EXP>
-__device__ bool prep_window(GroupLDS<CH, G, EXP> &L, const uint8_t *str, const uint8_t *cut, uint64_t pos,
+// Atomise window bytes [pos, pos+wlen) into L: the bytes themselves, atom byte offsets,
+// code-point prefixes (+ word-start bits) and the word list.  One packed DPP scan per 256
+// bytes.  Returns false if an atom is longer than MAX_ATOM_BYTES (ATOMS mode only).
+template <int CH, int G>
+__device__ bool prep_window(GroupLDS<CH, G> &L, const uint8_t *str, const uint8_t *cut, uint64_t pos,
                             unsigned wlen, int mode, unsigned lane, unsigned &n_atoms_o, unsigned &n_words_o) {
-    constexpr unsigned EX_BUDGET = GroupLDS<CH, G, EXP>::NE - 8;
     const bool raw = mode == 0;
-    unsigned n_atoms = 0, n_ex = 0, cp_tot = 0, n_words = 0;
+    unsigned n_atoms = 0, cp_tot = 0, n_words = 0;
     for (unsigned c0 = 0; c0 < wlen; c0 += 256) {
-        uint8_t bt[4];
-        unsigned cpl[4];
         bool ast[4], wst[4];
-        unsigned ex_sum = 0, cp_sum = 0, a_sum = 0, w_sum = 0;
+        unsigned cpl[4];
+        unsigned word = 0;
+        unsigned a_sum = 0, w_sum = 0, cp_sum = 0;
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             const unsigned k = c0 + lane * 4 + u;
             const bool in = k < wlen;
             const uint64_t p = pos + k;
             const uint8_t b = in ? str[p] : 0;
-            const bool first = in && p == 0;
             const uint8_t cm = (in && !raw) ? cut[p] : 0;
+            const bool first = in && p == 0;
             // mode 2 (ATOMS): atom starts come from the mask (bit 1), word starts from bit 0
             const bool cont = in && !first && (mode == 2 ? (cm & 3) == 0 : (b & 0xC0) == 0x80);
             const bool as = in && !cont;
             bool wsf;
-            unsigned el, cl;
+            unsigned cl;
             if (raw) {
                 wsf = as && (k == 0 || b == ' ');
-                el = !in ? 0 : first ? 4 : (b == ' ' ? 3 : (b == '\n' ? 6 : 1));
-                cl = !in ? 0 : first ? 2 : (b == '\n' ? 6 : (cont ? 0 : 1));
+                cl = !in ? 0 : first ? 2 : (b == '\n' ? 6 : ((b & 0xC0) == 0x80 ? 0 : 1));
             } else {
                 wsf = as && (k == 0 || (mode == 1 ? cm != 0 : (cm & 1) != 0));
-                el = in ? 1 : 0;
                 cl = (in && (b & 0xC0) != 0x80) ? 1 : 0;   // code points, whatever the atoms
             }
-            bt[u] = b; cpl[u] = cl; ast[u] = as; wst[u] = wsf;
-            ex_sum += el; cp_sum += cl; a_sum += as; w_sum += wsf;
+            word |= (unsigned)b << (8 * u);
+            ast[u] = as; wst[u] = wsf; cpl[u] = cl;
+            a_sum += as; w_sum += wsf; cp_sum += cl;
         }
-        // packed scans: (ex | cp<<16), (atoms | words<<16); every field < 65536
-        const unsigned v1 = ex_sum | (cp_sum << 16);
-        const unsigned v2 = a_sum | (w_sum << 16);
-        const unsigned i1 = wave_incl_scan_add(v1);
-        const unsigned i2 = wave_incl_scan_add(v2);
-        const unsigned t1 = __builtin_amdgcn_readlane(i1, 63);
-        const unsigned t2 = __builtin_amdgcn_readlane(i2, 63);
-        if (n_ex + (t1 & 0xFFFF) > EX_BUDGET) return false;
-        unsigned ex = n_ex + ((i1 - v1) & 0xFFFF);
-        unsigned cp = cp_tot + ((i1 - v1) >> 16);
-        unsigned ai = n_atoms + ((i2 - v2) & 0xFFFF);
-        unsigned wi = n_words + ((i2 - v2) >> 16);
-        // does the byte after each of mine start an atom / a word?
-        const unsigned my_first_flags = (ast[0] ? 1u : 0u) | (wst[0] ? 2u : 0u);
-        unsigned next_flags = (unsigned)__shfl_down((int)my_first_flags, 1);
-        const unsigned kn = c0 + 256;
-        unsigned chunk_next = 3;  // end of window: atom end + word end
-        if (kn < wlen) {
-            const uint64_t p = pos + kn;
-            const uint8_t b = str[p];
-            const uint8_t cm = raw ? 0 : cut[p];
-            const bool as = mode == 2 ? (cm & 3) != 0 : (b & 0xC0) != 0x80;
-            const bool wsf = as && (raw ? b == ' ' : (mode == 1 ? cm != 0 : (cm & 1) != 0));
-            chunk_next = (as ? 1u : 0u) | (wsf ? 2u : 0u);
-        }
+        // one packed scan: atoms (9 bits) | words (9 bits) << 9 | code points (14 bits) << 18
+        const unsigned v = a_sum | (w_sum << 9) | (cp_sum << 18);
+        const unsigned incl = wave_incl_scan_add(v);
+        const unsigned tot = __builtin_amdgcn_readlane(incl, 63);
+        const unsigned ex = incl - v;
+        unsigned ai = n_atoms + (ex & 0x1FFu);
+        unsigned wi = n_words + ((ex >> 9) & 0x1FFu);
+        unsigned cp = cp_tot + (ex >> 18);
+        if (c0 + lane * 4 < wlen) *reinterpret_cast<uint32_t *>(&L.bytes[c0 + lane * 4]) = word;
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             const unsigned k = c0 + lane * 4 + u;
-            if (k >= wlen) break;
-            const uint64_t p = pos + k;
-            unsigned nf;
-            if (k + 1 >= wlen) nf = 3;
-            else if (u < 3) nf = (ast[u + 1] ? 1u : 0u) | (wst[u + 1] ? 2u : 0u);
-            else nf = (lane == 63) ? chunk_next : next_flags;
             if (ast[u]) {
-                L.aoff[ai] = (uint16_t)ex;
+                L.aoff[ai] = (uint16_t)k;
                 L.rec[ai].cpos = (uint16_t)(cp | (wst[u] ? CP_WS : 0));
                 if (wst[u]) { L.wsl[wi] = (uint16_t)ai; wi++; }
                 ai++;
             }
-            const uint8_t b = bt[u];
-            if (raw && p == 0) {
-                L.ebyte[ex] = 0xE2; L.ebyte[ex + 1] = 0x96; L.ebyte[ex + 2] = 0x81; L.ebyte[ex + 3] = b;
-                L.etag[ex] = 0; L.etag[ex + 1] = 0; L.etag[ex + 2] = 0;
-                ex += 3;
-            } else if (raw && b == ' ') {
-                L.ebyte[ex] = 0xE2; L.ebyte[ex + 1] = 0x96; L.ebyte[ex + 2] = 0x81;
-                L.etag[ex] = 0; L.etag[ex + 1] = 0;
-                ex += 2;
-            } else if (raw && b == '\n') {
-                L.ebyte[ex] = '<'; L.ebyte[ex + 1] = '0'; L.ebyte[ex + 2] = 'x';
-                L.ebyte[ex + 3] = '0'; L.ebyte[ex + 4] = 'A'; L.ebyte[ex + 5] = '>';
-                L.etag[ex] = 0; L.etag[ex + 1] = 0; L.etag[ex + 2] = 0; L.etag[ex + 3] = 0; L.etag[ex + 4] = 0;
-                ex += 5;
-            } else {
-                L.ebyte[ex] = b;
-            }
-            L.etag[ex] = (uint8_t)(((nf & 1) ? TAG_ATOM_END : 0) | ((nf & 2) ? TAG_WORD_END : 0));
-            ex++;
             cp += cpl[u];
         }
-        n_ex += t1 & 0xFFFF; cp_tot += t1 >> 16;
-        n_atoms += t2 & 0xFFFF; n_words += t2 >> 16;
+        n_atoms += tot & 0x1FFu;
+        n_words += (tot >> 9) & 0x1FFu;
+        cp_tot += tot >> 18;
     }
     if (lane == 0) {
-        L.aoff[n_atoms] = (uint16_t)n_ex;
+        L.aoff[n_atoms] = (uint16_t)wlen;
         L.rec[n_atoms].cpos = (uint16_t)(cp_tot | CP_WS);
         L.wsl[n_words] = (uint16_t)n_atoms;
     }
     n_atoms_o = n_atoms;
     n_words_o = n_words;
-    return true;
+    wave_sync();
+    // per-atom walk descriptor for phase A (parked in gem[], which phase B overwrites):
+    //   byte offset | byte length << 12 | "a word or the window ends after it" << 16 | "first atom of the string" << 17
+    const unsigned lim = raw ? 4u : MAX_ATOM_BYTES;   // raw: '▁' + one code point must fit 8 bytes
+    bool bad = false;
+    for (unsigned j = lane; j < n_atoms; j += 64) {
+        const unsigned p0 = L.aoff[j], la = (unsigned)L.aoff[j + 1] - p0;
+        const unsigned stop = L.rec[j + 1].cpos >> 15;
+        const unsigned first = (raw && pos == 0 && j == 0) ? 1u : 0u;
+        bad |= la > lim;
+        ainfo(L, j) = p0 | (la << 12) | (stop << 16) | (first << 17);
+    }
+    return ballot(bad) == 0;
 }
 
 // ------------------------------------------------------------------ the tokenize kernel
 
-template <int CH, int G, int EXP, bool BIG>
+template <int CH, int G, bool BIG>
 __global__ void __launch_bounds__(64)
 tokenize_kernel(EncodeArgs a, TrieView tv) {
     constexpr int NG = 64 / G;
-    using GL = GroupLDS<CH, G, EXP>;
+    using GL = GroupLDS<CH, G>;
     using GR = Group<G>;
     using M = typename GR::M;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    SlotState *const SS = reinterpret_cast<SlotState *>(smem + NG * group_lds_bytes<CH, G, EXP>());
-    auto grp = [&](unsigned g) -> GL & { return *reinterpret_cast<GL *>(smem + g * group_lds_bytes<CH, G, EXP>()); };
+    SlotState *const SS = reinterpret_cast<SlotState *>(smem + NG * group_lds_bytes<CH, G>());
+    auto grp = [&](unsigned g) -> GL & { return *reinterpret_cast<GL *>(smem + g * group_lds_bytes<CH, G>()); };
 
     const unsigned lane = lane_id();
     const unsigned mg = lane / G;        // my group
@@ -372,8 +387,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
     const bool raw = mode == 0;
     const bool uncapped = (a.mode & DPT_FLAG_UNCAPPED) != 0;   // f2: inspect_tokenizer's inf-initialised DP
     const bool len_only = (a.mode & (DPT_FLAG_UNCAPPED | DPT_FLAG_LEN_ONLY)) != 0;
-    uint64_t next = blockIdx.x;          // one wave per block
-    const uint64_t stride = gridDim.x;
+    bool exhausted = false;              // strings are handed out by a device counter
     STAMP_DECL
 
     if (lane < (unsigned)NG) SS[lane].active = 0;
@@ -387,9 +401,12 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
             SlotState &S = SS[g];
             for (;;) {
                 if (!uni(S.active)) {
-                    if (next >= n_work) break;
-                    const uint64_t s = BIG ? (uint64_t)a.work_list[next] : next;
-                    next += stride;
+                    if (exhausted) break;
+                    unsigned idx = 0;
+                    if (lane == 0) idx = atomicAdd(a.work_next, 1u);
+                    idx = __builtin_amdgcn_readlane(idx, 0);
+                    if ((uint64_t)idx >= n_work) { exhausted = true; break; }
+                    const uint64_t s = BIG ? (uint64_t)a.work_list[idx] : (uint64_t)idx;
                     const uint64_t sb = a.str_off[s] - base_off;
                     const uint64_t sl = a.str_off[s + 1] - a.str_off[s];
                     if (lane == 0) {
@@ -406,9 +423,9 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 unsigned wlen = 0, na = 0, nw = 0;
                 bool ok = status != 2;
                 if (ok) ok = window_bounds<CH>(str, cut, slen, pos, mode, lane, wlen);
-                if (ok) ok = prep_window<CH, G, EXP>(L, str, cut, pos, wlen, mode, lane, na, nw);
+                if (ok) ok = prep_window<CH, G>(L, str, cut, pos, wlen, mode, lane, na, nw);
                 if (ok) {
-                    if (lane == 0) { S.wlen = wlen; S.n_atoms = na; S.n_words = nw; }
+                    if (lane == 0) { S.wlen = wlen; S.n_atoms = na; S.n_words = nw; S.wtok = 0; S.inval = 0; }
                     busy++;
                     break;
                 }
@@ -450,35 +467,51 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 for (int g = 0; g < NG; g++) base = (gsel == (unsigned)g) ? pre[g] : base;
                 j = uu - base;
             };
+            // lane state: start atom j of group gsel, atoms matched so far (len), the trie node, the
+            // expanded bytes left of the current atom (seq, cnt) and those of the next one (prefetched)
             unsigned u = lane;
             bool active = u < total;
-            unsigned e = 0;
             int32_t nb = tv.root_base, node = 0;
-            unsigned len = 0, mask = 0;
-            uint64_t mask64 = 0;
-            if (active) { locate(u); e = grp(gsel).aoff[j]; }
+            unsigned len = 0, mask = 0, cnt = 0, ncnt = 0;
+            uint32_t info = 0, ninfo = 0;
+            uint64_t mask64 = 0, seq = 0, nseq = 0;
+            auto start = [&]() {
+                locate(u);
+                GL &L = grp(gsel);
+                info = ainfo(L, j);
+                seq = atom_from_info(L.bytes, info, raw, cnt);
+                if (!(info & 0x10000u)) { ninfo = ainfo(L, j + 1); nseq = atom_from_info(L.bytes, ninfo, raw, ncnt); }
+            };
+            if (active) start();
             unsigned nxt = 64;
             while (ballot(active)) {
                 bool done = false;
                 if (active) {
-                    GL &L = grp(gsel);
-                    const uint8_t b = L.ebyte[e];
-                    const uint8_t tg = L.etag[e];
-                    const int32_t t = nb + (int32_t)b;
+                    const int32_t t = nb + (int32_t)(seq & 0xFFu);
                     const int2 ent = tv.slots[t];
+                    seq >>= 8;
+                    cnt--;
                     if (ent.y != node) {
                         done = true;
                     } else {
                         node = t;
                         nb = ent.x & 0x7FFFFFFF;
-                        e++;
-                        if (tg & TAG_ATOM_END) {
+                        if (cnt == 0) {   // atom j+len-1 ends: the span j..j+len is a candidate token
                             len++;
                             if (ent.x & TERM_BIT) {
                                 if (G == 64) mask64 |= 1ull << (len - 1);
                                 else mask |= 1u << (len - 1);
                             }
-                            if ((tg & TAG_WORD_END) || len == (unsigned)G) done = true;
+                            if ((info & 0x10000u) || len == (unsigned)G) {
+                                done = true;
+                            } else {
+                                info = ninfo; seq = nseq; cnt = ncnt;
+                                if (!(info & 0x10000u) && len + 1 < (unsigned)G) {
+                                    GL &L = grp(gsel);
+                                    ninfo = ainfo(L, j + len + 1);
+                                    nseq = atom_from_info(L.bytes, ninfo, raw, ncnt);
+                                }
+                            }
                         }
                     }
                 }
@@ -489,7 +522,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                     const unsigned rank = __builtin_amdgcn_mbcnt_hi((unsigned)(dm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)dm, 0u));
                     u = nxt + rank;
                     active = u < total;
-                    if (active) { locate(u); e = grp(gsel).aoff[j]; nb = tv.root_base; node = 0; len = 0; mask = 0; mask64 = 0; }
+                    if (active) { start(); nb = tv.root_base; node = 0; len = 0; mask = 0; mask64 = 0; }
                 }
                 nxt += (unsigned)__builtin_popcountll(dm);
             }
@@ -504,96 +537,140 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
             unsigned imax = 0;
 #pragma unroll
             for (int g = 0; g < NG; g++) imax = max(imax, uni(SS[g].n_atoms));
-            // st (lane d, candidate j = i-1-d) = (cost[j]+1) << 16 | invalid[j] << 15 | G[j]
-            constexpr unsigned ST0 = 0x10000u;   // word start: cost 0, reachable, G 0
-            unsigned ws = 0, w = 0, wsum = 0, winv = 0;
-            if constexpr (G == 16) {
-                const uint32_t *rec32 = reinterpret_cast<const uint32_t *>(L.rec);
-                const uint32_t r0 = rec32[0];
+            // Steps past a slot's own n_atoms (up to the wave's imax <= CH) compute garbage that
+            // lands in gem[]/wfin[] entries nobody reads, so the loop body has no per-slot guard.
+            // Recording the edges (f1) and the uncapped DP (f2) are hoisted out as loop versions.
+            auto forward = [&](auto EDGES, auto UNCAPPED) {
+                constexpr bool edges = decltype(EDGES)::value, unc = decltype(UNCAPPED)::value;
+                // st (lane d, candidate j = i-1-d) = (cost[j]+1) << 16 | invalid[j] << 15 | G[j]
+                constexpr unsigned ST0 = 0x10000u;   // word start: cost 0, reachable, G 0
+                unsigned ws = 0;
                 unsigned st = d == 0 ? ST0 : 0u;
                 unsigned cpj = 0;
-                unsigned m = (d == 0 && na > 0) ? (r0 >> 16) : 0u;
-                uint32_t nx = rec32[1];
-                for (unsigned i = 1; i <= imax; i++) {
-                    const uint32_t cur = nx;
-                    nx = rec32[i + 1];                         // i+1 <= CH+1 < NA: always in bounds
-                    const unsigned cpi = cur & 0x7FFFu;
-                    const unsigned span = cpi - cpj;
-                    const unsigned gj = st & 0x7FFFu;
-                    const unsigned kv = (st | 0x7FFFu) - (gj > span ? gj : span);
-                    const unsigned key = ((m >> d) & 1u) ? kv : 0xFFFFFFFFu;
-                    unsigned r = row_min_u32(key);
-                    const unsigned capkey = uncapped ? 0xFFFFFFFFu : (((i - ws) << 16) | 0xFFFFu);
-                    r = r < capkey ? r : capkey;
-                    const uint64_t gmb = ballot(key == r);
-                    const uint64_t emb = ballot((key ^ r) < 0x8000u);
-                    const bool live = i <= na;
-                    if (a.edges && d == 0 && live)
-                        a.edges[SS[mg].sb + SS[mg].abase + i - 1] = (unsigned)(emb >> (16u * mg)) & 0xFFFFu;
-                    const bool wend = live && (cur & CP_WS);  // CP_WS marks word starts and the window end
-                    const bool boundary = wend && i < na;
-                    if (d == 0 && live) {
-                        const unsigned sh = 16u * mg;
-                        L.gem[i].v = ((unsigned)(gmb >> sh) & 0xFFFFu) | ((unsigned)(emb >> sh) << 16);
-                        if (wend) L.wfin[w] = r;
+                if constexpr (G == 16) {
+                    const uint32_t *rec32 = reinterpret_cast<const uint32_t *>(L.rec);
+                    const uint32_t r0 = rec32[0];
+                    const unsigned bitd = 1u << d;
+                    unsigned m = (d == 0 && na > 0) ? (r0 >> 16) : 0u;
+                    uint32_t nx = rec32[1];
+                    for (unsigned i = 1; i <= imax; i++) {
+                        const uint32_t cur = nx;
+                        nx = rec32[i + 1];                         // i+1 <= CH+1 < NA: always in bounds
+                        const unsigned cpi = cur & 0x7FFFu;
+                        const unsigned span = cpi - cpj;
+                        const unsigned gj = st & 0x7FFFu;
+                        const unsigned kv = (st | 0x7FFFu) - (gj > span ? gj : span);
+                        const unsigned key = (m & bitd) ? kv : 0xFFFFFFFFu;
+                        unsigned r = row_min_u32(key);
+                        if constexpr (!unc) {
+                            const unsigned capkey = ((i - ws) << 16) | 0xFFFFu;
+                            r = r < capkey ? r : capkey;
+                        }
+                        const uint64_t gmb = ballot(key == r);
+                        const uint64_t emb = ballot((key ^ r) < 0x8000u);
+                        if (d == 0) {
+                            const unsigned sh = 16u * mg;
+                            const unsigned em16 = (unsigned)(emb >> sh) & 0xFFFFu;
+                            L.gem[i].v = ((unsigned)(gmb >> sh) & 0xFFFFu) | (em16 << 16);
+                            L.wfin[i] = Wfin<G>::pack(r);
+                            if constexpr (edges)
+                                if (i <= na) a.edges[SS[mg].sb + SS[mg].abase + i - 1] = em16;
+                        }
+                        const bool wend = (cur & CP_WS) != 0;   // word starts and the window end
+                        ws = wend ? i : ws;
+                        unsigned nxt = (r ^ 0x7FFFu) + 0x10000u;
+                        if constexpr (unc) nxt = r >= 0xFFFE0000u ? 0xFFFF8000u : nxt;   // unreachable: cost stays inf
+                        const unsigned sin = wend ? ST0 : nxt;
+                        st = row_shift_in(st, sin);
+                        cpj = row_shift_in(cpj, cpi);
+                        m = row_shift_in(m, cur >> 16);
                     }
-                    wsum += wend ? (r >> 16) : 0u;
-                    winv |= wend ? (r & 0x8000u) : 0u;
-                    w += boundary ? 1u : 0u;
-                    ws = boundary ? i : ws;
-                    // (uncapped DP: an unreachable position saturates at cost 0xFFFF = inf)
-                    const unsigned sin = boundary ? ST0 : (r >= 0xFFFE0000u ? 0xFFFF8000u : ((r ^ 0x7FFFu) + 0x10000u));
-                    st = row_shift_in(st, sin);
-                    cpj = row_shift_in(cpj, cpi);
-                    m = row_shift_in(m, cur >> 16);
+                } else {
+                    const uint64_t m0 = na > 0 ? L.rec[0].smask : 0ull;
+                    unsigned mlo = d == 0 ? (unsigned)m0 : 0u, mhi = d == 0 ? (unsigned)(m0 >> 32) : 0u;
+                    for (unsigned i = 1; i <= imax; i++) {
+                        const unsigned cur = L.rec[i].cpos;
+                        const uint64_t mi = L.rec[i].smask;
+                        const unsigned cpi = cur & 0x7FFFu;
+                        const unsigned span = cpi - cpj;
+                        const unsigned gj = st & 0x7FFFu;
+                        const unsigned kv = (st | 0x7FFFu) - (gj > span ? gj : span);
+                        const unsigned bit = (d < 32 ? (mlo >> d) : (mhi >> (d - 32))) & 1u;
+                        const unsigned key = bit ? kv : 0xFFFFFFFFu;
+                        unsigned r = wave_min_u32(key);
+                        if constexpr (!unc) {
+                            const unsigned capkey = ((i - ws) << 16) | 0xFFFFu;
+                            r = r < capkey ? r : capkey;
+                        }
+                        const uint64_t gmb = ballot(key == r);
+                        const uint64_t emb = ballot((key ^ r) < 0x8000u);
+                        if (lane == 0) {
+                            L.gem[i].gm = gmb;
+                            L.gem[i].em = emb;
+                            L.wfin[i] = Wfin<G>::pack(r);
+                            if constexpr (edges)
+                                if (i <= na) a.edges[SS[0].sb + SS[0].abase + i - 1] = emb;
+                        }
+                        const bool wend = (cur & CP_WS) != 0;
+                        ws = wend ? i : ws;
+                        unsigned nxt = (r ^ 0x7FFFu) + 0x10000u;
+                        if constexpr (unc) nxt = r >= 0xFFFE0000u ? 0xFFFF8000u : nxt;
+                        const unsigned sin = wend ? ST0 : nxt;
+                        st = wave_shift_in(st, sin);
+                        cpj = wave_shift_in(cpj, cpi);
+                        mlo = wave_shift_in(mlo, (unsigned)mi);
+                        mhi = wave_shift_in(mhi, (unsigned)(mi >> 32));
+                    }
                 }
+            };
+            using T_ = std::true_type;
+            using F_ = std::false_type;
+            if (a.edges) {
+                if (uncapped) forward(T_{}, T_{}); else forward(T_{}, F_{});
             } else {
-                unsigned st = d == 0 ? ST0 : 0u;
-                unsigned cpj = 0;
-                const uint64_t m0 = na > 0 ? L.rec[0].smask : 0ull;
-                unsigned mlo = d == 0 ? (unsigned)m0 : 0u, mhi = d == 0 ? (unsigned)(m0 >> 32) : 0u;
-                for (unsigned i = 1; i <= imax; i++) {
-                    const unsigned cur = L.rec[i].cpos;
-                    const uint64_t mi = L.rec[i].smask;
-                    const unsigned cpi = cur & 0x7FFFu;
-                    const unsigned span = cpi - cpj;
-                    const unsigned gj = st & 0x7FFFu;
-                    const unsigned kv = (st | 0x7FFFu) - (gj > span ? gj : span);
-                    const unsigned bit = (d < 32 ? (mlo >> d) : (mhi >> (d - 32))) & 1u;
-                    const unsigned key = bit ? kv : 0xFFFFFFFFu;
-                    unsigned r = wave_min_u32(key);
-                    const unsigned capkey = uncapped ? 0xFFFFFFFFu : (((i - ws) << 16) | 0xFFFFu);
-                    r = r < capkey ? r : capkey;
-                    const uint64_t gmb = ballot(key == r);
-                    const uint64_t emb = ballot((key ^ r) < 0x8000u);
-                    if (a.edges && lane == 0) a.edges[SS[0].sb + SS[0].abase + i - 1] = emb;
-                    const bool wend = (cur & CP_WS) != 0;
-                    const bool boundary = wend && i < na;
-                    if (lane == 0) {
-                        L.gem[i].gm = gmb;
-                        L.gem[i].em = emb;
-                        if (wend) L.wfin[w] = r;
-                    }
-                    wsum += wend ? (r >> 16) : 0u;
-                    winv |= wend ? (r & 0x8000u) : 0u;
-                    w += boundary ? 1u : 0u;
-                    ws = boundary ? i : ws;
-                    const unsigned sin = boundary ? ST0 : (r >= 0xFFFE0000u ? 0xFFFF8000u : ((r ^ 0x7FFFu) + 0x10000u));
-                    st = wave_shift_in(st, sin);
-                    cpj = wave_shift_in(cpj, cpi);
-                    mlo = wave_shift_in(mlo, (unsigned)mi);
-                    mhi = wave_shift_in(mhi, (unsigned)(mi >> 32));
-                }
-            }
-            if (d == 0 && na > 0) {
-                SlotState &S = SS[mg];
-                S.capsum += wsum;
-                S.inval = winv ? 1u : 0u;
-                S.wtok = wsum;
+                if (uncapped) forward(F_{}, T_{}); else forward(F_{}, F_{});
             }
         }
         wave_sync();
         STAMP(2);
+
+        // ---------------------------------------------------------- C0: per-window token counts and validity
+        // (word w ends at atom wsl[w+1]; its final state is wfin[wsl[w+1]])
+        {
+            unsigned pre[NG + 1];
+            pre[0] = 0;
+#pragma unroll
+            for (int g = 0; g < NG; g++) pre[g + 1] = pre[g] + (uni(SS[g].n_atoms) > 0 ? uni(SS[g].n_words) : 0u);
+            const unsigned total = pre[NG];
+            for (unsigned u0 = 0; u0 < total; u0 += 64) {
+                const unsigned u = u0 + lane;
+                unsigned g = 0;
+#pragma unroll
+                for (int k = 1; k < NG; k++) g += u >= pre[k] ? 1u : 0u;
+                unsigned wbase = 0;
+#pragma unroll
+                for (int k = 0; k < NG; k++) wbase = g == (unsigned)k ? pre[k] : wbase;
+                unsigned cost = 0, inv = 0;
+                if (u < total) {
+                    const GL &L = grp(g);
+                    const typename Wfin<G>::T F = L.wfin[L.wsl[u - wbase + 1]];
+                    cost = Wfin<G>::cost(F);
+                    inv = Wfin<G>::invalid(F) ? 1u : 0u;
+                }
+                // per-group sums over this chunk: groups own contiguous lane ranges
+#pragma unroll
+                for (int k = 0; k < NG; k++) {
+                    const unsigned lo = pre[k] > u0 ? pre[k] - u0 : 0u, hi = pre[k + 1] > u0 ? pre[k + 1] - u0 : 0u;
+                    if (hi <= lo) continue;
+                    const bool mine = lane >= lo && lane < (hi < 64u ? hi : 64u);
+                    const unsigned cs = wave_incl_scan_add(mine ? cost : 0u);
+                    const unsigned csum = __builtin_amdgcn_readlane(cs, 63);
+                    const unsigned anyinv = ballot(mine && inv) != 0 ? 1u : 0u;
+                    if (lane == 0) { SS[k].wtok += csum; SS[k].inval |= anyinv; }
+                }
+            }
+        }
+        wave_sync();
 
         // ---------------------------------------------------------- C1: selection, one lane per word
         {
@@ -620,15 +697,15 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                     if (g == (unsigned)k) { wbase = pre[k]; tbase = tokpre[k]; ginv = inv_g[k]; }
                 GL &L = grp(g);
                 const unsigned w = u - wbase;
-                const unsigned F = in ? L.wfin[w] : 0u;
-                const unsigned cost = in ? (F >> 16) : 0u;
+                const typename Wfin<G>::T F = in ? L.wfin[L.wsl[w + 1]] : (typename Wfin<G>::T)0;
+                const unsigned cost = in ? Wfin<G>::cost(F) : 0u;
                 const unsigned incl = wave_incl_scan_add(cost);
                 const unsigned tok_base = carry + incl - cost - tbase;
                 carry += __builtin_amdgcn_readlane(incl, 63);
                 if (in && !ginv && !len_only) {
                     const unsigned ws = L.wsl[w];
                     unsigned i = L.wsl[w + 1];
-                    const unsigned Ls = 0x7FFFu - (F & 0x7FFFu);   // G of the word = the longest token to reach
+                    const unsigned Ls = Wfin<G>::gmax(F);   // G of the word = the longest token to reach
                     unsigned c = cost, A = 0;
                     unsigned pend = L.rec[i].cpos & 0x7FFFu;
                     while (i > ws) {
@@ -642,7 +719,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                         if (sel == 0 || dd + 1 > i - ws || c == 0) break;   // unreachable by Appendix A
                         const unsigned j = i - 1 - dd;
                         c--;
-                        L.tok[tok_base + c] = (uint16_t)j;
+                        L.rec[tok_base + c].smask = (M)j;   // span masks are dead after B
                         pend = cpi;
                         i = j;
                     }
@@ -655,12 +732,14 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
         // ---------------------------------------------------------- C2: ids (lanes over all slots' tokens)
         {
             unsigned pre[NG + 1], na_g[NG];
+            unsigned firstmask = 0;   // groups whose window starts the string (raw '▁' + first atom)
             pre[0] = 0;
 #pragma unroll
             for (int g = 0; g < NG; g++) {
                 const bool gv = !len_only && uni(SS[g].inval) == 0 && uni(SS[g].status) == 0 && uni(SS[g].n_atoms) > 0;
                 pre[g + 1] = pre[g] + (gv ? uni(SS[g].wtok) : 0u);
                 na_g[g] = uni(SS[g].n_atoms);
+                firstmask |= (uni64(SS[g].pos) == 0 ? 1u : 0u) << g;
             }
             const unsigned total = pre[NG];
             for (unsigned t0 = 0; t0 < total; t0 += 64) {
@@ -675,17 +754,22 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                         if (g == (unsigned)k) { base = pre[k]; na = na_g[k]; ntk = pre[k + 1] - pre[k]; }
                     GL &L = grp(g);
                     const unsigned k = t - base;
-                    const unsigned j0 = L.tok[k];
-                    const unsigned j1 = k + 1 < ntk ? L.tok[k + 1] : na;
-                    const unsigned e0 = L.aoff[j0], e1 = L.aoff[j1];
+                    const unsigned j0 = (unsigned)L.rec[k].smask;
+                    const unsigned j1 = k + 1 < ntk ? (unsigned)L.rec[k + 1].smask : na;
+                    const bool first = raw && j0 == 0 && ((firstmask >> g) & 1u);
                     int32_t node = 0, nb = tv.root_base;
                     bool ok = true;
-                    for (unsigned e = e0; e < e1; e++) {
-                        const int32_t sl = nb + (int32_t)L.ebyte[e];
-                        const int2 ent = tv.slots[sl];
-                        ok &= ent.y == node;
-                        node = sl;
-                        nb = ent.x & 0x7FFFFFFF;
+                    for (unsigned jj = j0; jj < j1; jj++) {
+                        const unsigned p0 = L.aoff[jj], la = (unsigned)L.aoff[jj + 1] - p0;
+                        unsigned cnt;
+                        uint64_t seq = atom_from_info(L.bytes, p0 | (la << 12) | ((first && jj == 0) ? (1u << 17) : 0u), raw, cnt);
+                        for (; cnt; cnt--, seq >>= 8) {
+                            const int32_t sl = nb + (int32_t)(seq & 0xFFu);
+                            const int2 ent = tv.slots[sl];
+                            ok &= ent.y == node;
+                            node = sl;
+                            nb = ent.x & 0x7FFFFFFF;
+                        }
                     }
                     const SlotState &S = SS[g];
                     a.staging[S.sb + S.ntok + k] = ok ? tv.ids[node] : -1;
@@ -698,6 +782,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
         if (lane < (unsigned)NG) {
             SlotState &S = SS[lane];
             if (S.active && S.n_atoms > 0) {
+                S.capsum += S.wtok;
                 if (S.inval && S.status == 0) S.status = 1;
                 if (S.status == 0 && !len_only) S.ntok += S.wtok;
                 S.pos += S.wlen;
@@ -733,7 +818,8 @@ __global__ void __launch_bounds__(256) compact_kernel(const int32_t *__restrict_
 }
 
 __global__ void zero_first(uint64_t *p, uint32_t *rc) {
-    if (threadIdx.x == 0) { p[0] = 0; *rc = 0; }
+    if (threadIdx.x < 4) rc[threadIdx.x] = 0;   // retry count, pass-1 / pass-2 work counters
+    if (threadIdx.x == 0) p[0] = 0;
 }
 
 // ------------------------------------------------------------------ histogram
@@ -762,17 +848,36 @@ __global__ void __launch_bounds__(256) hist_kernel(const uint64_t *__restrict__ 
 
 // ------------------------------------------------------------------ launchers
 
-constexpr int SMALL_CH = 256, SMALL_EXP = 2;
-constexpr int BIG_CH = 2048, BIG_EXP = 6;
+constexpr int SMALL_CH = 256;
+constexpr int BIG_CH = 2048;
 
-static_assert(block_lds_bytes<SMALL_CH, 16, SMALL_EXP>() <= 64 * 1024, "small LDS");
-static_assert(block_lds_bytes<SMALL_CH, 64, SMALL_EXP>() <= 64 * 1024, "small LDS");
-static_assert(block_lds_bytes<BIG_CH, 64, BIG_EXP>() <= 160 * 1024, "big LDS");
+static_assert(block_lds_bytes<SMALL_CH, 16>() <= 64 * 1024, "small LDS");
+static_assert(block_lds_bytes<SMALL_CH, 64>() <= 64 * 1024, "small LDS");
+static_assert(block_lds_bytes<BIG_CH, 64>() <= 160 * 1024, "big LDS");
 
-template <int CH, int G, int EXP, bool BIG>
-static void launch_tok(const EncodeArgs &a, const TrieView &tv, unsigned blocks, hipStream_t stream) {
-    constexpr int lds = block_lds_bytes<CH, G, EXP>();
-    hipLaunchKernelGGL((tokenize_kernel<CH, G, EXP, BIG>), dim3(blocks), dim3(64), lds, stream, a, tv);
+// Resident waves per CU for an instantiation (LDS / VGPR limited); DPT_WAVES_PER_CU overrides.
+template <int CH, int G, bool BIG>
+static unsigned resident_per_cu() {
+    static unsigned cached = 0;
+    if (cached) return cached;
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, tokenize_kernel<CH, G, BIG>, 64, block_lds_bytes<CH, G>()) != hipSuccess || nb <= 0)
+        nb = 8;
+    if (const char *e = getenv("DPT_WAVES_PER_CU")) {
+        const int v = atoi(e);
+        if (v > 0) nb = v;
+    }
+    cached = (unsigned)nb;
+    return cached;
+}
+
+// Persistent grid: every resident wave pulls strings from the work counter until it runs dry.
+template <int CH, int G, bool BIG>
+static void launch_tok(const EncodeArgs &a, const TrieView &tv, uint64_t n_units, unsigned n_cu, hipStream_t stream) {
+    constexpr int lds = block_lds_bytes<CH, G>();
+    uint64_t blocks = (uint64_t)n_cu * resident_per_cu<CH, G, BIG>();
+    if (blocks > n_units) blocks = n_units ? n_units : 1;
+    hipLaunchKernelGGL((tokenize_kernel<CH, G, BIG>), dim3((unsigned)blocks), dim3(64), lds, stream, a, tv);
 }
 
 hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t ev[6]) {
@@ -782,6 +887,7 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     a.retry_list = p.retry_list; a.retry_count = p.retry_count; a.work_list = nullptr; a.work_count = nullptr;
     a.mode = p.mode;
     a.edges = p.edges;
+    a.work_next = p.retry_count + 1;
     TrieView tv{p.slots, p.slot_ids, p.root_base};
 
     hipLaunchKernelGGL(zero_first, dim3(1), dim3(64), 0, stream, p.id_off, p.retry_count);
@@ -792,16 +898,16 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
             if (blocks > (uint64_t)p.max_blocks) blocks = p.max_blocks;
             launch_lane(p, (unsigned)blocks, stream);
         } else {
-            const unsigned ng = p.variant == KERNEL_ROWS16 ? 4u : 1u;
-            uint64_t blocks = (p.n_str + ng - 1) / ng;
-            if (blocks > (uint64_t)p.max_blocks) blocks = p.max_blocks;
-            if (p.variant == KERNEL_ROWS16) launch_tok<SMALL_CH, 16, SMALL_EXP, false>(a, tv, (unsigned)blocks, stream);
-            else launch_tok<SMALL_CH, 64, SMALL_EXP, false>(a, tv, (unsigned)blocks, stream);
+            const unsigned n_cu = p.max_blocks / 64;
+            if (p.variant == KERNEL_ROWS16) launch_tok<SMALL_CH, 16, false>(a, tv, (p.n_str + 3) / 4, n_cu, stream);
+            else if (p.variant == KERNEL_ROWS16_128) launch_tok<128, 16, false>(a, tv, (p.n_str + 3) / 4, n_cu, stream);
+            else launch_tok<SMALL_CH, 64, false>(a, tv, p.n_str, n_cu, stream);
         }
         // second pass over the strings whose single word (or expansion) did not fit the small window
         EncodeArgs b = a;
         b.work_list = p.retry_list; b.work_count = p.retry_count;
-        launch_tok<BIG_CH, 64, BIG_EXP, true>(b, tv, 256, stream);
+        b.work_next = p.retry_count + 2;
+        launch_tok<BIG_CH, 64, true>(b, tv, p.n_str, p.max_blocks / 64, stream);
     }
     if (ev) hipEventRecord(ev[1], stream);
     if (p.n_str > 0) {
@@ -838,8 +944,8 @@ hipError_t launch_histogram(const uint64_t *id_off, const int32_t *status, uint6
 hipError_t kernel_init() {
     static bool done = false;
     if (done) return hipSuccess;
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&tokenize_kernel<BIG_CH, 64, BIG_EXP, true>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, block_lds_bytes<BIG_CH, 64, BIG_EXP>());
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&tokenize_kernel<BIG_CH, 64, true>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, block_lds_bytes<BIG_CH, 64>());
     if (e == hipSuccess) done = true;
     return e;
 }
