@@ -115,22 +115,26 @@ __device__ __forceinline__ void wave_sync() {
 template <int G> struct Group;
 
 // G = 16: four strings per wave, one per DPP row.  Per atom: {cpos, span mask} in one
-// dword; per end position: {gm, em} in one dword.
+// dword; per end position i, one dword `fin`: the back distances (minus one) of the largest
+// reachable j in E(i) attaining G[i] (dg) and of the largest reachable j in E(i) (de) --
+// G when there is none -- and the final state when i ends a word (Wfin<16>).
 template <> struct Group<16> {
     using M = uint16_t;  // span mask: bit L-1 = an L-atom token starts here
     struct Rec { uint16_t cpos; uint16_t smask; };
-    struct Gem { uint32_t v; };
-    static __device__ __forceinline__ unsigned gm(const Gem &x) { return x.v & 0xFFFFu; }
-    static __device__ __forceinline__ unsigned em(const Gem &x) { return x.v >> 16; }
+    struct Fin { uint32_t v; };
+    static __device__ __forceinline__ unsigned dg(const Fin &x) { return x.v & 31u; }
+    static __device__ __forceinline__ unsigned de(const Fin &x) { return (x.v >> 5) & 31u; }
+    static __device__ __forceinline__ uint16_t wfin(const Fin &x) { return (uint16_t)(x.v >> 16); }
 };
 
 // G = 64: one string per wave (vocabularies with tokens of 17..64 code points).
 template <> struct Group<64> {
     using M = uint64_t;
     struct Rec { uint64_t smask; uint16_t cpos; uint16_t pad[3]; };
-    struct Gem { uint64_t gm, em; };
-    static __device__ __forceinline__ uint64_t gm(const Gem &x) { return x.gm; }
-    static __device__ __forceinline__ uint64_t em(const Gem &x) { return x.em; }
+    struct Fin { uint32_t d; uint32_t w; };
+    static __device__ __forceinline__ unsigned dg(const Fin &x) { return x.d & 127u; }
+    static __device__ __forceinline__ unsigned de(const Fin &x) { return (x.d >> 8) & 127u; }
+    static __device__ __forceinline__ uint32_t wfin(const Fin &x) { return x.w; }
 };
 
 // ------------------------------------------------------------------ LDS layout
@@ -165,9 +169,7 @@ struct GroupLDS {
     //         span mask of tokens of 1..G atoms starting at j; after phase B the mask field holds
     //         the first atom of selected token j (tokens tile the window)
     typename Group<G>::Rec rec[NA];
-    // gem[i]: lanes d (j = i-1-d) in E(i) that are reachable (em) and that attain G[i] (gm)
-    typename Group<G>::Gem gem[NA];
-    typename Wfin<G>::T wfin[NA];   // per end position: final state (read at word ends)
+    typename Group<G>::Fin fin[NA];   // per end position, see Group<G>
     uint16_t aoff[NA];              // atom -> byte offset in the window
     uint16_t wsl[NA];               // word -> first atom
     uint8_t bytes[CH + 16];         // the window's input bytes (expanded on the fly)
@@ -228,10 +230,10 @@ __device__ unsigned long long g_stamps[8];
 #define STAMP_FLUSH
 #endif
 
-// phase A's per-atom descriptor lives in the (not yet written) gem[] entry of the atom
+// phase A's per-atom descriptor lives in the (not yet written) fin[] entry of the atom
 template <int CH, int G>
 __device__ __forceinline__ uint32_t &ainfo(GroupLDS<CH, G> &L, unsigned j) {
-    return *reinterpret_cast<uint32_t *>(&L.gem[j]);
+    return *reinterpret_cast<uint32_t *>(&L.fin[j]);
 }
 
 // la (<= 8) window bytes from offset p: three aligned dword reads and a funnel shift
@@ -351,7 +353,7 @@ __device__ bool prep_window(GroupLDS<CH, G> &L, const uint8_t *str, const uint8_
     n_atoms_o = n_atoms;
     n_words_o = n_words;
     wave_sync();
-    // per-atom walk descriptor for phase A (parked in gem[], which phase B overwrites):
+    // per-atom walk descriptor for phase A (parked in fin[], which phase B overwrites):
     //   byte offset | byte length << 12 | "a word or the window ends after it" << 16 | "first atom of the string" << 17
     const unsigned lim = raw ? 4u : MAX_ATOM_BYTES;   // raw: '▁' + one code point must fit 8 bytes
     bool bad = false;
@@ -538,7 +540,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
 #pragma unroll
             for (int g = 0; g < NG; g++) imax = max(imax, uni(SS[g].n_atoms));
             // Steps past a slot's own n_atoms (up to the wave's imax <= CH) compute garbage that
-            // lands in gem[]/wfin[] entries nobody reads, so the loop body has no per-slot guard.
+            // lands in fin[] entries nobody reads, so the loop body has no per-slot guard.
             // Recording the edges (f1) and the uncapped DP (f2) are hoisted out as loop versions.
             auto forward = [&](auto EDGES, auto UNCAPPED) {
                 constexpr bool edges = decltype(EDGES)::value, unc = decltype(UNCAPPED)::value;
@@ -570,11 +572,11 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                         const uint64_t emb = ballot((key ^ r) < 0x8000u);
                         if (d == 0) {
                             const unsigned sh = 16u * mg;
-                            const unsigned em16 = (unsigned)(emb >> sh) & 0xFFFFu;
-                            L.gem[i].v = ((unsigned)(gmb >> sh) & 0xFFFFu) | (em16 << 16);
-                            L.wfin[i] = Wfin<G>::pack(r);
+                            const unsigned gs = (unsigned)(gmb >> sh), es = (unsigned)(emb >> sh);
+                            const unsigned dg = (unsigned)__builtin_ctz(gs | 0x10000u), de = (unsigned)__builtin_ctz(es | 0x10000u);
+                            L.fin[i].v = dg | (de << 5) | ((unsigned)Wfin<G>::pack(r) << 16);
                             if constexpr (edges)
-                                if (i <= na) a.edges[SS[mg].sb + SS[mg].abase + i - 1] = em16;
+                                if (i <= na) a.edges[SS[mg].sb + SS[mg].abase + i - 1] = es & 0xFFFFu;
                         }
                         const bool wend = (cur & CP_WS) != 0;   // word starts and the window end
                         ws = wend ? i : ws;
@@ -605,9 +607,10 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                         const uint64_t gmb = ballot(key == r);
                         const uint64_t emb = ballot((key ^ r) < 0x8000u);
                         if (lane == 0) {
-                            L.gem[i].gm = gmb;
-                            L.gem[i].em = emb;
-                            L.wfin[i] = Wfin<G>::pack(r);
+                            const unsigned dg = gmb ? (unsigned)__builtin_ctzll(gmb) : 64u;
+                            const unsigned de = emb ? (unsigned)__builtin_ctzll(emb) : 64u;
+                            L.fin[i].d = dg | (de << 8);
+                            L.fin[i].w = Wfin<G>::pack(r);
                             if constexpr (edges)
                                 if (i <= na) a.edges[SS[0].sb + SS[0].abase + i - 1] = emb;
                         }
@@ -635,7 +638,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
         STAMP(2);
 
         // ---------------------------------------------------------- C0: per-window token counts and validity
-        // (word w ends at atom wsl[w+1]; its final state is wfin[wsl[w+1]])
+        // (word w ends at atom wsl[w+1]; its final state is in fin[wsl[w+1]])
         {
             unsigned pre[NG + 1];
             pre[0] = 0;
@@ -653,7 +656,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 unsigned cost = 0, inv = 0;
                 if (u < total) {
                     const GL &L = grp(g);
-                    const typename Wfin<G>::T F = L.wfin[L.wsl[u - wbase + 1]];
+                    const typename Wfin<G>::T F = GR::wfin(L.fin[L.wsl[u - wbase + 1]]);
                     cost = Wfin<G>::cost(F);
                     inv = Wfin<G>::invalid(F) ? 1u : 0u;
                 }
@@ -697,7 +700,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                     if (g == (unsigned)k) { wbase = pre[k]; tbase = tokpre[k]; ginv = inv_g[k]; }
                 GL &L = grp(g);
                 const unsigned w = u - wbase;
-                const typename Wfin<G>::T F = in ? L.wfin[L.wsl[w + 1]] : (typename Wfin<G>::T)0;
+                const typename Wfin<G>::T F = in ? GR::wfin(L.fin[L.wsl[w + 1]]) : (typename Wfin<G>::T)0;
                 const unsigned cost = in ? Wfin<G>::cost(F) : 0u;
                 const unsigned incl = wave_incl_scan_add(cost);
                 const unsigned tok_base = carry + incl - cost - tbase;
@@ -709,14 +712,12 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                     unsigned c = cost, A = 0;
                     unsigned pend = L.rec[i].cpos & 0x7FFFu;
                     while (i > ws) {
-                        const typename GR::Gem gem = L.gem[i];
+                        const typename GR::Fin f = L.fin[i];
                         const unsigned cpi = L.rec[i].cpos & 0x7FFFu;
                         const unsigned sp = pend - cpi;
                         A = A > sp ? A : sp;                 // the token emitted last step ended at pend
-                        const M sel = (M)(A < Ls ? GR::gm(gem) : GR::em(gem));
-                        const unsigned dd = (G == 64) ? (unsigned)__builtin_ctzll((uint64_t)sel | (1ull << 63))
-                                                      : (unsigned)__builtin_ctz((unsigned)sel | 0x80000000u);
-                        if (sel == 0 || dd + 1 > i - ws || c == 0) break;   // unreachable by Appendix A
+                        const unsigned dd = A < Ls ? GR::dg(f) : GR::de(f);
+                        if (dd >= (unsigned)G || dd + 1 > i - ws || c == 0) break;   // unreachable by Appendix A
                         const unsigned j = i - 1 - dd;
                         c--;
                         L.rec[tok_base + c].smask = (M)j;   // span masks are dead after B
