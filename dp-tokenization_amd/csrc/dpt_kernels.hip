@@ -114,7 +114,7 @@ __device__ __forceinline__ void wave_sync() {
 
 template <int G> struct Group;
 
-// G = 16: four strings per wave, one per DPP row.  Per atom: {cpos, span mask} in one
+// G = 16: four strings per wave, one per DPP row.  Per atom: {cpos, ~span mask} in one
 // dword; per end position i, one dword `fin`: the back distances (minus one) of the largest
 // reachable j in E(i) attaining G[i] (dg) and of the largest reachable j in E(i) (de) --
 // G when there is none -- and the final state when i ends a word (Wfin<16>).
@@ -122,9 +122,9 @@ template <> struct Group<16> {
     using M = uint16_t;  // span mask: bit L-1 = an L-atom token starts here
     struct Rec { uint16_t cpos; uint16_t smask; };
     struct Fin { uint32_t v; };
-    static __device__ __forceinline__ unsigned dg(const Fin &x) { return x.v & 31u; }
-    static __device__ __forceinline__ unsigned de(const Fin &x) { return (x.v >> 5) & 31u; }
-    static __device__ __forceinline__ uint16_t wfin(const Fin &x) { return (uint16_t)(x.v >> 16); }
+    static __device__ __forceinline__ unsigned dg(const Fin &x) { return (x.v >> 5) & 31u; }
+    static __device__ __forceinline__ unsigned de(const Fin &x) { return (x.v >> 10) & 31u; }
+    static __device__ __forceinline__ uint32_t wfin(const Fin &x) { return x.v; }
 };
 
 // G = 64: one string per wave (vocabularies with tokens of 17..64 code points).
@@ -142,15 +142,13 @@ template <> struct Group<64> {
 constexpr uint16_t CP_WS = 0x8000;        // cpos bit: atom starts a word
 constexpr unsigned MAX_ATOM_BYTES = 8;    // expanded atom = one u64 (raw: '▁'+4-byte code point = 7)
 
-// final state at a word end: G = 16 packs cost (<= 1023) | invalid | 31-G (G <= 16) in 16 bits
-// (straight from the key: its low 5 bits are 31-G, bit 15 the invalid flag)
+// final state at a word end.  G = 16: fin[i] itself -- the group-min key with the back
+// distances in its constant bits 5..14: cost << 16 | invalid << 15 | de << 10 | dg << 5 | 31-G
 template <int G> struct Wfin;
 template <> struct Wfin<16> {
-    using T = uint16_t;
-    static __device__ __forceinline__ T pack(unsigned r) { return (T)(((r >> 10) & 0xFFE0u) | (r & 31u)); }
-    // 1023 = the uncapped DP's "inf" (0xFFFF, inspect_tokenizer.py:80); capped costs stay <= CH
-    static __device__ __forceinline__ unsigned cost(T x) { return (x >> 6) == 1023u ? 0xFFFFu : (x >> 6); }
-    static __device__ __forceinline__ bool invalid(T x) { return (x >> 5) & 1u; }
+    using T = uint32_t;
+    static __device__ __forceinline__ unsigned cost(T x) { return x >> 16; }
+    static __device__ __forceinline__ bool invalid(T x) { return (x >> 15) & 1u; }
     static __device__ __forceinline__ unsigned gmax(T x) { return 31u - (x & 31u); }
 };
 template <> struct Wfin<64> {
@@ -369,6 +367,10 @@ __device__ bool prep_window(GroupLDS<CH, G> &L, const uint8_t *str, const uint8_
 
 // ------------------------------------------------------------------ the tokenize kernel
 
+#ifndef A_WALKS
+#define A_WALKS 2   // concurrent trie walks per lane in phase A
+#endif
+
 template <int CH, int G, bool BIG>
 __global__ void __launch_bounds__(64)
 tokenize_kernel(EncodeArgs a, TrieView tv) {
@@ -459,74 +461,87 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
 #pragma unroll
             for (int g = 0; g < NG; g++) pre[g + 1] = pre[g] + uni(SS[g].n_atoms);
             const unsigned total = pre[NG];
-            unsigned gsel = 0, j = 0;
-            auto locate = [&](unsigned uu) {
-                gsel = 0;
+            // Each lane runs A_WALKS independent walks so that as many trie loads are in flight.
+            // Walk state: start atom j of group gsel, atoms matched so far (len), the trie node,
+            // the expanded bytes left of the current atom (seq, cnt) and of the next one (prefetched).
+            struct Walk {
+                unsigned gsel, j, len, cnt, ncnt;
+                int32_t nb, node;
+                uint32_t info, ninfo;
+                uint64_t seq, nseq;
+                M mask;
+                bool active;
+            };
+            auto start = [&](Walk &w, unsigned uu) {
+                unsigned gs = 0;
 #pragma unroll
-                for (int g = 1; g < NG; g++) gsel += uu >= pre[g] ? 1u : 0u;
+                for (int g = 1; g < NG; g++) gs += uu >= pre[g] ? 1u : 0u;
                 unsigned base = 0;
 #pragma unroll
-                for (int g = 0; g < NG; g++) base = (gsel == (unsigned)g) ? pre[g] : base;
-                j = uu - base;
+                for (int g = 0; g < NG; g++) base = (gs == (unsigned)g) ? pre[g] : base;
+                w.gsel = gs;
+                w.j = uu - base;
+                GL &L = grp(gs);
+                w.info = ainfo(L, w.j);
+                w.seq = atom_from_info(L.bytes, w.info, raw, w.cnt);
+                if (!(w.info & 0x10000u)) { w.ninfo = ainfo(L, w.j + 1); w.nseq = atom_from_info(L.bytes, w.ninfo, raw, w.ncnt); }
+                w.nb = tv.root_base; w.node = 0; w.len = 0; w.mask = 0;
             };
-            // lane state: start atom j of group gsel, atoms matched so far (len), the trie node, the
-            // expanded bytes left of the current atom (seq, cnt) and those of the next one (prefetched)
-            unsigned u = lane;
-            bool active = u < total;
-            int32_t nb = tv.root_base, node = 0;
-            unsigned len = 0, mask = 0, cnt = 0, ncnt = 0;
-            uint32_t info = 0, ninfo = 0;
-            uint64_t mask64 = 0, seq = 0, nseq = 0;
-            auto start = [&]() {
-                locate(u);
-                GL &L = grp(gsel);
-                info = ainfo(L, j);
-                seq = atom_from_info(L.bytes, info, raw, cnt);
-                if (!(info & 0x10000u)) { ninfo = ainfo(L, j + 1); nseq = atom_from_info(L.bytes, ninfo, raw, ncnt); }
-            };
-            if (active) start();
-            unsigned nxt = 64;
-            while (ballot(active)) {
-                bool done = false;
-                if (active) {
-                    const int32_t t = nb + (int32_t)(seq & 0xFFu);
-                    const int2 ent = tv.slots[t];
-                    seq >>= 8;
-                    cnt--;
-                    if (ent.y != node) {
-                        done = true;
-                    } else {
-                        node = t;
-                        nb = ent.x & 0x7FFFFFFF;
-                        if (cnt == 0) {   // atom j+len-1 ends: the span j..j+len is a candidate token
-                            len++;
-                            if (ent.x & TERM_BIT) {
-                                if (G == 64) mask64 |= 1ull << (len - 1);
-                                else mask |= 1u << (len - 1);
-                            }
-                            if ((info & 0x10000u) || len == (unsigned)G) {
-                                done = true;
-                            } else {
-                                info = ninfo; seq = nseq; cnt = ncnt;
-                                if (!(info & 0x10000u) && len + 1 < (unsigned)G) {
-                                    GL &L = grp(gsel);
-                                    ninfo = ainfo(L, j + len + 1);
-                                    nseq = atom_from_info(L.bytes, ninfo, raw, ncnt);
+            Walk W[A_WALKS];
+#pragma unroll
+            for (int q = 0; q < A_WALKS; q++) {
+                W[q].active = q * 64u + lane < total;
+                if (W[q].active) start(W[q], q * 64u + lane);
+            }
+            unsigned nxt = A_WALKS * 64u;
+            for (;;) {
+                bool any = false;
+#pragma unroll
+                for (int q = 0; q < A_WALKS; q++) any |= W[q].active;
+                if (!ballot(any)) break;
+                int2 ent[A_WALKS];
+#pragma unroll
+                for (int q = 0; q < A_WALKS; q++)   // issue every walk's load before using any
+                    ent[q] = tv.slots[W[q].active ? W[q].nb + (int32_t)(W[q].seq & 0xFFu) : 0];
+#pragma unroll
+                for (int q = 0; q < A_WALKS; q++) {
+                    Walk &w = W[q];
+                    bool done = false;
+                    if (w.active) {
+                        const int32_t t = w.nb + (int32_t)(w.seq & 0xFFu);
+                        w.seq >>= 8;
+                        w.cnt--;
+                        if (ent[q].y != w.node) {
+                            done = true;
+                        } else {
+                            w.node = t;
+                            w.nb = ent[q].x & 0x7FFFFFFF;
+                            if (w.cnt == 0) {   // atom j+len-1 ends: the span j..j+len is a candidate token
+                                w.len++;
+                                if (ent[q].x & TERM_BIT) w.mask |= (M)1 << (w.len - 1);
+                                if ((w.info & 0x10000u) || w.len == (unsigned)G) {
+                                    done = true;
+                                } else {
+                                    w.info = w.ninfo; w.seq = w.nseq; w.cnt = w.ncnt;
+                                    if (!(w.info & 0x10000u) && w.len + 1 < (unsigned)G) {
+                                        GL &L = grp(w.gsel);
+                                        w.ninfo = ainfo(L, w.j + w.len + 1);
+                                        w.nseq = atom_from_info(L.bytes, w.ninfo, raw, w.ncnt);
+                                    }
                                 }
                             }
                         }
                     }
+                    const uint64_t dm = ballot(done);
+                    if (done) {
+                        grp(w.gsel).rec[w.j].smask = G == 16 ? (M)~w.mask : w.mask;   // B (G = 16) reads it inverted
+                        const unsigned rank = __builtin_amdgcn_mbcnt_hi((unsigned)(dm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)dm, 0u));
+                        const unsigned uu = nxt + rank;
+                        w.active = uu < total;
+                        if (w.active) start(w, uu);
+                    }
+                    nxt += (unsigned)__builtin_popcountll(dm);
                 }
-                const uint64_t dm = ballot(done);
-                if (done) {
-                    if (G == 64) grp(gsel).rec[j].smask = (M)mask64;
-                    else grp(gsel).rec[j].smask = (M)mask;
-                    const unsigned rank = __builtin_amdgcn_mbcnt_hi((unsigned)(dm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)dm, 0u));
-                    u = nxt + rank;
-                    active = u < total;
-                    if (active) { start(); nb = tv.root_base; node = 0; len = 0; mask = 0; mask64 = 0; }
-                }
-                nxt += (unsigned)__builtin_popcountll(dm);
             }
         }
         wave_sync();
@@ -550,22 +565,29 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 unsigned st = d == 0 ? ST0 : 0u;
                 unsigned cpj = 0;
                 if constexpr (G == 16) {
+                    // Lane d carries x = rec[j] = {cpos[j], ~smask[j]} (one DPP shift moves both) and
+                    // its state in key form: (cost[j]+1) << 16 | invalid[j] << 15 | (0x7FFF - G[j]),
+                    // so the candidate key is min(st, (st | 0x7FFF) - span) and a dead span is one
+                    // sign-extended bit of x.
+                    constexpr unsigned SK0 = 0x17FFFu;   // word start in key form
                     const uint32_t *rec32 = reinterpret_cast<const uint32_t *>(L.rec);
-                    const uint32_t r0 = rec32[0];
-                    const unsigned bitd = 1u << d;
-                    unsigned m = (d == 0 && na > 0) ? (r0 >> 16) : 0u;
+                    const unsigned sbit = 16u + d;
+                    unsigned sk = d == 0 ? SK0 : 0u;
+                    unsigned x = d == 0 ? rec32[0] : 0xFFFF0000u;
+                    unsigned wsh = 0;                    // word start << 16
                     uint32_t nx = rec32[1];
-                    for (unsigned i = 1; i <= imax; i++) {
+                    // one step; (sk, x) in, (sk', x') out -- called alternately on two register sets
+                    // so the DPP shifts need no copies
+                    auto step = [&](unsigned i, unsigned skI, unsigned xI, unsigned &skO, unsigned &xO) {
                         const uint32_t cur = nx;
                         nx = rec32[i + 1];                         // i+1 <= CH+1 < NA: always in bounds
-                        const unsigned cpi = cur & 0x7FFFu;
-                        const unsigned span = cpi - cpj;
-                        const unsigned gj = st & 0x7FFFu;
-                        const unsigned kv = (st | 0x7FFFu) - (gj > span ? gj : span);
-                        const unsigned key = (m & bitd) ? kv : 0xFFFFFFFFu;
+                        const unsigned span = (cur - xI) & 0x7FFFu;  // cp(j..i); borrows only move up
+                        unsigned kv = (skI | 0x7FFFu) - span;
+                        kv = skI < kv ? skI : kv;
+                        const unsigned key = kv | (unsigned)__builtin_amdgcn_sbfe((int)xI, sbit, 1);
                         unsigned r = row_min_u32(key);
                         if constexpr (!unc) {
-                            const unsigned capkey = ((i - ws) << 16) | 0xFFFFu;
+                            const unsigned capkey = ((i << 16) | 0xFFFFu) - wsh;
                             r = r < capkey ? r : capkey;
                         }
                         const uint64_t gmb = ballot(key == r);
@@ -574,19 +596,24 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                             const unsigned sh = 16u * mg;
                             const unsigned gs = (unsigned)(gmb >> sh), es = (unsigned)(emb >> sh);
                             const unsigned dg = (unsigned)__builtin_ctz(gs | 0x10000u), de = (unsigned)__builtin_ctz(es | 0x10000u);
-                            L.fin[i].v = dg | (de << 5) | ((unsigned)Wfin<G>::pack(r) << 16);
+                            L.fin[i].v = (r & 0xFFFF801Fu) | (dg << 5) | (de << 10);
                             if constexpr (edges)
                                 if (i <= na) a.edges[SS[mg].sb + SS[mg].abase + i - 1] = es & 0xFFFFu;
                         }
                         const bool wend = (cur & CP_WS) != 0;   // word starts and the window end
-                        ws = wend ? i : ws;
-                        unsigned nxt = (r ^ 0x7FFFu) + 0x10000u;
+                        wsh = wend ? (i << 16) : wsh;
+                        unsigned nxt = r + 0x10000u;
                         if constexpr (unc) nxt = r >= 0xFFFE0000u ? 0xFFFF8000u : nxt;   // unreachable: cost stays inf
-                        const unsigned sin = wend ? ST0 : nxt;
-                        st = row_shift_in(st, sin);
-                        cpj = row_shift_in(cpj, cpi);
-                        m = row_shift_in(m, cur >> 16);
+                        skO = row_shift_in(skI, wend ? SK0 : nxt);
+                        xO = row_shift_in(xI, cur);
+                    };
+                    unsigned sk2, x2;
+                    unsigned i = 1;
+                    for (; i + 1 <= imax; i += 2) {
+                        step(i, sk, x, sk2, x2);
+                        step(i + 1, sk2, x2, sk, x);
                     }
+                    if (i <= imax) step(i, sk, x, sk2, x2);
                 } else {
                     const uint64_t m0 = na > 0 ? L.rec[0].smask : 0ull;
                     unsigned mlo = d == 0 ? (unsigned)m0 : 0u, mhi = d == 0 ? (unsigned)(m0 >> 32) : 0u;
