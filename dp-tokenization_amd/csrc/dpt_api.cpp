@@ -132,7 +132,6 @@ int kernel_variant(uint32_t max_cp) {
         if (!strcmp(e, "rows16")) v = dpt::KERNEL_ROWS16;
         else if (!strcmp(e, "rows64")) v = dpt::KERNEL_ROWS64;
         else if (!strcmp(e, "lane")) v = dpt::KERNEL_LANE;
-        else if (!strcmp(e, "rows16w128")) v = dpt::KERNEL_ROWS16_128;
     }
     if (max_cp > 16) v = dpt::KERNEL_ROWS64;
     return v;

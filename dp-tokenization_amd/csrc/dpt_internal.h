@@ -41,7 +41,6 @@ struct EncodeLaunch {
 constexpr int KERNEL_LANE = 0;    // lane per string, register ring of 16 walks (vocab max_cp <= 16)
 constexpr int KERNEL_ROWS16 = 1;  // 4 strings per wave in 16-lane DPP rows, LDS windows (max_cp <= 16)
 constexpr int KERNEL_ROWS64 = 2;  // 1 string per wave, 64-lane DPP (max_cp <= 64)
-constexpr int KERNEL_ROWS16_128 = 3;  // rows16 with 128-byte windows (half the LDS per slot)
 
 hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t ev[6]);
 void launch_lane(const EncodeLaunch &p, unsigned blocks, hipStream_t stream);

@@ -258,24 +258,65 @@ __device__ __forceinline__ uint64_t atom_from_info(const uint8_t *bytes, uint32_
 
 // ------------------------------------------------------------------ prep: one slot's window
 
+// The bytes (and cut-mask bytes) of a window, in registers: lane l holds bytes
+// [256c + 4l, 256c + 4l + 4) of chunk c, little-endian; *_end is the byte at CH (the probe
+// for the last word start when the string continues past the window).
+template <int CH> struct WinRegs {
+    static constexpr int NC = CH / 256;
+    uint32_t t[NC], c[NC];
+    uint32_t t_end, c_end;
+};
+
+__device__ __forceinline__ uint32_t load_u32_at(__amdgpu_buffer_rsrc_t r, unsigned off, unsigned sh) {
+    const uint32_t lo = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+    const uint32_t hi = __builtin_amdgcn_raw_buffer_load_b32(r, off + 4u, 0, 0);
+    return __builtin_amdgcn_alignbyte(hi, lo, sh);
+}
+
+// Aligned dword buffer loads over [base + pos, base + slen): bytes past the string's last
+// aligned dword read as 0 (buffer range check), and no load leaves that dword, so no load
+// can touch a page the string does not.
+template <int CH>
+__device__ __forceinline__ void load_window_bytes(const uint8_t *base, uint64_t pos, uint64_t slen, unsigned lane,
+                                                  uint32_t (&out)[CH / 256], uint32_t &end) {
+    const uint8_t *p = base + pos;
+    const unsigned sh = (unsigned)((uintptr_t)p & 3u);
+    uint64_t n = (slen - pos + sh + 3u) & ~(uint64_t)3;
+    if (n > (uint64_t)(CH + 16)) n = CH + 16;
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)(p - sh), (short)0, (int)n, 0x00020000);
+#pragma unroll
+    for (int c = 0; c < CH / 256; c++) out[c] = load_u32_at(r, c * 256u + lane * 4u, sh);
+    end = load_u32_at(r, (unsigned)CH, sh) & 0xFFu;
+}
+
+template <int CH>
+__device__ __forceinline__ void load_window(WinRegs<CH> &W, const uint8_t *str, const uint8_t *cut, uint64_t pos,
+                                            uint64_t slen, bool raw, unsigned lane) {
+    load_window_bytes<CH>(str, pos, slen, lane, W.t, W.t_end);
+    if (!raw) load_window_bytes<CH>(cut, pos, slen, lane, W.c, W.c_end);
+}
+
+__device__ __forceinline__ bool is_word_start(unsigned b, unsigned cm, int mode) {
+    return mode == 0 ? (b == ' ') : (mode == 1 ? (cm != 0 && (b & 0xC0u) != 0x80u) : (cm & 1u) != 0);
+}
+
 // Finds the window [pos, pos+wlen) (ends at a word start or at the string end).
 // Returns false when a single word does not fit in CH bytes.
 template <int CH>
-__device__ bool window_bounds(const uint8_t *str, const uint8_t *cut, uint64_t slen, uint64_t pos, int mode,
-                              unsigned lane, unsigned &wlen) {
+__device__ bool window_bounds(const WinRegs<CH> &W, uint64_t slen, uint64_t pos, int mode, unsigned lane, unsigned &wlen) {
     const uint64_t rem = slen - pos;
     if (rem <= (uint64_t)CH) {
         wlen = (unsigned)rem;
         return true;
     }
-    int best = -1;
-    for (int k = lane; k <= CH; k += 64) {
-        if (k == 0) continue;
-        const uint64_t p = pos + k;
-        const uint8_t b = str[p];
-        const bool ws = mode == 0 ? (b == ' ') : (mode == 1 ? (cut[p] != 0 && (b & 0xC0) != 0x80) : (cut[p] & 1) != 0);
-        if (ws) best = k;
-    }
+    int best = is_word_start(W.t_end, W.c_end, mode) ? CH : -1;
+#pragma unroll
+    for (int c = 0; c < CH / 256; c++)
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int k = c * 256 + (int)lane * 4 + u;
+            if (k > 0 && is_word_start((W.t[c] >> (8 * u)) & 0xFFu, (W.c[c] >> (8 * u)) & 0xFFu, mode)) best = max(best, k);
+        }
     const unsigned q = wave_max_u32((unsigned)(best + 1));
     if (q == 0) return false;
     wlen = q - 1;
@@ -284,25 +325,26 @@ __device__ bool window_bounds(const uint8_t *str, const uint8_t *cut, uint64_t s
 
 // Atomise window bytes [pos, pos+wlen) into L: the bytes themselves, atom byte offsets,
 // code-point prefixes (+ word-start bits) and the word list.  One packed DPP scan per 256
-// bytes.  Returns false if an atom is longer than MAX_ATOM_BYTES (ATOMS mode only).
+// bytes.  Returns false if an atom is longer than MAX_ATOM_BYTES (4 bytes in RAW mode).
 template <int CH, int G>
-__device__ bool prep_window(GroupLDS<CH, G> &L, const uint8_t *str, const uint8_t *cut, uint64_t pos,
+__device__ bool prep_window(GroupLDS<CH, G> &L, const WinRegs<CH> &W, uint64_t pos,
                             unsigned wlen, int mode, unsigned lane, unsigned &n_atoms_o, unsigned &n_words_o) {
     const bool raw = mode == 0;
     unsigned n_atoms = 0, cp_tot = 0, n_words = 0;
-    for (unsigned c0 = 0; c0 < wlen; c0 += 256) {
+#pragma unroll
+    for (int c = 0; c < CH / 256; c++) {
+        const unsigned c0 = c * 256u;
+        if (c0 >= wlen) break;
         bool ast[4], wst[4];
         unsigned cpl[4];
-        unsigned word = 0;
         unsigned a_sum = 0, w_sum = 0, cp_sum = 0;
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             const unsigned k = c0 + lane * 4 + u;
             const bool in = k < wlen;
-            const uint64_t p = pos + k;
-            const uint8_t b = in ? str[p] : 0;
-            const uint8_t cm = (in && !raw) ? cut[p] : 0;
-            const bool first = in && p == 0;
+            const unsigned b = (W.t[c] >> (8 * u)) & 0xFFu;
+            const unsigned cm = raw ? 0u : (W.c[c] >> (8 * u)) & 0xFFu;
+            const bool first = in && pos + k == 0;
             // mode 2 (ATOMS): atom starts come from the mask (bit 1), word starts from bit 0
             const bool cont = in && !first && (mode == 2 ? (cm & 3) == 0 : (b & 0xC0) == 0x80);
             const bool as = in && !cont;
@@ -315,7 +357,6 @@ __device__ bool prep_window(GroupLDS<CH, G> &L, const uint8_t *str, const uint8_
                 wsf = as && (k == 0 || (mode == 1 ? cm != 0 : (cm & 1) != 0));
                 cl = (in && (b & 0xC0) != 0x80) ? 1 : 0;   // code points, whatever the atoms
             }
-            word |= (unsigned)b << (8 * u);
             ast[u] = as; wst[u] = wsf; cpl[u] = cl;
             a_sum += as; w_sum += wsf; cp_sum += cl;
         }
@@ -327,7 +368,7 @@ __device__ bool prep_window(GroupLDS<CH, G> &L, const uint8_t *str, const uint8_
         unsigned ai = n_atoms + (ex & 0x1FFu);
         unsigned wi = n_words + ((ex >> 9) & 0x1FFu);
         unsigned cp = cp_tot + (ex >> 18);
-        if (c0 + lane * 4 < wlen) *reinterpret_cast<uint32_t *>(&L.bytes[c0 + lane * 4]) = word;
+        if (c0 + lane * 4 < wlen) *reinterpret_cast<uint32_t *>(&L.bytes[c0 + lane * 4]) = W.t[c];
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             const unsigned k = c0 + lane * 4 + u;
@@ -399,39 +440,61 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
 
     for (;;) {
         // ---------------------------------------------------------- slots: fetch strings, find windows, prep
-        unsigned busy = 0;
-        for (unsigned g = 0; g < (unsigned)NG; g++) {
-            GL &L = grp(g);
-            SlotState &S = SS[g];
-            for (;;) {
-                if (!uni(S.active)) {
-                    if (exhausted) break;
-                    unsigned idx = 0;
-                    if (lane == 0) idx = atomicAdd(a.work_next, 1u);
-                    idx = __builtin_amdgcn_readlane(idx, 0);
-                    if ((uint64_t)idx >= n_work) { exhausted = true; break; }
-                    const uint64_t s = BIG ? (uint64_t)a.work_list[idx] : (uint64_t)idx;
-                    const uint64_t sb = a.str_off[s] - base_off;
-                    const uint64_t sl = a.str_off[s + 1] - a.str_off[s];
-                    if (lane == 0) {
-                        S.s = s; S.sb = sb; S.slen = sl; S.pos = 0; S.active = 1;
-                        S.status = sl == 0 ? 2u : 0u;  // pretokenize_raw('') == [[]] -> IndexError
+        // Inactive slots are refilled together (one counter atomic, offsets loaded by one lane
+        // per slot), and every slot's window bytes are loaded before any is atomised, so the
+        // HBM round trips of the NG slots overlap.
+        unsigned busy = 0, prepared = 0;
+        for (;;) {
+            unsigned need = 0;
+#pragma unroll
+            for (int g = 0; g < NG; g++) need |= uni(SS[g].active) ? 0u : (1u << g);
+            if (need && !exhausted) {
+                const unsigned n_need = (unsigned)__builtin_popcount(need);
+                unsigned base = 0;
+                if (lane == 0) base = atomicAdd(a.work_next, n_need);
+                base = __builtin_amdgcn_readlane(base, 0);
+                if ((uint64_t)base + n_need >= n_work) exhausted = true;
+                if (lane < (unsigned)NG && ((need >> lane) & 1u)) {
+                    const uint64_t idx = (uint64_t)base + (unsigned)__builtin_popcount(need & ((1u << lane) - 1u));
+                    if (idx < n_work) {
+                        const uint64_t s = BIG ? (uint64_t)a.work_list[idx] : idx;
+                        const uint64_t o0 = a.str_off[s], o1 = a.str_off[s + 1];
+                        SlotState &S = SS[lane];
+                        S.s = s; S.sb = o0 - base_off; S.slen = o1 - o0; S.pos = 0; S.active = 1;
+                        S.status = o1 == o0 ? 2u : 0u;  // pretokenize_raw('') == [[]] -> IndexError
                         S.ntok = 0; S.capsum = 0; S.abase = 0;
                     }
-                    wave_sync();
                 }
-                const uint64_t sb = uni64(S.sb), slen = uni64(S.slen), pos = uni64(S.pos);
+                wave_sync();
+            }
+            unsigned todo = 0;
+#pragma unroll
+            for (int g = 0; g < NG; g++) todo |= (uni(SS[g].active) && !((prepared >> g) & 1u)) ? (1u << g) : 0u;
+            if (!todo) break;
+            WinRegs<CH> W[NG];
+#pragma unroll
+            for (int g = 0; g < NG; g++) {
+                if (!((todo >> g) & 1u)) continue;
+                const uint64_t sb = uni64(SS[g].sb);
+                load_window<CH>(W[g], a.text + sb, raw ? nullptr : a.cut_mask + sb, uni64(SS[g].pos), uni64(SS[g].slen), raw, lane);
+            }
+            bool refill = false;
+#pragma unroll
+            for (int g = 0; g < NG; g++) {
+                if (!((todo >> g) & 1u)) continue;
+                GL &L = grp(g);
+                SlotState &S = SS[g];
+                const uint64_t slen = uni64(S.slen), pos = uni64(S.pos);
                 unsigned status = uni(S.status);
-                const uint8_t *str = a.text + sb;
-                const uint8_t *cut = raw ? nullptr : a.cut_mask + sb;
                 unsigned wlen = 0, na = 0, nw = 0;
                 bool ok = status != 2;
-                if (ok) ok = window_bounds<CH>(str, cut, slen, pos, mode, lane, wlen);
-                if (ok) ok = prep_window<CH, G>(L, str, cut, pos, wlen, mode, lane, na, nw);
+                if (ok) ok = window_bounds<CH>(W[g], slen, pos, mode, lane, wlen);
+                if (ok) ok = prep_window<CH, G>(L, W[g], pos, wlen, mode, lane, na, nw);
                 if (ok) {
                     if (lane == 0) { S.wlen = wlen; S.n_atoms = na; S.n_words = nw; S.wtok = 0; S.inval = 0; }
+                    prepared |= 1u << g;
                     busy++;
-                    break;
+                    continue;
                 }
                 // the string ends here: empty, or a word too long for this pass
                 if (status != 2) status = 3;
@@ -446,10 +509,12 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                     if (a.capped) a.capped[s] = status == 2 ? 0 : -1;
                     S.active = 0;
                 }
-                wave_sync();
+                refill = true;
             }
-            if (lane == 0 && !S.active) { S.n_atoms = 0; S.n_words = 0; }
+            wave_sync();
+            if (!refill || exhausted) break;
         }
+        if (lane < (unsigned)NG && !((prepared >> lane) & 1u)) { SS[lane].n_atoms = 0; SS[lane].n_words = 0; }
         wave_sync();
         if (busy == 0) break;
         STAMP(0);
@@ -928,7 +993,6 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
         } else {
             const unsigned n_cu = p.max_blocks / 64;
             if (p.variant == KERNEL_ROWS16) launch_tok<SMALL_CH, 16, false>(a, tv, (p.n_str + 3) / 4, n_cu, stream);
-            else if (p.variant == KERNEL_ROWS16_128) launch_tok<128, 16, false>(a, tv, (p.n_str + 3) / 4, n_cu, stream);
             else launch_tok<SMALL_CH, 64, false>(a, tv, p.n_str, n_cu, stream);
         }
         // second pass over the strings whose single word (or expansion) did not fit the small window
