@@ -96,6 +96,21 @@ def cpu_baseline(texts, budget, cores):
     return done_bytes / dt, n_done, n_to, dt
 
 
+def traffic_for(n_str: int, lb: int):
+    """HBM bytes per tokenize launch measured by tools/pmc_traffic.py (PMC FETCH_SIZE x2 +
+    WRITE_SIZE) -- only when it was measured on these kernel sources and this workload."""
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        from pmc_traffic import source_hash
+        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as fh:
+            rec = json.load(fh)
+        if rec.get("source_sha256") == source_hash() and rec.get("n_str") == n_str and lb == 256:
+            return rec["traffic_bytes_per_launch"]
+    except (OSError, ValueError, KeyError, ImportError):
+        pass
+    return None
+
+
 def main():
     args = parse()
     import torch
@@ -221,8 +236,8 @@ def main():
             "stage_ms_per_step": {"tokenize": ms_stage[0] / max(launches, 1), "scan": ms_stage[1] / max(launches, 1),
                                   "compact": ms_stage[2] / max(launches, 1)},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "tokenize_kernel<256,4>", "alg_bytes_per_launch": alg_bytes},
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic_for(M, Lb),
+                         "kernel": "tokenize_kernel<256,16,false>", "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -1,0 +1,58 @@
+"""HBM traffic of the tokenize kernel per launch from rocprofv3 PMC passes.
+
+Usage (GPU box):  python tools/pmc_traffic.py [N] [tag]
+Runs two separate `rocprofv3 --kernel-trace --pmc` passes (FETCH_SIZE, WRITE_SIZE -- they do
+not fit one pass) over tools/prof_driver.py on the bench workload, then writes
+profiles/pmc_traffic.json:  FETCH_SIZE x 2 (the gfx950 correction of MI355X_MICROARCH.md
+§HBM) + WRITE_SIZE, KB -> bytes, mean over the dispatches of the first-pass tokenize kernel,
+keyed by the sha256 of the kernel sources so bench.py only reports it for the same code.
+"""
+import csv, glob, hashlib, json, os, subprocess, sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = ["dpt_kernels.hip", "dpt_lane.hip", "dpt_api.cpp", "dpt_vocab.cpp", "dpt_internal.h"]
+
+
+def source_hash() -> str:
+    h = hashlib.sha256()
+    for f in SRC:
+        with open(os.path.join(ROOT, "dp-tokenization_amd", "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def run_pass(counter: str, n: int, out: str) -> float:
+    env = dict(os.environ, TMPDIR="/tmp")
+    cmd = ["rocprofv3", "--kernel-trace", "--pmc", counter, "-d", out, "-o", "run", "--output-format", "csv",
+           "--", sys.executable, os.path.join(ROOT, "tools", "prof_driver.py"), str(n), "3", "ascii"]
+    with open(out + ".log", "w") as log:
+        subprocess.run(cmd, check=True, stdout=log, stderr=subprocess.STDOUT, env=env, timeout=600)
+    vals = []
+    for f in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
+        for row in csv.DictReader(open(f)):
+            if "tokenize_kernel" in row.get("Kernel_Name", "") and "true>" not in row["Kernel_Name"] \
+                    and row["Counter_Name"] == counter:
+                vals.append(float(row["Counter_Value"]))
+    if not vals:
+        raise RuntimeError("no %s samples for the tokenize kernel" % counter)
+    return sum(vals) / len(vals) * 1024.0   # KB -> bytes
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
+    tag = sys.argv[2] if len(sys.argv) > 2 else "traffic"
+    out = os.path.join(ROOT, "gpurun_out", "pmc_" + tag)
+    os.makedirs(out, exist_ok=True)
+    fetch = run_pass("FETCH_SIZE", n, os.path.join(out, "fetch"))
+    write = run_pass("WRITE_SIZE", n, os.path.join(out, "write"))
+    rec = {"source_sha256": source_hash(), "workload": "cfg2 %d x 256 B random ASCII" % n, "n_str": n,
+           "fetch_bytes_raw": fetch, "fetch_bytes": 2 * fetch, "write_bytes": write,
+           "traffic_bytes_per_launch": 2 * fetch + write,
+           "method": "rocprofv3 --kernel-trace --pmc FETCH_SIZE | WRITE_SIZE (separate passes); FETCH_SIZE x2 (gfx950)"}
+    with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as fh:
+        json.dump(rec, fh, indent=1)
+    print(json.dumps(rec))
+
+
+if __name__ == "__main__":
+    main()
