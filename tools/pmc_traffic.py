@@ -7,17 +7,27 @@ profiles/pmc_traffic.json:  FETCH_SIZE x 2 (the gfx950 correction of MI355X_MICR
 §HBM) + WRITE_SIZE, KB -> bytes, mean over the dispatches of the first-pass tokenize kernel,
 keyed by the sha256 of the kernel sources so bench.py only reports it for the same code.
 """
-import csv, glob, hashlib, json, os, subprocess, sys
+import csv, glob, hashlib, json, os, re, subprocess, sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = ["dpt_kernels.hip", "dpt_lane.hip", "dpt_api.cpp", "dpt_vocab.cpp", "dpt_internal.h"]
 
 
-def source_hash() -> str:
+def normalized(src: str) -> str:
+    """Source text without // comments and whitespace, so comment edits keep the key."""
+    return "".join(re.sub(r"//.*", "", line).split() and "".join(re.sub(r"//.*", "", line).split()) or ""
+                   for line in src.splitlines())
+
+
+def source_hash(read=None) -> str:
     h = hashlib.sha256()
     for f in SRC:
-        with open(os.path.join(ROOT, "dp-tokenization_amd", "csrc", f), "rb") as fh:
-            h.update(fh.read())
+        if read is None:
+            with open(os.path.join(ROOT, "dp-tokenization_amd", "csrc", f)) as fh:
+                src = fh.read()
+        else:
+            src = read(f)
+        h.update(normalized(src).encode())
     return h.hexdigest()
 
 
