@@ -15,8 +15,7 @@ SRC = ["dpt_kernels.hip", "dpt_lane.hip", "dpt_api.cpp", "dpt_vocab.cpp", "dpt_i
 
 def normalized(src: str) -> str:
     """Source text without // comments and whitespace, so comment edits keep the key."""
-    return "".join(re.sub(r"//.*", "", line).split() and "".join(re.sub(r"//.*", "", line).split()) or ""
-                   for line in src.splitlines())
+    return "".join("".join(re.sub(r"//.*", "", line).split()) for line in src.splitlines())
 
 
 def source_hash(read=None) -> str:
