@@ -168,9 +168,16 @@ struct GroupLDS {
     //         the first atom of selected token j (tokens tile the window)
     typename Group<G>::Rec rec[NA];
     typename Group<G>::Fin fin[NA];   // per end position, see Group<G>
-    uint16_t aoff[NA];              // atom -> byte offset in the window
-    uint16_t wsl[NA];               // word -> first atom
-    uint8_t bytes[CH + 16];         // the window's input bytes (expanded on the fly)
+    // CH = 256: u8, stored mod 256 -- offsets and word starts are < 256; the sentinels (wlen,
+    // n_atoms <= 256) are recovered with modular differences (atom_len, word_end)
+    using Idx = std::conditional_t<(CH <= 256), uint8_t, uint16_t>;
+    Idx aoff[NA];                   // atom -> byte offset in the window
+    Idx wsl[NA];                    // word -> first atom
+    __device__ __forceinline__ unsigned atom_len(unsigned j) const { return (Idx)(aoff[j + 1] - aoff[j]); }
+    __device__ __forceinline__ unsigned word_end(unsigned w) const {
+        return CH <= 256 ? (((unsigned)wsl[w + 1] + 255u) & 0xFFu) + 1u : (unsigned)wsl[w + 1];
+    }
+    alignas(16) uint8_t bytes[CH + 16];         // the window's input bytes (expanded on the fly)
 };
 
 struct SlotState {
@@ -373,9 +380,9 @@ __device__ bool prep_window(GroupLDS<CH, G> &L, const WinRegs<CH> &W, uint64_t p
         for (int u = 0; u < 4; u++) {
             const unsigned k = c0 + lane * 4 + u;
             if (ast[u]) {
-                L.aoff[ai] = (uint16_t)k;
+                L.aoff[ai] = (typename GroupLDS<CH, G>::Idx)k;
                 L.rec[ai].cpos = (uint16_t)(cp | (wst[u] ? CP_WS : 0));
-                if (wst[u]) { L.wsl[wi] = (uint16_t)ai; wi++; }
+                if (wst[u]) { L.wsl[wi] = (typename GroupLDS<CH, G>::Idx)ai; wi++; }
                 ai++;
             }
             cp += cpl[u];
@@ -385,9 +392,9 @@ __device__ bool prep_window(GroupLDS<CH, G> &L, const WinRegs<CH> &W, uint64_t p
         cp_tot += tot >> 18;
     }
     if (lane == 0) {
-        L.aoff[n_atoms] = (uint16_t)wlen;
+        L.aoff[n_atoms] = (typename GroupLDS<CH, G>::Idx)wlen;
         L.rec[n_atoms].cpos = (uint16_t)(cp_tot | CP_WS);
-        L.wsl[n_words] = (uint16_t)n_atoms;
+        L.wsl[n_words] = (typename GroupLDS<CH, G>::Idx)n_atoms;
     }
     n_atoms_o = n_atoms;
     n_words_o = n_words;
@@ -397,10 +404,10 @@ __device__ bool prep_window(GroupLDS<CH, G> &L, const WinRegs<CH> &W, uint64_t p
     const unsigned lim = raw ? 4u : MAX_ATOM_BYTES;   // raw: '▁' + one code point must fit 8 bytes
     bool bad = false;
     for (unsigned j = lane; j < n_atoms; j += 64) {
-        const unsigned p0 = L.aoff[j], la = (unsigned)L.aoff[j + 1] - p0;
+        const unsigned p0 = L.aoff[j], la = L.atom_len(j);
         const unsigned stop = L.rec[j + 1].cpos >> 15;
         const unsigned first = (raw && pos == 0 && j == 0) ? 1u : 0u;
-        bad |= la > lim;
+        bad |= la == 0 || la > lim;   // 0: a 256-byte atom, wrapped
         ainfo(L, j) = p0 | (la << 12) | (stop << 16) | (first << 17);
     }
     return ballot(bad) == 0;
@@ -730,7 +737,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
         STAMP(2);
 
         // ---------------------------------------------------------- C0: per-window token counts and validity
-        // (word w ends at atom wsl[w+1]; its final state is in fin[wsl[w+1]])
+        // (word w ends at atom word_end(w); its final state is in fin[word_end(w)])
         {
             unsigned pre[NG + 1];
             pre[0] = 0;
@@ -748,7 +755,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 unsigned cost = 0, inv = 0;
                 if (u < total) {
                     const GL &L = grp(g);
-                    const typename Wfin<G>::T F = GR::wfin(L.fin[L.wsl[u - wbase + 1]]);
+                    const typename Wfin<G>::T F = GR::wfin(L.fin[L.word_end(u - wbase)]);
                     cost = Wfin<G>::cost(F);
                     inv = Wfin<G>::invalid(F) ? 1u : 0u;
                 }
@@ -792,14 +799,14 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                     if (g == (unsigned)k) { wbase = pre[k]; tbase = tokpre[k]; ginv = inv_g[k]; }
                 GL &L = grp(g);
                 const unsigned w = u - wbase;
-                const typename Wfin<G>::T F = in ? GR::wfin(L.fin[L.wsl[w + 1]]) : (typename Wfin<G>::T)0;
+                const typename Wfin<G>::T F = in ? GR::wfin(L.fin[L.word_end(w)]) : (typename Wfin<G>::T)0;
                 const unsigned cost = in ? Wfin<G>::cost(F) : 0u;
                 const unsigned incl = wave_incl_scan_add(cost);
                 const unsigned tok_base = carry + incl - cost - tbase;
                 carry += __builtin_amdgcn_readlane(incl, 63);
                 if (in && !ginv && !len_only) {
                     const unsigned ws = L.wsl[w];
-                    unsigned i = L.wsl[w + 1];
+                    unsigned i = L.word_end(w);
                     const unsigned Ls = Wfin<G>::gmax(F);   // G of the word = the longest token to reach
                     unsigned c = cost, A = 0;
                     unsigned pend = L.rec[i].cpos & 0x7FFFu;
@@ -853,7 +860,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                     int32_t node = 0, nb = tv.root_base;
                     bool ok = true;
                     for (unsigned jj = j0; jj < j1; jj++) {
-                        const unsigned p0 = L.aoff[jj], la = (unsigned)L.aoff[jj + 1] - p0;
+                        const unsigned p0 = L.aoff[jj], la = L.atom_len(jj);
                         unsigned cnt;
                         uint64_t seq = atom_from_info(L.bytes, p0 | (la << 12) | ((first && jj == 0) ? (1u << 17) : 0u), raw, cnt);
                         for (; cnt; cnt--, seq >>= 8) {
