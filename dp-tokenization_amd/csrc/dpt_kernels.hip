@@ -115,26 +115,25 @@ __device__ __forceinline__ void wave_sync() {
 template <int G> struct Group;
 
 // G = 16: four strings per wave, one per DPP row.  Per atom: {cpos, ~span mask} in one
-// dword; per end position i, one dword `fin`: the back distances (minus one) of the largest
-// reachable j in E(i) attaining G[i] (dg) and of the largest reachable j in E(i) (de) --
-// G when there is none -- and the final state when i ends a word (Wfin<16>).
+// dword (after phase B the mask half of a word-end atom holds the word's final key, Wfin<16>,
+// and in C1 the mask halves take the selected tokens); per end position i, one u16 `fin`:
+// the back distances (minus one) of the largest reachable j in E(i) attaining G[i] (dg) and
+// of the largest reachable j in E(i) (de) -- 16 or more when there is none.
 template <> struct Group<16> {
     using M = uint16_t;  // span mask: bit L-1 = an L-atom token starts here
     struct Rec { uint16_t cpos; uint16_t smask; };
-    struct Fin { uint32_t v; };
-    static __device__ __forceinline__ unsigned dg(const Fin &x) { return (x.v >> 5) & 31u; }
-    static __device__ __forceinline__ unsigned de(const Fin &x) { return (x.v >> 10) & 31u; }
-    static __device__ __forceinline__ uint32_t wfin(const Fin &x) { return x.v; }
+    struct Fin { uint16_t v; };
+    static __device__ __forceinline__ unsigned dg(const Fin &x) { return x.v & 31u; }
+    static __device__ __forceinline__ unsigned de(const Fin &x) { return (x.v >> 5) & 31u; }
 };
 
 // G = 64: one string per wave (vocabularies with tokens of 17..64 code points).
 template <> struct Group<64> {
     using M = uint64_t;
     struct Rec { uint64_t smask; uint16_t cpos; uint16_t pad[3]; };
-    struct Fin { uint32_t d; uint32_t w; };
+    struct Fin { uint32_t d; uint32_t w; };   // w: the final key (Wfin<64>)
     static __device__ __forceinline__ unsigned dg(const Fin &x) { return x.d & 127u; }
     static __device__ __forceinline__ unsigned de(const Fin &x) { return (x.d >> 8) & 127u; }
-    static __device__ __forceinline__ uint32_t wfin(const Fin &x) { return x.w; }
 };
 
 // ------------------------------------------------------------------ LDS layout
@@ -142,13 +141,15 @@ template <> struct Group<64> {
 constexpr uint16_t CP_WS = 0x8000;        // cpos bit: atom starts a word
 constexpr unsigned MAX_ATOM_BYTES = 8;    // expanded atom = one u64 (raw: '▁'+4-byte code point = 7)
 
-// final state at a word end.  G = 16: fin[i] itself -- the group-min key with the back
-// distances in its constant bits 5..14: cost << 16 | invalid << 15 | de << 10 | dg << 5 | 31-G
+// final state at a word end.  G = 16: 16 bits in the word-end atom's mask half:
+// cost << 6 | invalid << 5 | 31-G, straight from the key (its bits 10..14 are constant 1s);
+// cost 1023 = the uncapped DP's "inf" (0xFFFF, inspect_tokenizer.py:80), capped costs <= CH
 template <int G> struct Wfin;
 template <> struct Wfin<16> {
-    using T = uint32_t;
-    static __device__ __forceinline__ unsigned cost(T x) { return x >> 16; }
-    static __device__ __forceinline__ bool invalid(T x) { return (x >> 15) & 1u; }
+    using T = uint16_t;
+    static __device__ __forceinline__ T pack(unsigned r) { return (T)(((r >> 10) & 0xFFE0u) | (r & 31u)); }
+    static __device__ __forceinline__ unsigned cost(T x) { return (x >> 6) == 1023u ? 0xFFFFu : (x >> 6); }
+    static __device__ __forceinline__ bool invalid(T x) { return (x >> 5) & 1u; }
     static __device__ __forceinline__ unsigned gmax(T x) { return 31u - (x & 31u); }
 };
 template <> struct Wfin<64> {
@@ -168,6 +169,11 @@ struct GroupLDS {
     //         the first atom of selected token j (tokens tile the window)
     typename Group<G>::Rec rec[NA];
     typename Group<G>::Fin fin[NA];   // per end position, see Group<G>
+    // the final key of the word ending at atom e
+    __device__ __forceinline__ typename Wfin<G>::T wkey(unsigned e) const {
+        if constexpr (G == 16) return rec[e].smask;
+        else return fin[e].w;
+    }
     // CH = 256: u8, stored mod 256 -- offsets and word starts are < 256; the sentinels (wlen,
     // n_atoms <= 256) are recovered with modular differences (atom_len, word_end)
     using Idx = std::conditional_t<(CH <= 256), uint8_t, uint16_t>;
@@ -235,10 +241,28 @@ __device__ unsigned long long g_stamps[8];
 #define STAMP_FLUSH
 #endif
 
-// phase A's per-atom descriptor lives in the (not yet written) fin[] entry of the atom
+// Phase A's per-atom descriptor: byte offset | byte length << PB | "a word or the window ends
+// after it" << PB+4 | "first atom of the string" << PB+5 (16 bits for 256-byte windows).  It is
+// parked in the (not yet written) fin[] entry of the atom.
+template <int CH> struct AInfo {
+    static constexpr unsigned PB = CH <= 256 ? 8u : 12u;
+    static constexpr unsigned STOP = 1u << (PB + 4), FIRST = 1u << (PB + 5);
+    static __device__ __forceinline__ unsigned pack(unsigned p0, unsigned la, unsigned stop, unsigned first) {
+        return p0 | (la << PB) | (stop ? STOP : 0u) | (first ? FIRST : 0u);
+    }
+    static __device__ __forceinline__ unsigned off(unsigned x) { return x & ((1u << PB) - 1u); }
+    static __device__ __forceinline__ unsigned len(unsigned x) { return (x >> PB) & 15u; }
+};
+
 template <int CH, int G>
-__device__ __forceinline__ uint32_t &ainfo(GroupLDS<CH, G> &L, unsigned j) {
-    return *reinterpret_cast<uint32_t *>(&L.fin[j]);
+__device__ __forceinline__ unsigned ainfo_get(const GroupLDS<CH, G> &L, unsigned j) {
+    if constexpr (G == 16) return L.fin[j].v;
+    else return L.fin[j].d;
+}
+template <int CH, int G>
+__device__ __forceinline__ void ainfo_set(GroupLDS<CH, G> &L, unsigned j, unsigned v) {
+    if constexpr (G == 16) L.fin[j].v = (uint16_t)v;
+    else L.fin[j].d = v;
 }
 
 // la (<= 8) window bytes from offset p: three aligned dword reads and a funnel shift
@@ -251,12 +275,13 @@ __device__ __forceinline__ uint64_t load_bytes(const uint8_t *bytes, unsigned p,
     return la >= 8 ? v : (v & ((1ull << (8u * la)) - 1ull));
 }
 
-// expanded bytes of the atom described by `info` (see prep_window)
+// expanded bytes of the atom described by `info` (AInfo)
+template <int CH>
 __device__ __forceinline__ uint64_t atom_from_info(const uint8_t *bytes, uint32_t info, bool raw, unsigned &cnt) {
-    const unsigned p = info & 0xFFFu, la = (info >> 12) & 0xFu;
-    const uint64_t v = load_bytes(bytes, p, la);
+    const unsigned la = AInfo<CH>::len(info);
+    const uint64_t v = load_bytes(bytes, AInfo<CH>::off(info), la);
     const unsigned b0 = (unsigned)(v & 0xFFu);
-    if (raw && (info & (1u << 17))) { cnt = 3 + la; return 0x8196E2ull | (v << 24); }
+    if (raw && (info & AInfo<CH>::FIRST)) { cnt = 3 + la; return 0x8196E2ull | (v << 24); }
     if (raw && b0 == ' ') { cnt = 3; return 0x8196E2ull; }
     if (raw && b0 == '\n') { cnt = 6; return 0x3E413078303Cull; }
     cnt = la;
@@ -408,7 +433,7 @@ __device__ bool prep_window(GroupLDS<CH, G> &L, const WinRegs<CH> &W, uint64_t p
         const unsigned stop = L.rec[j + 1].cpos >> 15;
         const unsigned first = (raw && pos == 0 && j == 0) ? 1u : 0u;
         bad |= la == 0 || la > lim;   // 0: a 256-byte atom, wrapped
-        ainfo(L, j) = p0 | (la << 12) | (stop << 16) | (first << 17);
+        ainfo_set(L, j, AInfo<CH>::pack(p0, la, stop, first));
     }
     return ballot(bad) == 0;
 }
@@ -554,9 +579,9 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 w.gsel = gs;
                 w.j = uu - base;
                 GL &L = grp(gs);
-                w.info = ainfo(L, w.j);
-                w.seq = atom_from_info(L.bytes, w.info, raw, w.cnt);
-                if (!(w.info & 0x10000u)) { w.ninfo = ainfo(L, w.j + 1); w.nseq = atom_from_info(L.bytes, w.ninfo, raw, w.ncnt); }
+                w.info = ainfo_get(L, w.j);
+                w.seq = atom_from_info<CH>(L.bytes, w.info, raw, w.cnt);
+                if (!(w.info & AInfo<CH>::STOP)) { w.ninfo = ainfo_get(L, w.j + 1); w.nseq = atom_from_info<CH>(L.bytes, w.ninfo, raw, w.ncnt); }
                 w.nb = tv.root_base; w.node = 0; w.len = 0; w.mask = 0;
             };
             Walk W[A_WALKS];
@@ -591,14 +616,14 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                             if (w.cnt == 0) {   // atom j+len-1 ends: the span j..j+len is a candidate token
                                 w.len++;
                                 if (ent[q].x & TERM_BIT) w.mask |= (M)1 << (w.len - 1);
-                                if ((w.info & 0x10000u) || w.len == (unsigned)G) {
+                                if ((w.info & AInfo<CH>::STOP) || w.len == (unsigned)G) {
                                     done = true;
                                 } else {
                                     w.info = w.ninfo; w.seq = w.nseq; w.cnt = w.ncnt;
-                                    if (!(w.info & 0x10000u) && w.len + 1 < (unsigned)G) {
+                                    if (!(w.info & AInfo<CH>::STOP) && w.len + 1 < (unsigned)G) {
                                         GL &L = grp(w.gsel);
-                                        w.ninfo = ainfo(L, w.j + w.len + 1);
-                                        w.nseq = atom_from_info(L.bytes, w.ninfo, raw, w.ncnt);
+                                        w.ninfo = ainfo_get(L, w.j + w.len + 1);
+                                        w.nseq = atom_from_info<CH>(L.bytes, w.ninfo, raw, w.ncnt);
                                     }
                                 }
                             }
@@ -668,7 +693,8 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                             const unsigned sh = 16u * mg;
                             const unsigned gs = (unsigned)(gmb >> sh), es = (unsigned)(emb >> sh);
                             const unsigned dg = (unsigned)__builtin_ctz(gs | 0x10000u), de = (unsigned)__builtin_ctz(es | 0x10000u);
-                            L.fin[i].v = (r & 0xFFFF801Fu) | (dg << 5) | (de << 10);
+                            L.fin[i].v = (uint16_t)(dg | (de << 5));
+                            L.rec[i].smask = Wfin<G>::pack(r);   // rec[i] was consumed at step i-1
                             if constexpr (edges)
                                 if (i <= na) a.edges[SS[mg].sb + SS[mg].abase + i - 1] = es & 0xFFFFu;
                         }
@@ -755,7 +781,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 unsigned cost = 0, inv = 0;
                 if (u < total) {
                     const GL &L = grp(g);
-                    const typename Wfin<G>::T F = GR::wfin(L.fin[L.word_end(u - wbase)]);
+                    const typename Wfin<G>::T F = L.wkey(L.word_end(u - wbase));
                     cost = Wfin<G>::cost(F);
                     inv = Wfin<G>::invalid(F) ? 1u : 0u;
                 }
@@ -799,7 +825,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                     if (g == (unsigned)k) { wbase = pre[k]; tbase = tokpre[k]; ginv = inv_g[k]; }
                 GL &L = grp(g);
                 const unsigned w = u - wbase;
-                const typename Wfin<G>::T F = in ? GR::wfin(L.fin[L.word_end(w)]) : (typename Wfin<G>::T)0;
+                const typename Wfin<G>::T F = in ? L.wkey(L.word_end(w)) : (typename Wfin<G>::T)0;
                 const unsigned cost = in ? Wfin<G>::cost(F) : 0u;
                 const unsigned incl = wave_incl_scan_add(cost);
                 const unsigned tok_base = carry + incl - cost - tbase;
@@ -862,7 +888,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                     for (unsigned jj = j0; jj < j1; jj++) {
                         const unsigned p0 = L.aoff[jj], la = L.atom_len(jj);
                         unsigned cnt;
-                        uint64_t seq = atom_from_info(L.bytes, p0 | (la << 12) | ((first && jj == 0) ? (1u << 17) : 0u), raw, cnt);
+                        uint64_t seq = atom_from_info<CH>(L.bytes, AInfo<CH>::pack(p0, la, 0, first && jj == 0), raw, cnt);
                         for (; cnt; cnt--, seq >>= 8) {
                             const int32_t sl = nb + (int32_t)(seq & 0xFFu);
                             const int2 ent = tv.slots[sl];
