@@ -33,6 +33,7 @@ struct dpt_ctx {
     uint32_t *retry_list = nullptr;
     uint64_t cap_str = 0;
     uint32_t *retry_count = nullptr;
+    uint8_t *wsl_scratch = nullptr;   // word lists of the 256-byte pass (dpt::wsl_scratch_bytes)
     void *scan_temp = nullptr;
     size_t scan_bytes = 0;
     unsigned max_blocks = 0;
@@ -114,6 +115,10 @@ int ensure_workspace(dpt_ctx *c, uint64_t n_bytes, uint64_t n_str) {
             if (e != hipSuccess) return hip_fail(e, "hipMalloc(scan)");
             c->scan_bytes = tb;
         }
+    }
+    if (!c->wsl_scratch) {
+        e = hipMalloc((void **)&c->wsl_scratch, dpt::wsl_scratch_bytes(c->max_blocks));
+        if (e != hipSuccess) return hip_fail(e, "hipMalloc(wsl_scratch)");
     }
     if (!c->retry_count) {
         e = hipMalloc((void **)&c->retry_count, 16);
@@ -240,7 +245,7 @@ int dpt_ctx_create(int device, dpt_ctx **out) {
 int dpt_ctx_destroy(dpt_ctx *c) {
     if (!c) return DPT_OK;
     DeviceGuard g(c->device);
-    void *ps[] = {c->staging, c->rec, c->counts, c->retry_list, c->retry_count, c->scan_temp, c->h_text, c->h_cut,
+    void *ps[] = {c->staging, c->rec, c->counts, c->retry_list, c->retry_count, c->wsl_scratch, c->scan_temp, c->h_text, c->h_cut,
                   c->h_ids, c->h_off, c->h_idoff, c->h_status, c->h_capped, c->h_edges};
     for (void *p : ps)
         if (p) hipFree(p);
@@ -287,6 +292,7 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
     p.counts = c->counts;
     p.retry_list = c->retry_list;
     p.retry_count = c->retry_count;
+    p.wsl_scratch = c->wsl_scratch;
     p.scan_temp = c->scan_temp;
     p.scan_temp_bytes = c->scan_bytes;
     p.max_blocks = c->max_blocks;

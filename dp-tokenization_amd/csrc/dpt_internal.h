@@ -24,6 +24,7 @@ struct EncodeLaunch {
     uint64_t *counts;
     uint32_t *retry_list;
     uint32_t *retry_count;
+    uint8_t *wsl_scratch;    // max_blocks x wsl_scratch_bytes(1) bytes
     void *scan_temp;
     size_t scan_temp_bytes;
     unsigned max_blocks;
@@ -45,6 +46,7 @@ constexpr int KERNEL_ROWS64 = 2;  // 1 string per wave, 64-lane DPP (max_cp <= 6
 hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t ev[6]);
 void launch_lane(const EncodeLaunch &p, unsigned blocks, hipStream_t stream);
 size_t scan_temp_bytes(uint64_t n_str);
+size_t wsl_scratch_bytes(unsigned max_blocks);
 hipError_t launch_histogram(const uint64_t *id_off, const int32_t *status, uint64_t n_str, int64_t *hist,
                             uint32_t n_bins, hipStream_t stream);
 hipError_t kernel_init();

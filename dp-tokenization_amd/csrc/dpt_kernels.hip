@@ -177,20 +177,36 @@ struct GroupLDS {
     // CH = 256: u8, stored mod 256 -- offsets and word starts are < 256; the sentinels (wlen,
     // n_atoms <= 256) are recovered with modular differences (atom_len, word_end)
     using Idx = std::conditional_t<(CH <= 256), uint8_t, uint16_t>;
+    // word -> first atom: in global scratch for 256-byte windows (WSLG; LDS is what limits the
+    // resident waves there), in LDS for the 2048-byte pass
+    static constexpr bool WSLG = CH <= 256;
+    static constexpr int WSL_STRIDE = (NA + 15) & ~15;
     Idx aoff[NA];                   // atom -> byte offset in the window
-    Idx wsl[NA];                    // word -> first atom
+    Idx wsl[WSLG ? 1 : NA];
     __device__ __forceinline__ unsigned atom_len(unsigned j) const { return (Idx)(aoff[j + 1] - aoff[j]); }
-    __device__ __forceinline__ unsigned word_end(unsigned w) const {
-        return CH <= 256 ? (((unsigned)wsl[w + 1] + 255u) & 0xFFu) + 1u : (unsigned)wsl[w + 1];
+    // word w's first atom / its end (= the next word's first atom, or n_atoms)
+    __device__ __forceinline__ unsigned word_start(const uint8_t *gw, unsigned w) const {
+        if constexpr (WSLG) return gw[w];
+        else return wsl[w];
+    }
+    __device__ __forceinline__ unsigned word_end(const uint8_t *gw, unsigned w) const {
+        if constexpr (WSLG) return (((unsigned)gw[w + 1] + 255u) & 0xFFu) + 1u;
+        else return wsl[w + 1];
+    }
+    __device__ __forceinline__ void set_word_start(uint8_t *gw, unsigned w, unsigned v) {
+        if constexpr (WSLG) gw[w] = (uint8_t)v;
+        else wsl[w] = (Idx)v;
     }
     alignas(16) uint8_t bytes[CH + 16];         // the window's input bytes (expanded on the fly)
 };
 
+// strings are < 4 GiB (dpt.h); abase: atoms of the string's earlier windows
 struct SlotState {
-    uint64_t s, sb, slen, pos;
-    uint32_t active, status, ntok, capsum;
-    uint32_t wlen, n_atoms, n_words, wtok;
-    uint32_t inval, abase, pad1, pad2;   // abase: atoms of the string's earlier windows
+    uint64_t sb;
+    uint32_t s, slen, pos, active;
+    uint32_t status, ntok, capsum, wlen;
+    uint32_t n_atoms, n_words, wtok, inval;
+    uint32_t abase, pad;
 };
 
 template <int CH, int G>
@@ -225,6 +241,7 @@ struct EncodeArgs {
     const uint32_t *work_list;  // 2048-byte pass: the retry list
     const uint32_t *work_count;
     uint32_t *work_next;        // dynamic work distribution counter (zeroed per launch)
+    uint8_t *wsl_scratch;       // word lists of the 256-byte pass: grid x NG x WSL_STRIDE bytes
     uint64_t *edges;            // nullable: per atom end, the E(i) & reachable back-distance mask
     int mode;                   // DPT_MODE_* | DPT_FLAG_*
 };
@@ -359,7 +376,7 @@ __device__ bool window_bounds(const WinRegs<CH> &W, uint64_t slen, uint64_t pos,
 // code-point prefixes (+ word-start bits) and the word list.  One packed DPP scan per 256
 // bytes.  Returns false if an atom is longer than MAX_ATOM_BYTES (4 bytes in RAW mode).
 template <int CH, int G>
-__device__ bool prep_window(GroupLDS<CH, G> &L, const WinRegs<CH> &W, uint64_t pos,
+__device__ bool prep_window(GroupLDS<CH, G> &L, uint8_t *gw, const WinRegs<CH> &W, uint64_t pos,
                             unsigned wlen, int mode, unsigned lane, unsigned &n_atoms_o, unsigned &n_words_o) {
     const bool raw = mode == 0;
     unsigned n_atoms = 0, cp_tot = 0, n_words = 0;
@@ -407,7 +424,7 @@ __device__ bool prep_window(GroupLDS<CH, G> &L, const WinRegs<CH> &W, uint64_t p
             if (ast[u]) {
                 L.aoff[ai] = (typename GroupLDS<CH, G>::Idx)k;
                 L.rec[ai].cpos = (uint16_t)(cp | (wst[u] ? CP_WS : 0));
-                if (wst[u]) { L.wsl[wi] = (typename GroupLDS<CH, G>::Idx)ai; wi++; }
+                if (wst[u]) { L.set_word_start(gw, wi, ai); wi++; }
                 ai++;
             }
             cp += cpl[u];
@@ -419,7 +436,7 @@ __device__ bool prep_window(GroupLDS<CH, G> &L, const WinRegs<CH> &W, uint64_t p
     if (lane == 0) {
         L.aoff[n_atoms] = (typename GroupLDS<CH, G>::Idx)wlen;
         L.rec[n_atoms].cpos = (uint16_t)(cp_tot | CP_WS);
-        L.wsl[n_words] = (typename GroupLDS<CH, G>::Idx)n_atoms;
+        L.set_word_start(gw, n_words, n_atoms);
     }
     n_atoms_o = n_atoms;
     n_words_o = n_words;
@@ -441,7 +458,7 @@ __device__ bool prep_window(GroupLDS<CH, G> &L, const WinRegs<CH> &W, uint64_t p
 // ------------------------------------------------------------------ the tokenize kernel
 
 #ifndef A_WALKS
-#define A_WALKS 2   // concurrent trie walks per lane in phase A
+#define A_WALKS 1   // concurrent trie walks per lane in phase A (2 measured slower once LDS allowed 19 waves/CU)
 #endif
 
 template <int CH, int G, bool BIG>
@@ -454,6 +471,9 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     SlotState *const SS = reinterpret_cast<SlotState *>(smem + NG * group_lds_bytes<CH, G>());
     auto grp = [&](unsigned g) -> GL & { return *reinterpret_cast<GL *>(smem + g * group_lds_bytes<CH, G>()); };
+    auto wsl_of = [&](unsigned g) -> uint8_t * {
+        return GL::WSLG ? a.wsl_scratch + ((size_t)blockIdx.x * NG + g) * GL::WSL_STRIDE : nullptr;
+    };
 
     const unsigned lane = lane_id();
     const unsigned mg = lane / G;        // my group
@@ -492,7 +512,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                         const uint64_t s = BIG ? (uint64_t)a.work_list[idx] : idx;
                         const uint64_t o0 = a.str_off[s], o1 = a.str_off[s + 1];
                         SlotState &S = SS[lane];
-                        S.s = s; S.sb = o0 - base_off; S.slen = o1 - o0; S.pos = 0; S.active = 1;
+                        S.s = (uint32_t)s; S.sb = o0 - base_off; S.slen = (uint32_t)(o1 - o0); S.pos = 0; S.active = 1;
                         S.status = o1 == o0 ? 2u : 0u;  // pretokenize_raw('') == [[]] -> IndexError
                         S.ntok = 0; S.capsum = 0; S.abase = 0;
                     }
@@ -521,7 +541,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 unsigned wlen = 0, na = 0, nw = 0;
                 bool ok = status != 2;
                 if (ok) ok = window_bounds<CH>(W[g], slen, pos, mode, lane, wlen);
-                if (ok) ok = prep_window<CH, G>(L, W[g], pos, wlen, mode, lane, na, nw);
+                if (ok) ok = prep_window<CH, G>(L, wsl_of(g), W[g], pos, wlen, mode, lane, na, nw);
                 if (ok) {
                     if (lane == 0) { S.wlen = wlen; S.n_atoms = na; S.n_words = nw; S.wtok = 0; S.inval = 0; }
                     prepared |= 1u << g;
@@ -781,7 +801,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 unsigned cost = 0, inv = 0;
                 if (u < total) {
                     const GL &L = grp(g);
-                    const typename Wfin<G>::T F = L.wkey(L.word_end(u - wbase));
+                    const typename Wfin<G>::T F = L.wkey(L.word_end(wsl_of(g), u - wbase));
                     cost = Wfin<G>::cost(F);
                     inv = Wfin<G>::invalid(F) ? 1u : 0u;
                 }
@@ -825,14 +845,14 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                     if (g == (unsigned)k) { wbase = pre[k]; tbase = tokpre[k]; ginv = inv_g[k]; }
                 GL &L = grp(g);
                 const unsigned w = u - wbase;
-                const typename Wfin<G>::T F = in ? L.wkey(L.word_end(w)) : (typename Wfin<G>::T)0;
+                const typename Wfin<G>::T F = in ? L.wkey(L.word_end(wsl_of(g), w)) : (typename Wfin<G>::T)0;
                 const unsigned cost = in ? Wfin<G>::cost(F) : 0u;
                 const unsigned incl = wave_incl_scan_add(cost);
                 const unsigned tok_base = carry + incl - cost - tbase;
                 carry += __builtin_amdgcn_readlane(incl, 63);
                 if (in && !ginv && !len_only) {
-                    const unsigned ws = L.wsl[w];
-                    unsigned i = L.word_end(w);
+                    const unsigned ws = L.word_start(wsl_of(g), w);
+                    unsigned i = L.word_end(wsl_of(g), w);
                     const unsigned Ls = Wfin<G>::gmax(F);   // G of the word = the longest token to reach
                     unsigned c = cost, A = 0;
                     unsigned pend = L.rec[i].cpos & 0x7FFFu;
@@ -1002,6 +1022,7 @@ template <int CH, int G, bool BIG>
 static void launch_tok(const EncodeArgs &a, const TrieView &tv, uint64_t n_units, unsigned n_cu, hipStream_t stream) {
     constexpr int lds = block_lds_bytes<CH, G>();
     uint64_t blocks = (uint64_t)n_cu * resident_per_cu<CH, G, BIG>();
+    if (blocks > (uint64_t)n_cu * 64u) blocks = (uint64_t)n_cu * 64u;   // the scratch is sized for 64 per CU
     if (blocks > n_units) blocks = n_units ? n_units : 1;
     hipLaunchKernelGGL((tokenize_kernel<CH, G, BIG>), dim3((unsigned)blocks), dim3(64), lds, stream, a, tv);
 }
@@ -1014,6 +1035,7 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     a.mode = p.mode;
     a.edges = p.edges;
     a.work_next = p.retry_count + 1;
+    a.wsl_scratch = p.wsl_scratch;
     TrieView tv{p.slots, p.slot_ids, p.root_base};
 
     hipLaunchKernelGGL(zero_first, dim3(1), dim3(64), 0, stream, p.id_off, p.retry_count);
@@ -1048,6 +1070,10 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     }
     if (ev) hipEventRecord(ev[3], stream);
     return hipGetLastError();
+}
+
+size_t wsl_scratch_bytes(unsigned max_blocks) {
+    return (size_t)max_blocks * 4 * GroupLDS<SMALL_CH, 16>::WSL_STRIDE;   // NG x stride covers both G at CH = 256
 }
 
 size_t scan_temp_bytes(uint64_t n_str) {
