@@ -104,6 +104,13 @@ __device__ __forceinline__ uint64_t uni64(uint64_t x) {
 
 __device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 
+// lowest set bit (v_ffbl_b32: 0xFFFFFFFF for 0, no select needed where 0 cannot matter)
+__device__ __forceinline__ unsigned ffbl(unsigned x) {
+    unsigned r;
+    asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_s_barrier();
@@ -118,13 +125,15 @@ template <int G> struct Group;
 // dword (after phase B the mask half of a word-end atom holds the word's final key, Wfin<16>,
 // and in C1 the mask halves take the selected tokens); per end position i, one u16 `fin`:
 // the back distances (minus one) of the largest reachable j in E(i) attaining G[i] (dg) and
-// of the largest reachable j in E(i) (de) -- 16 or more when there is none.
+// of the largest reachable j in E(i) (de), 4 bits each.  Both exist at every position of a
+// valid word's selected path (Appendix A: a reachable i has a reachable j attaining its key),
+// and C1 walks valid words only, so no "none" code is stored.
 template <> struct Group<16> {
     using M = uint16_t;  // span mask: bit L-1 = an L-atom token starts here
     struct Rec { uint16_t cpos; uint16_t smask; };
     struct Fin { uint16_t v; };
-    static __device__ __forceinline__ unsigned dg(const Fin &x) { return x.v & 31u; }
-    static __device__ __forceinline__ unsigned de(const Fin &x) { return (x.v >> 5) & 31u; }
+    static __device__ __forceinline__ unsigned dg(const Fin &x) { return x.v & 15u; }
+    static __device__ __forceinline__ unsigned de(const Fin &x) { return (x.v >> 4) & 15u; }
 };
 
 // G = 64: one string per wave (vocabularies with tokens of 17..64 code points).
@@ -285,11 +294,10 @@ __device__ __forceinline__ void ainfo_set(GroupLDS<CH, G> &L, unsigned j, unsign
 // la (<= 8) window bytes from offset p: three aligned dword reads and a funnel shift
 __device__ __forceinline__ uint64_t load_bytes(const uint8_t *bytes, unsigned p, unsigned la) {
     const uint32_t *w = reinterpret_cast<const uint32_t *>(bytes) + (p >> 2);
-    const unsigned sh = (p & 3u) * 8u;
-    const uint64_t lo = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
-    const uint64_t hi = w[2];
-    uint64_t v = sh ? ((lo >> sh) | (hi << (64u - sh))) : lo;
-    return la >= 8 ? v : (v & ((1ull << (8u * la)) - 1ull));
+    const unsigned sh = p & 3u;
+    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+    const uint64_t v = (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32);
+    return v & (~0ull >> (64u - 8u * la));   // 1 <= la <= 8
 }
 
 // expanded bytes of the atom described by `info` (AInfo)
@@ -298,11 +306,15 @@ __device__ __forceinline__ uint64_t atom_from_info(const uint8_t *bytes, uint32_
     const unsigned la = AInfo<CH>::len(info);
     const uint64_t v = load_bytes(bytes, AInfo<CH>::off(info), la);
     const unsigned b0 = (unsigned)(v & 0xFFu);
-    if (raw && (info & AInfo<CH>::FIRST)) { cnt = 3 + la; return 0x8196E2ull | (v << 24); }
-    if (raw && b0 == ' ') { cnt = 3; return 0x8196E2ull; }
-    if (raw && b0 == '\n') { cnt = 6; return 0x3E413078303Cull; }
-    cnt = la;
-    return v;
+    // branch-free selects (lanes of one wave take different cases)
+    const bool fi = raw && (info & AInfo<CH>::FIRST) != 0;
+    const bool sp = raw && !fi && b0 == ' ';
+    const bool nl = raw && !fi && b0 == '\n';
+    uint64_t seq = fi ? (0x8196E2ull | (v << 24)) : v;
+    seq = sp ? 0x8196E2ull : seq;
+    seq = nl ? 0x3E413078303Cull : seq;
+    cnt = fi ? 3 + la : (sp ? 3u : (nl ? 6u : la));
+    return seq;
 }
 
 // ------------------------------------------------------------------ prep: one slot's window
@@ -712,13 +724,15 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                         if (d == 0) {
                             const unsigned sh = 16u * mg;
                             const unsigned gs = (unsigned)(gmb >> sh), es = (unsigned)(emb >> sh);
-                            const unsigned dg = (unsigned)__builtin_ctz(gs | 0x10000u), de = (unsigned)__builtin_ctz(es | 0x10000u);
-                            L.fin[i].v = (uint16_t)(dg | (de << 5));
+                            // lowest set bit of the row; bits of other rows only land in fields
+                            // of positions C1 never reads (see Group<16>)
+                            const unsigned dg = ffbl(gs), de = ffbl(es);
+                            L.fin[i].v = (uint16_t)(dg | (de << 4));
                             L.rec[i].smask = Wfin<G>::pack(r);   // rec[i] was consumed at step i-1
                             if constexpr (edges)
                                 if (i <= na) a.edges[SS[mg].sb + SS[mg].abase + i - 1] = es & 0xFFFFu;
                         }
-                        const bool wend = (cur & CP_WS) != 0;   // word starts and the window end
+                        const bool wend = (int16_t)cur < 0;     // CP_WS: word starts and the window end
                         wsh = wend ? (i << 16) : wsh;
                         unsigned nxt = r + 0x10000u;
                         if constexpr (unc) nxt = r >= 0xFFFE0000u ? 0xFFFF8000u : nxt;   // unreachable: cost stays inf
