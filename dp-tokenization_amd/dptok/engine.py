@@ -163,6 +163,38 @@ class Encoder:
         ids, id_off, st, _ = self.encode_csr(text, offs, mode="presplit", cut_mask=cut)
         return ids.tolist(), int(st[0])
 
+    def encode_word_atoms(self, strings: Sequence[Sequence[Sequence[str]]]) -> List[Tuple[List[int], int]]:
+        """Strings given as words of atoms (DPT_MODE_ATOMS), one launch for the batch: per string
+        (ids, status).  A string with no words gives ([], ok) -- the BLOOM adapter's empty input
+        (reference tokenizer_utils.py:166-178 loops over zero words)."""
+        parts, cuts, offs = [], [], [0]
+        for words in strings:
+            n = 0
+            for atoms in words:
+                for k, a in enumerate(atoms):
+                    e = encode_utf8(a)
+                    if not e:
+                        raise ValueError("empty atom")
+                    c = bytearray(len(e))
+                    c[0] = 3 if k == 0 else 2          # bit 1: atom start, bit 0: word start
+                    parts.append(e)
+                    cuts.append(bytes(c))
+                    n += len(e)
+                if not atoms:
+                    raise ValueError("empty word")
+            offs.append(offs[-1] + n)
+        text = np.frombuffer(b"".join(parts) + b"\0", dtype=np.uint8)
+        cut = np.frombuffer(b"".join(cuts) + b"\0", dtype=np.uint8)
+        o = np.array(offs, dtype=np.uint64)
+        ids, id_off, st, _ = self.encode_csr(text, o, mode="atoms", cut_mask=cut)
+        out = []
+        for i, words in enumerate(strings):
+            if not words:
+                out.append(([], _lib.STATUS_OK))
+            else:
+                out.append((ids[int(id_off[i]):int(id_off[i + 1])].tolist(), int(st[i])))
+        return out
+
     def dp(self, text: np.ndarray, offs: np.ndarray, mode="atoms", cut_mask: Optional[np.ndarray] = None,
            uncapped: bool = False, edges: bool = False):
         """DP by-products without ids (dpt_dp_host): (status, lengths, edges or None).  lengths are

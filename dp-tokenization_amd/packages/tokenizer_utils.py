@@ -136,8 +136,59 @@ def dp_tokenize_llama(llama_tokenizer, pretokenize_option="llama"):
     return dp_tokenize, decode_dp_tokenization
 
 
+BLOOM_TOKENIZER_JSON = ("{}/models--bigscience--bloom-3b/snapshots/"
+                        "52bc5b43010b4844513826b8be3f78c7344c37d7/tokenizer.json")
+
+
 def dp_tokenize_bloom(bloom_tokenizer, HF_CACHE_DIR):
-    """BLOOM byte-level adapter (reference tokenizer_utils.py:98-181): SURVEY.md §8f row f3,
-    not part of this round's hot path."""
-    raise NotImplementedError("dp_tokenize_bloom: BLOOM byte-level path is row f3 (next); "
-                              "use dp_tokenize_llama or dptok.Encoder with a t2i vocabulary")
+    """BLOOM byte-level adapter (reference tokenizer_utils.py:98-181).
+
+    * the vocabulary is ``tokenizer.json``'s ``model.vocab`` with ids = its **enumeration
+      order** (reference :104-108, ``{token: index for index, token in enumerate(vocab)}``);
+    * words come from the tokenizer's own pre-tokenizer (``pre_tokenize_str``, :160-162);
+    * a word's atoms are ``convert_ids_to_tokens([vocab_to_index[c] for c in word])`` (:155-157;
+      a character outside the vocabulary raises KeyError there, as in the reference);
+    * the DP + longest-token selection + ids run on the GPU in atoms mode (one launch per
+      call; ``dp_tokenize.batch`` for many strings), ids = enumeration-order indices (:174-177).
+    The reference's ``merges`` -> ``token_to_source_merge`` map (:113-116) feeds only the unused
+    ``unwind_to_base_tokenization``; merges are parsed here in either tokenizer.json form
+    ("a b" strings or [a, b] pairs) and otherwise unused.
+    """
+    import json
+
+    with open(BLOOM_TOKENIZER_JSON.format(HF_CACHE_DIR), "r") as f:
+        tokenizer_json = json.load(f)
+    merges = tokenizer_json["model"]["merges"]
+    vocab_to_index = _InverseDict({token: index for index, token in enumerate(tokenizer_json["model"]["vocab"])})
+    token_to_source_merge = {}
+    for merge in merges:
+        a, b = merge.split() if isinstance(merge, str) else merge
+        token_to_source_merge[a + b] = (a, b)
+    engine = Encoder(Vocab(dict(vocab_to_index), _device()))
+
+    def pretokenize(input_str):
+        pretokenized = bloom_tokenizer._tokenizer.pre_tokenizer.pre_tokenize_str(input_str)
+        return [block[0] for block in pretokenized]
+
+    def atoms_of(word):
+        token_inds = [vocab_to_index[c] for c in word]   # KeyError for characters outside the vocab
+        return bloom_tokenizer.convert_ids_to_tokens(token_inds)
+
+    def encode_many(texts: Sequence[str]) -> List[List[int]]:
+        batch = [[atoms_of(w) for w in pretokenize(t)] for t in texts]
+        out = []
+        for t, (ids, st) in zip(texts, engine.encode_word_atoms(batch)):
+            raise_for_status(st, t)
+            out.append(ids)
+        return out
+
+    def dp_tokenize(input_str) -> List[int]:
+        return encode_many([input_str])[0]
+
+    def decode_dp_tokenization(encoding: List[int]):
+        return bloom_tokenizer.decode(encoding)   # reference :179-181
+
+    dp_tokenize.batch = encode_many
+    dp_tokenize.engine = engine
+    dp_tokenize.vocab_to_index = vocab_to_index
+    return dp_tokenize, decode_dp_tokenization

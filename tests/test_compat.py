@@ -152,3 +152,58 @@ def test_disregard_word_initial_marker():
     V = {"##ab", "##c", "a", "b"}
     toks, n = compute_shortest_tokenizations(list("abc"), V, True, "##")
     assert n == 2 and toks == [["ab", "c"]]
+
+
+# ------------------------------------------------------------------ BLOOM adapter (row f3)
+
+def test_bloom_fixture_shape():
+    """The synthetic BLOOM-shaped tokenizer loads where the reference reads it and pre-tokenizes
+    into byte-level words; the reference-generated fixture covers the texts."""
+    import tempfile
+    from bloom_fixture import bloom_texts, bloom_tokenizer, make_hf_cache
+    g = load_golden("bloom_cases.json.gz")
+    assert [c["text"] for c in g["cases"]] == bloom_texts()
+    with tempfile.TemporaryDirectory() as d:
+        tokz = bloom_tokenizer(make_hf_cache(d))
+        words = [w for w, _ in tokz._tokenizer.pre_tokenizer.pre_tokenize_str("hello  world, café 😀")]
+        assert words[0] == "hello" and "Ġworld" in words and all(w for w in words)
+
+
+@pytest.mark.gpu
+def test_dp_tokenize_bloom_matches_reference():
+    import tempfile
+    from bloom_fixture import bloom_tokenizer, make_hf_cache
+    from packages.tokenizer_utils import dp_tokenize_bloom
+    g = load_golden("bloom_cases.json.gz")
+    with tempfile.TemporaryDirectory() as d:
+        hf = make_hf_cache(d)
+        tokz = bloom_tokenizer(hf)
+        dp_tokenize, decode = dp_tokenize_bloom(tokz, hf)
+        for c in g["cases"][:60]:
+            assert dp_tokenize(c["text"]) == c["ids"], c["text"]
+        assert dp_tokenize.batch([c["text"] for c in g["cases"]]) == [c["ids"] for c in g["cases"]]
+        assert isinstance(decode(g["cases"][3]["ids"]), str)
+
+
+@pytest.mark.gpu
+def test_dp_tokenize_bloom_key_error_outside_vocab():
+    """A character outside tokenizer.json's vocab raises KeyError (reference :155)."""
+    import json
+    import os
+    import tempfile
+    from bloom_fixture import SNAPSHOT, bloom_tokenizer, make_hf_cache
+    from packages.tokenizer_utils import dp_tokenize_bloom
+    with tempfile.TemporaryDirectory() as d:
+        hf = make_hf_cache(d)
+        tokz = bloom_tokenizer(hf)
+        p = os.path.join(hf, SNAPSHOT, "tokenizer.json")
+        with open(p) as fh:
+            tj = json.load(fh)
+        tj["model"]["vocab"] = {t: i for t, i in tj["model"]["vocab"].items() if "z" not in t}
+        with open(p, "w") as fh:
+            json.dump(tj, fh)
+        dp_tokenize, _ = dp_tokenize_bloom(tokz, hf)
+        assert dp_tokenize("abc def") == dp_tokenize.batch(["abc def"])[0]
+        with pytest.raises(KeyError):
+            dp_tokenize("lazy")
+        assert dp_tokenize("") == []
