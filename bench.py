@@ -39,7 +39,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--strings", type=int, default=1_000_000, help="strings per GPU")
+    ap.add_argument("--workload", choices=["cfg2", "cfg4", "cfg5"], default="cfg2",
+                    help="cfg2 (the metric's config): 256-byte random ASCII; cfg4: S2ORC-shaped; cfg5: Arabic-shaped")
+    ap.add_argument("--strings", type=int, default=None, help="strings per GPU (default: 1M; cfg4: 200k)")
     ap.add_argument("--length", type=int, default=256)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--exact-sample", type=int, default=65536, help="strings checked against the C oracle (rank 0)")
@@ -122,16 +124,32 @@ def main():
     from dptok import Encoder, Vocab, synth
     from dptok import dist as ddist
     t2i = synth.llama_shaped_vocab()
-    M, Lb = args.strings, args.length
-    text, offs = synth.random_ascii_corpus(M, Lb, seed=args.seed, start=rank * M)
+    Lb = args.length
+    if args.workload == "cfg2":
+        M = args.strings or 1_000_000
+        text, offs = synth.random_ascii_corpus(M, Lb, seed=args.seed, start=rank * M)
+        wl = f"cfg2: {M // 1000}k x {Lb}-byte random ASCII strings per GPU, raw pre-tokenization"
+        data = "synthetic random printable ASCII (Philox keyed by seed+global index); synthetic Llama-shaped 32k vocab"
+    elif args.workload == "cfg4":
+        M = args.strings or 200_000
+        text, offs = synth.generate_parallel("s2orc", M, start=rank * M, procs=min(16, os.cpu_count() or 1), seed=4)
+        wl = f"cfg4: {M // 1000}k S2ORC-shaped abstracts per GPU (~1200 B, N(1200,400) clipped to [64,4096]), raw"
+        data = "synthetic S2ORC-shaped pseudo-English (dptok.synth.s2orc_like_corpus); synthetic Llama-shaped 32k vocab"
+    else:
+        M = args.strings or 1_000_000
+        text, offs = synth.generate_parallel("arabic", M, start=rank * M, procs=min(16, os.cpu_count() or 1),
+                                             length=Lb, seed=5)
+        wl = f"cfg5: {M // 1000}k x ~{Lb}-byte Arabic-shaped strings per GPU (2-byte code points), raw"
+        data = "synthetic Arabic-shaped UTF-8 (dptok.synth.arabic_corpus); synthetic Llama-shaped 32k vocab + Arabic letters"
+    Lb = int(offs[-1]) // M
     cores = max(1, min(16, os.cpu_count() or 1))
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # before any GPU call: the pool forks plain CPU workers
-        texts = synth.unpack(text[: args.cpu_sample * Lb], offs[: args.cpu_sample + 1])
+        texts = synth.unpack(text[: int(offs[args.cpu_sample])], offs[: args.cpu_sample + 1])
         v, nd, nto, cdt = cpu_baseline(texts, args.cpu_budget, cores)
         cpu = {"value": v, "unit": "bytes/s", "cores": cores, "kind": "port",
-               "sample": f"{nd} of the first {args.cpu_sample} cfg2 strings in {cdt:.1f}s "
+               "sample": f"{nd} of the first {args.cpu_sample} {args.workload} strings in {cdt:.1f}s "
                          f"(enumerate-then-select, oracle/ref_port.py; {nto} hit the 10s per-string limit)"}
 
     ddist.init_from_env("nccl")
@@ -208,13 +226,15 @@ def main():
         exact = {"rate": same / S, "sample": S, "checker": "oracle/dp_oracle.c"}
         if cpu is not None:
             t0c = time.perf_counter()
-            ov.encode_csr(text, offs[: 65537], nthreads=cores)
-            cpu["c_restatement_bytes_per_s"] = 65536 * Lb / (time.perf_counter() - t0c)
+            S2 = min(65536, M)
+            ov.encode_csr(text, offs[: S2 + 1], nthreads=cores)
+            cpu["c_restatement_bytes_per_s"] = int(offs[S2]) / (time.perf_counter() - t0c)
 
     if rank == 0:
         value = world * n_bytes * args.steps / dt
         line = {
-            "metric": "input bytes/sec/GPU + exact-match rate vs CPU DP, 256-byte strings",
+            "metric": "input bytes/sec/GPU + exact-match rate vs CPU DP, 256-byte strings"
+                      if args.workload == "cfg2" else "input bytes/sec/GPU + exact-match rate vs CPU DP (%s)" % args.workload,
             "value": value,
             "unit": "bytes/s",
             "n_gpus": world,
@@ -225,8 +245,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic random printable ASCII (Philox keyed by seed+global index); synthetic Llama-shaped 32k vocab",
-            "config": {"workload": "cfg2: 1M x 256-byte random ASCII strings per GPU, raw pre-tokenization",
+            "data": data,
+            "config": {"workload": wl,
                        "strings_per_gpu": M, "bytes_per_string": Lb, "vocab": "synthetic llama-shaped 32000",
                        "parallelism": f"dp{world} (corpus shards, 1 RCCL all-reduce of the histogram per step)"},
             "per_gpu_bytes_per_s": value / world,
@@ -236,7 +256,7 @@ def main():
             "stage_ms_per_step": {"tokenize": ms_stage[0] / max(launches, 1), "scan": ms_stage[1] / max(launches, 1),
                                   "compact": ms_stage[2] / max(launches, 1)},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic_for(M, Lb),
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic_for(M, Lb) if args.workload == "cfg2" else None,
                          "kernel": "tokenize_kernel<256,16,false>", "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
         }

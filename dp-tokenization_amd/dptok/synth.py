@@ -193,3 +193,26 @@ def unpack(text: np.ndarray, offs: np.ndarray) -> List[str]:
     raw = text.tobytes()
     o = [int(x) for x in offs]
     return [raw[o[i]:o[i + 1]].decode("utf-8", "surrogatepass") for i in range(len(o) - 1)]
+
+
+def _gen_chunk(args):
+    kind, n, start, kw = args
+    return {"s2orc": s2orc_like_corpus, "arabic": arabic_corpus}[kind](n, start=start, **kw)
+
+
+def generate_parallel(kind: str, n: int, start: int = 0, procs: int = 8, **kw) -> Tuple[np.ndarray, np.ndarray]:
+    """``s2orc_like_corpus`` / ``arabic_corpus`` over [start, start+n) split across ``procs``
+    forked processes (identical output: every string is keyed by its global index).  Call
+    before any GPU work (fork)."""
+    import multiprocessing as mp
+    if procs <= 1 or n < 4096:
+        return _gen_chunk((kind, n, start, kw))
+    step = (n + procs - 1) // procs
+    jobs = [(kind, min(step, n - s), start + s, kw) for s in range(0, n, step)]
+    with mp.get_context("fork").Pool(len(jobs)) as pool:
+        res = pool.map(_gen_chunk, jobs)
+    texts = [t for t, _ in res]
+    lens = np.concatenate([np.diff(o) for _, o in res])
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens, dtype=np.uint64)
+    return np.concatenate(texts), offs
