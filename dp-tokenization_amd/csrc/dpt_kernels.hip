@@ -876,18 +876,18 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 const unsigned tok_base = carry + incl - cost - tbase;
                 carry += __builtin_amdgcn_readlane(incl, 63);
                 if (in && !ginv && !len_only) {
-                    const unsigned ws = L.word_start(wsl_of(g), w);
+                    // a valid word's walk emits exactly `cost` tokens and ends at its first atom
+                    // (Appendix A), so the token count bounds the loop
                     unsigned i = L.word_end(wsl_of(g), w);
                     const unsigned Ls = Wfin<G>::gmax(F);   // G of the word = the longest token to reach
                     unsigned c = cost, A = 0;
                     unsigned pend = L.rec[i].cpos & 0x7FFFu;
-                    while (i > ws) {
+                    while (c > 0) {
                         const typename GR::Fin f = L.fin[i];
                         const unsigned cpi = L.rec[i].cpos & 0x7FFFu;
                         const unsigned sp = pend - cpi;
                         A = A > sp ? A : sp;                 // the token emitted last step ended at pend
                         const unsigned dd = A < Ls ? GR::dg(f) : GR::de(f);
-                        if (dd >= (unsigned)G || dd + 1 > i - ws || c == 0) break;   // unreachable by Appendix A
                         const unsigned j = i - 1 - dd;
                         c--;
                         L.rec[tok_base + c].smask = (M)j;   // span masks are dead after B
