@@ -215,7 +215,7 @@ struct SlotState {
     uint32_t s, slen, pos, active;
     uint32_t status, ntok, capsum, wlen;
     uint32_t n_atoms, n_words, wtok, inval;
-    uint32_t abase, pad;
+    uint32_t abase, capb;   // capb: some atom of the window is not a token by itself (the cap can bind)
 };
 
 template <int CH, int G>
@@ -558,7 +558,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 if (ok) ok = window_bounds<CH>(W[g], slen, pos, mode, lane, wlen);
                 if (ok) ok = prep_window<CH, G>(L, wsl_of(g), W[g], pos, wlen, mode, lane, na, nw);
                 if (ok) {
-                    if (lane == 0) { S.wlen = wlen; S.n_atoms = na; S.n_words = nw; S.wtok = 0; S.inval = 0; }
+                    if (lane == 0) { S.wlen = wlen; S.n_atoms = na; S.n_words = nw; S.wtok = 0; S.inval = 0; S.capb = 0; }
                     prepared |= 1u << g;
                     busy++;
                     continue;
@@ -675,6 +675,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                     const uint64_t dm = ballot(done);
                     if (done) {
                         grp(w.gsel).rec[w.j].smask = G == 16 ? (M)~w.mask : w.mask;   // B (G = 16) reads it inverted
+                        if (!(w.mask & 1u)) SS[w.gsel].capb = 1;
                         const unsigned rank = __builtin_amdgcn_mbcnt_hi((unsigned)(dm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)dm, 0u));
                         const unsigned uu = nxt + rank;
                         w.active = uu < total;
@@ -697,8 +698,13 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
             // Steps past a slot's own n_atoms (up to the wave's imax <= CH) compute garbage that
             // lands in fin[] entries nobody reads, so the loop body has no per-slot guard.
             // Recording the edges (f1) and the uncapped DP (f2) are hoisted out as loop versions.
-            auto forward = [&](auto EDGES, auto UNCAPPED) {
-                constexpr bool edges = decltype(EDGES)::value, unc = decltype(UNCAPPED)::value;
+            // CAPM 0: the reference's capped DP (cost[i] <= i, dp_tokenize.py:28); 1: uncapped with
+            // "inf" (inspect_tokenizer.py:77-86); 2: neither -- exact for both when every atom of
+            // the wave's windows is a token by itself (then cost[i] <= i - ws on a valid path, so
+            // the cap never wins and nothing is unreachable)
+            auto forward = [&](auto EDGES, auto CAPM) {
+                constexpr bool edges = decltype(EDGES)::value;
+                constexpr int capm = decltype(CAPM)::value;
                 // st (lane d, candidate j = i-1-d) = (cost[j]+1) << 16 | invalid[j] << 15 | G[j]
                 constexpr unsigned ST0 = 0x10000u;   // word start: cost 0, reachable, G 0
                 unsigned ws = 0;
@@ -726,7 +732,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                         kv = skI < kv ? skI : kv;
                         const unsigned key = kv | (unsigned)__builtin_amdgcn_sbfe((int)xI, sbit, 1);
                         unsigned r = row_min_u32(key);
-                        if constexpr (!unc) {
+                        if constexpr (capm == 0) {
                             const unsigned capkey = ((i << 16) | 0xFFFFu) - wsh;
                             r = r < capkey ? r : capkey;
                         }
@@ -746,7 +752,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                         const bool wend = (int16_t)cur < 0;     // CP_WS: word starts and the window end
                         wsh = wend ? (i << 16) : wsh;
                         unsigned nxt = r + 0x10000u;
-                        if constexpr (unc) nxt = r >= 0xFFFE0000u ? 0xFFFF8000u : nxt;   // unreachable: cost stays inf
+                        if constexpr (capm == 1) nxt = r >= 0xFFFE0000u ? 0xFFFF8000u : nxt;   // unreachable: cost stays inf
                         skO = row_shift_in(skI, wend ? SK0 : nxt);
                         xO = row_shift_in(xI, cur);
                     };
@@ -770,7 +776,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                         const unsigned bit = (d < 32 ? (mlo >> d) : (mhi >> (d - 32))) & 1u;
                         const unsigned key = bit ? kv : 0xFFFFFFFFu;
                         unsigned r = wave_min_u32(key);
-                        if constexpr (!unc) {
+                        if constexpr (capm == 0) {
                             const unsigned capkey = ((i - ws) << 16) | 0xFFFFu;
                             r = r < capkey ? r : capkey;
                         }
@@ -787,7 +793,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                         const bool wend = (cur & CP_WS) != 0;
                         ws = wend ? i : ws;
                         unsigned nxt = (r ^ 0x7FFFu) + 0x10000u;
-                        if constexpr (unc) nxt = r >= 0xFFFE0000u ? 0xFFFF8000u : nxt;
+                        if constexpr (capm == 1) nxt = r >= 0xFFFE0000u ? 0xFFFF8000u : nxt;
                         const unsigned sin = wend ? ST0 : nxt;
                         st = wave_shift_in(st, sin);
                         cpj = wave_shift_in(cpj, cpi);
@@ -798,10 +804,16 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
             };
             using T_ = std::true_type;
             using F_ = std::false_type;
+            using C0_ = std::integral_constant<int, 0>;
+            using C1_ = std::integral_constant<int, 1>;
+            using C2_ = std::integral_constant<int, 2>;
+            unsigned capb = 0;
+#pragma unroll
+            for (int g = 0; g < NG; g++) capb |= uni(SS[g].capb);
             if (a.edges) {
-                if (uncapped) forward(T_{}, T_{}); else forward(T_{}, F_{});
+                if (!capb) forward(T_{}, C2_{}); else if (uncapped) forward(T_{}, C1_{}); else forward(T_{}, C0_{});
             } else {
-                if (uncapped) forward(F_{}, T_{}); else forward(F_{}, F_{});
+                if (!capb) forward(F_{}, C2_{}); else if (uncapped) forward(F_{}, C1_{}); else forward(F_{}, C0_{});
             }
         }
         wave_sync();
