@@ -156,7 +156,12 @@ constexpr unsigned MAX_ATOM_BYTES = 8;    // expanded atom = one u64 (raw: '▁'
 template <int G> struct Wfin;
 template <> struct Wfin<16> {
     using T = uint16_t;
-    static __device__ __forceinline__ T pack(unsigned r) { return (T)(((r >> 10) & 0xFFE0u) | (r & 31u)); }
+    // one v_bfi: bits 5..15 from r >> 10, the rest from r (bits 16+ fall off in the u16)
+    static __device__ __forceinline__ T pack(unsigned r) {
+        unsigned o;
+        asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(o) : "s"(0xFFE0u), "v"(r >> 10), "v"(r));
+        return (T)o;
+    }
     static __device__ __forceinline__ unsigned cost(T x) { return (x >> 6) == 1023u ? 0xFFFFu : (x >> 6); }
     static __device__ __forceinline__ bool invalid(T x) { return (x >> 5) & 1u; }
     static __device__ __forceinline__ unsigned gmax(T x) { return 31u - (x & 31u); }
