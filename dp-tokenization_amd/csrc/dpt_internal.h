@@ -55,7 +55,7 @@ int big_window_bytes();
 
 // host double-array trie over token bytes (dpt_vocab.cpp)
 struct DoubleArray {
-    // slot t: base[t] (| TERM bit when a token ends here), check[t] = parent slot (-1 free)
+    // slot t: base[t] (| TERM bit 31 when a token ends here, | LEAF bit 30 when no child), check[t] = parent slot (-1 free)
     int32_t *base = nullptr;
     int32_t *check = nullptr;
     int32_t *id = nullptr;

@@ -238,6 +238,8 @@ struct TrieView {
 };
 
 constexpr int32_t TERM_BIT = (int32_t)0x80000000;
+constexpr int32_t LEAF_BIT = 0x40000000;       // no children: the walk ends here
+constexpr int32_t BASE_MASK = 0x3FFFFFFF;
 
 // ------------------------------------------------------------------ arguments
 
@@ -474,6 +476,9 @@ __device__ bool prep_window(GroupLDS<CH, G> &L, uint8_t *gw, const WinRegs<CH> &
 
 // ------------------------------------------------------------------ the tokenize kernel
 
+#ifndef DPT_DOUBLE   // diagnostic builds only: run one phase twice to measure its marginal cost
+#define DPT_DOUBLE 0
+#endif
 #ifndef A_PREFETCH
 #define A_PREFETCH 0   // 1: load the walk's next atom one atom ahead (measured 6 % slower: VALU-bound)
 #endif
@@ -592,6 +597,10 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
         STAMP(0);
 
         // ---------------------------------------------------------- A: match discovery (all slots)
+#if DPT_DOUBLE == 1
+        for (int rep_ = 0; rep_ < 2; rep_++) {
+            if (rep_) wave_sync();
+#endif
         {
             unsigned pre[NG + 1];
             pre[0] = 0;
@@ -654,11 +663,12 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                             done = true;
                         } else {
                             w.node = t;
-                            w.nb = ent[q].x & 0x7FFFFFFF;
+                            w.nb = ent[q].x & BASE_MASK;
+                            const bool leaf = (ent[q].x & LEAF_BIT) != 0;
                             if (w.cnt == 0) {   // atom j+len-1 ends: the span j..j+len is a candidate token
                                 w.len++;
                                 if (ent[q].x & TERM_BIT) w.mask |= (M)1 << (w.len - 1);
-                                if ((w.info & AInfo<CH>::STOP) || w.len == (unsigned)G) {
+                                if (leaf || (w.info & AInfo<CH>::STOP) || w.len == (unsigned)G) {
                                     done = true;
                                 } else {
 #if A_PREFETCH
@@ -674,6 +684,8 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                                     w.seq = atom_from_info<CH>(L.bytes, w.info, raw, w.cnt);
 #endif
                                 }
+                            } else if (leaf) {
+                                done = true;   // no token continues inside this atom
                             }
                         }
                     }
@@ -690,6 +702,9 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 }
             }
         }
+#if DPT_DOUBLE == 1
+        }
+#endif
         wave_sync();
         STAMP(1);
 
@@ -863,6 +878,10 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
         wave_sync();
 
         // ---------------------------------------------------------- C1: selection, one lane per word
+#if DPT_DOUBLE == 3
+        for (int rep_ = 0; rep_ < 2; rep_++) {
+            if (rep_) wave_sync();
+#endif
         {
             unsigned pre[NG + 1], tokpre[NG + 1], inv_g[NG];
             pre[0] = 0; tokpre[0] = 0;
@@ -914,10 +933,17 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 }
             }
         }
+#if DPT_DOUBLE == 3
+        }
+#endif
         wave_sync();
         STAMP(3);
 
         // ---------------------------------------------------------- C2: ids (lanes over all slots' tokens)
+#if DPT_DOUBLE == 4
+        for (int rep_ = 0; rep_ < 2; rep_++) {
+            if (rep_) wave_sync();
+#endif
         {
             unsigned pre[NG + 1], na_g[NG];
             unsigned firstmask = 0;   // groups whose window starts the string (raw '▁' + first atom)
@@ -956,7 +982,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                             const int2 ent = tv.slots[sl];
                             ok &= ent.y == node;
                             node = sl;
-                            nb = ent.x & 0x7FFFFFFF;
+                            nb = ent.x & BASE_MASK;
                         }
                     }
                     const SlotState &S = SS[g];
@@ -964,6 +990,9 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 }
             }
         }
+#if DPT_DOUBLE == 4
+        }
+#endif
         wave_sync();
 
         // ---------------------------------------------------------- advance slots, finish strings

@@ -170,7 +170,7 @@ lane_kernel(Args a) {
                     int2 ent[RING];
 #pragma unroll
                     for (int k = 0; k < RING; k++) {
-                        t[k] = (nb[k] & 0x7FFFFFFF) + byte;
+                        t[k] = (nb[k] & 0x3FFFFFFF) + byte;   // bits 31/30: terminal / leaf
                         if (le && node[k] >= 0) ent[k] = load_slot(srd, t[k]);
                     }
 #pragma unroll

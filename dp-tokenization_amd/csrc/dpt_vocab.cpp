@@ -3,7 +3,8 @@
 // becomes a byte-level double-array trie that the kernels walk from L2.
 //
 //   slot t of a node reached by byte b from parent p:  t = base[p] + b, check[t] == p
-//   base[t] carries bit 31 when a token ends at t; id[t] is that token's id.
+//   base[t] carries bit 31 when a token ends at t (id[t] is that token's id) and bit 30 when
+//   the node has no children (a walk that reaches it is over without another lookup).
 //
 // Placement is first-fit over free slots (a find-next-free forest with path
 // compression), breadth-first from the root, so hot short prefixes sit in the
@@ -123,7 +124,7 @@ const char *build_double_array(const uint8_t *blob, const uint64_t *off, const i
             labels.push_back(nodes[c].label);
             kids.push_back(c);
         }
-        if (labels.empty()) { base[slot] = 0; continue; }
+        if (labels.empty()) { base[slot] = 0x40000000; continue; }   // leaf
         // smallest b >= 0 with every b+label free
         uint32_t x = labels[0];
         uint32_t b;
@@ -147,7 +148,7 @@ const char *build_double_array(const uint8_t *blob, const uint64_t *off, const i
             if (t > max_slot) max_slot = t;
             queue.push_back({kids[k], t});
         }
-        if (b > 0x7FFFFF00u) return "double array too large";
+        if (b > 0x3FFFFF00u) return "double array too large";
     }
     // mark terminals
     const uint32_t n_slots = max_slot + 1 + 256;
@@ -161,7 +162,7 @@ const char *build_double_array(const uint8_t *blob, const uint64_t *off, const i
     out->n_tokens = n_tok;
     out->max_bytes = max_bytes;
     out->max_cp = max_cp;
-    out->root_base = base[0] & 0x7FFFFFFF;
+    out->root_base = base[0] & 0x3FFFFFFF;
     out->base = (int32_t *)malloc(sizeof(int32_t) * n_slots);
     out->check = (int32_t *)malloc(sizeof(int32_t) * n_slots);
     out->id = (int32_t *)malloc(sizeof(int32_t) * n_slots);
