@@ -234,6 +234,7 @@ constexpr int block_lds_bytes() { return (64 / G) * (group_lds_bytes<CH, G>() + 
 struct TrieView {
     const int2 *__restrict__ slots;   // .x = base | TERM<<31, .y = check (parent slot, -1 free)
     const int32_t *__restrict__ ids;  // token id of a terminal slot
+    const int4 *__restrict__ slots4;  // {base, check, id, 0}: C2's walks get the id with the last node
     int32_t root_base;
 };
 
@@ -971,7 +972,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                     const unsigned j0 = (unsigned)L.rec[k].smask;
                     const unsigned j1 = k + 1 < ntk ? (unsigned)L.rec[k + 1].smask : na;
                     const bool first = raw && j0 == 0 && ((firstmask >> g) & 1u);
-                    int32_t node = 0, nb = tv.root_base;
+                    int32_t node = 0, nb = tv.root_base, id = -1;
                     bool ok = true;
                     for (unsigned jj = j0; jj < j1; jj++) {
                         const unsigned p0 = L.aoff[jj], la = L.atom_len(jj);
@@ -979,14 +980,15 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                         uint64_t seq = atom_from_info<CH>(L.bytes, AInfo<CH>::pack(p0, la, 0, first && jj == 0), raw, cnt);
                         for (; cnt; cnt--, seq >>= 8) {
                             const int32_t sl = nb + (int32_t)(seq & 0xFFu);
-                            const int2 ent = tv.slots[sl];
+                            const int4 ent = tv.slots4[sl];
                             ok &= ent.y == node;
                             node = sl;
                             nb = ent.x & BASE_MASK;
+                            id = ent.z;
                         }
                     }
                     const SlotState &S = SS[g];
-                    a.staging[S.sb + S.ntok + k] = ok ? tv.ids[node] : -1;
+                    a.staging[S.sb + S.ntok + k] = ok ? id : -1;
                 }
             }
         }
@@ -1107,7 +1109,7 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     a.edges = p.edges;
     a.work_next = p.retry_count + 1;
     a.wsl_scratch = p.wsl_scratch;
-    TrieView tv{p.slots, p.slot_ids, p.root_base};
+    TrieView tv{p.slots, p.slot_ids, p.slots4, p.root_base};
 
     hipLaunchKernelGGL(zero_first, dim3(1), dim3(64), 0, stream, p.id_off, p.retry_count);
     if (ev) hipEventRecord(ev[0], stream);
