@@ -1023,16 +1023,41 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
 
 // ------------------------------------------------------------------ compaction
 
+// One wave per 64 consecutive strings: their offsets arrive in one coalesced load per lane,
+// then the wave copies string after string with up to 256 ids (4 loads per lane) in flight.
 __global__ void __launch_bounds__(256) compact_kernel(const int32_t *__restrict__ staging, const uint64_t *__restrict__ str_off,
                                                       const uint64_t *__restrict__ id_off, uint64_t n_str,
                                                       int32_t *__restrict__ ids) {
     const uint64_t base_off = str_off[0];
     const unsigned lane = threadIdx.x & 63;
-    const uint64_t wstride = (uint64_t)gridDim.x * 4;
-    for (uint64_t s = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); s < n_str; s += wstride) {
-        const uint64_t src = str_off[s] - base_off, dst = id_off[s];
-        const uint64_t n = id_off[s + 1] - dst;
-        for (uint64_t k = lane; k < n; k += 64) ids[dst + k] = staging[src + k];
+    const uint64_t n_batches = (n_str + 63) / 64;
+    for (uint64_t bt = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); bt < n_batches; bt += (uint64_t)gridDim.x * 4) {
+        const uint64_t s = bt * 64 + lane;
+        uint64_t src = 0, dst = 0, n = 0;
+        if (s < n_str) {
+            src = str_off[s] - base_off;
+            dst = id_off[s];
+            n = id_off[s + 1] - dst;
+        }
+        const unsigned cnt = (unsigned)min((uint64_t)64, n_str - bt * 64);
+        for (unsigned t = 0; t < cnt; t++) {
+            const uint64_t so = uni64(__builtin_amdgcn_readlane((unsigned)src, t) | ((uint64_t)__builtin_amdgcn_readlane((unsigned)(src >> 32), t) << 32));
+            const uint64_t dO = ((uint64_t)__builtin_amdgcn_readlane((unsigned)(dst >> 32), t) << 32) | __builtin_amdgcn_readlane((unsigned)dst, t);
+            const unsigned nn = __builtin_amdgcn_readlane((unsigned)n, t);
+            for (unsigned k0 = 0; k0 < nn; k0 += 256) {
+                int32_t v[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const unsigned k = k0 + q * 64 + lane;
+                    v[q] = k < nn ? staging[so + k] : 0;
+                }
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const unsigned k = k0 + q * 64 + lane;
+                    if (k < nn) ids[dO + k] = v[q];
+                }
+            }
+        }
     }
 }
 
@@ -1137,8 +1162,8 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     }
     if (ev) hipEventRecord(ev[2], stream);
     if (p.n_str > 0) {
-        uint64_t blocks = (p.n_str + 3) / 4;
-        if (blocks > 8192) blocks = 8192;
+        uint64_t blocks = (p.n_str + 255) / 256;   // 4 waves x 64 strings
+        if (blocks > 4096) blocks = 4096;
         hipLaunchKernelGGL(compact_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, p.staging, p.str_off, p.id_off, p.n_str, p.ids);
     }
     if (ev) hipEventRecord(ev[3], stream);
