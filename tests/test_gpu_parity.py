@@ -174,3 +174,28 @@ def test_long_token_vocab_uses_64_lane_rows():
     texts += [" ".join(texts[k:k + 3]) for k in range(0, 300, 3)]
     text, offs = _csr(texts)
     _cmp_csr(Encoder(v).encode_csr(text, offs), oracle.OracleVocab(t2i).encode_csr(text, offs))
+
+
+def test_mixed_unicode_vs_oracle(engines, oracles):
+    """Valid UTF-8 with NUL, tabs, newlines, 2/3/4-byte code points (many outside the vocabulary,
+    so the capped DP and status 1 paths run) against the C oracle, raw mode."""
+    rng = np.random.default_rng(5)
+    pool = ["\x00", "\t", "\n", " ", "é", "ß", "ع", "中", "文", "😀", "🤖", "▁", "<0x0A>", "<s>"] + \
+           [chr(c) for c in range(0x21, 0x7F)] * 3
+    texts = ["".join(rng.choice(pool, size=int(rng.integers(0, 300)))) for _ in range(6000)]
+    text, offs = _csr(texts)
+    for name in ("llama32k", "toy1k"):
+        _cmp_csr(engines[name].encode_csr(text, offs), oracles[name].encode_csr(text, offs))
+
+
+def test_atoms_mode_limits():
+    """ATOMS mode: atoms of up to 8 bytes are walked exactly; a longer atom makes the string
+    status 3 (DptError through the compat layer) instead of a wrong answer."""
+    from dptok import Encoder, Vocab
+    t2i = {"abcdefgh": 0, "ab": 1, "cdefgh": 2, "x": 3, "abcdefghi": 4, "i": 5}
+    enc = Encoder(Vocab(t2i, 0))
+    (ids, st), (ids2, st2), (ids3, st3) = enc.encode_word_atoms([[["abcdefgh", "x"]], [["ab", "cdefgh"]],
+                                                                  [["abcdefghi"]]])
+    assert (ids, st) == ([0, 3], 0)
+    assert st2 == 0 and ids2 == [0]          # 'ab'+'cdefgh' = one token 'abcdefgh'
+    assert st3 == 3 and ids3 == []
