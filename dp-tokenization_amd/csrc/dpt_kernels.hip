@@ -232,11 +232,24 @@ constexpr int block_lds_bytes() { return (64 / G) * (group_lds_bytes<CH, G>() + 
 // ------------------------------------------------------------------ trie access
 
 struct TrieView {
-    const int2 *__restrict__ slots;   // .x = base | TERM<<31, .y = check (parent slot, -1 free)
+    const int2 *__restrict__ slots;   // .x = base | TERM<<31 | LEAF<<30, .y = check (parent slot, -1 free)
     const int32_t *__restrict__ ids;  // token id of a terminal slot
     const int4 *__restrict__ slots4;  // {base, check, id, 0}: C2's walks get the id with the last node
     int32_t root_base;
+    uint32_t n_slots;
 };
+
+// Trie reads through buffer resources: 32-bit slot offsets (no 64-bit address arithmetic) and a
+// range check that makes any index safe (out of range reads {0, 0}: a failed transition).
+__device__ __forceinline__ int2 trie_slot(const TrieView &tv, int32_t t) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)tv.slots, (short)0, (int)(tv.n_slots * 8u), 0x00020000);
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, (unsigned)t * 8u, 0, 0);
+    return make_int2((int32_t)v[0], (int32_t)v[1]);
+}
+__device__ __forceinline__ int4 trie_slot4(const TrieView &tv, int32_t t) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)tv.slots4, (short)0, (int)(tv.n_slots * 16u), 0x00020000);
+    return __builtin_bit_cast(int4, __builtin_amdgcn_raw_buffer_load_b128(r, (unsigned)t * 16u, 0, 0));
+}
 
 constexpr int32_t TERM_BIT = (int32_t)0x80000000;
 constexpr int32_t LEAF_BIT = 0x40000000;       // no children: the walk ends here
@@ -308,11 +321,21 @@ __device__ __forceinline__ uint64_t load_bytes(const uint8_t *bytes, unsigned p,
     return v & (~0ull >> (64u - 8u * la));   // 1 <= la <= 8
 }
 
-// expanded bytes of the atom described by `info` (AInfo)
-template <int CH>
+// expanded bytes of the atom described by `info` (AInfo).  WIDE (ATOMS mode): atoms of up to 8
+// bytes; otherwise (RAW / PRESPLIT) atoms are UTF-8 code points of at most 4 bytes, read with
+// two dword loads.
+template <int CH, bool WIDE>
 __device__ __forceinline__ uint64_t atom_from_info(const uint8_t *bytes, uint32_t info, bool raw, unsigned &cnt) {
     const unsigned la = AInfo<CH>::len(info);
-    const uint64_t v = load_bytes(bytes, AInfo<CH>::off(info), la);
+    const unsigned off = AInfo<CH>::off(info);
+    uint64_t v;
+    if constexpr (WIDE) {
+        v = load_bytes(bytes, off, la);
+    } else {
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(bytes) + (off >> 2);
+        const unsigned sh = 32u - 8u * la;   // 1 <= la <= 4
+        v = (__builtin_amdgcn_alignbyte(w[1], w[0], off & 3u) << sh) >> sh;
+    }
     const unsigned b0 = (unsigned)(v & 0xFFu);
     // branch-free selects (lanes of one wave take different cases)
     const bool fi = raw && (info & AInfo<CH>::FIRST) != 0;
@@ -395,7 +418,7 @@ __device__ bool window_bounds(const WinRegs<CH> &W, uint64_t slen, uint64_t pos,
 // Atomise window bytes [pos, pos+wlen) into L: the bytes themselves, atom byte offsets,
 // code-point prefixes (+ word-start bits) and the word list.  One packed DPP scan per 256
 // bytes.  Returns false if an atom is longer than MAX_ATOM_BYTES (4 bytes in RAW mode).
-template <int CH, int G>
+template <int CH, int G, bool WIDE>
 __device__ bool prep_window(GroupLDS<CH, G> &L, uint8_t *gw, const WinRegs<CH> &W, uint64_t pos,
                             unsigned wlen, int mode, unsigned lane, unsigned &n_atoms_o, unsigned &n_words_o) {
     const bool raw = mode == 0;
@@ -463,7 +486,7 @@ __device__ bool prep_window(GroupLDS<CH, G> &L, uint8_t *gw, const WinRegs<CH> &
     wave_sync();
     // per-atom walk descriptor for phase A (parked in fin[], which phase B overwrites):
     //   byte offset | byte length << 12 | "a word or the window ends after it" << 16 | "first atom of the string" << 17
-    const unsigned lim = raw ? 4u : MAX_ATOM_BYTES;   // raw: '▁' + one code point must fit 8 bytes
+    const unsigned lim = WIDE ? MAX_ATOM_BYTES : 4u;   // RAW / PRESPLIT: code points (and '▁' + one fits 8 bytes)
     bool bad = false;
     for (unsigned j = lane; j < n_atoms; j += 64) {
         const unsigned p0 = L.aoff[j], la = L.atom_len(j);
@@ -480,14 +503,8 @@ __device__ bool prep_window(GroupLDS<CH, G> &L, uint8_t *gw, const WinRegs<CH> &
 #ifndef DPT_DOUBLE   // diagnostic builds only: run one phase twice to measure its marginal cost
 #define DPT_DOUBLE 0
 #endif
-#ifndef A_PREFETCH
-#define A_PREFETCH 0   // 1: load the walk's next atom one atom ahead (measured 6 % slower: VALU-bound)
-#endif
-#ifndef A_WALKS
-#define A_WALKS 1   // concurrent trie walks per lane in phase A (2 measured slower once LDS allowed 19 waves/CU)
-#endif
 
-template <int CH, int G, bool BIG>
+template <int CH, int G, bool BIG, bool WIDE>
 __global__ void __launch_bounds__(64)
 tokenize_kernel(EncodeArgs a, TrieView tv) {
     constexpr int NG = 64 / G;
@@ -567,7 +584,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 unsigned wlen = 0, na = 0, nw = 0;
                 bool ok = status != 2;
                 if (ok) ok = window_bounds<CH>(W[g], slen, pos, mode, lane, wlen);
-                if (ok) ok = prep_window<CH, G>(L, wsl_of(g), W[g], pos, wlen, mode, lane, na, nw);
+                if (ok) ok = prep_window<CH, G, WIDE>(L, wsl_of(g), W[g], pos, wlen, mode, lane, na, nw);
                 if (ok) {
                     if (lane == 0) { S.wlen = wlen; S.n_atoms = na; S.n_words = nw; S.wtok = 0; S.inval = 0; S.capb = 0; }
                     prepared |= 1u << g;
@@ -608,99 +625,70 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
 #pragma unroll
             for (int g = 0; g < NG; g++) pre[g + 1] = pre[g] + uni(SS[g].n_atoms);
             const unsigned total = pre[NG];
-            // Each lane runs A_WALKS independent walks so that as many trie loads are in flight.
-            // Walk state: start atom j of group gsel, atoms matched so far (len), the trie node,
-            // the expanded bytes left of the current atom (seq, cnt) and of the next one (prefetched).
-            struct Walk {
-                unsigned gsel, j, len, cnt, ncnt;
-                int32_t nb, node;
-                uint32_t info, ninfo;
-                uint64_t seq, nseq;
-                M mask;
-                bool active;
-            };
-            auto start = [&](Walk &w, unsigned uu) {
+            // One walk per lane.  Walk state: start atom j, the LDS byte offset of its slot's group,
+            // atoms matched so far (len), the trie node, the expanded bytes left of the current atom
+            // (seq, cnt) and its descriptor (info).  Finished walks take the next start (ballot +
+            // mbcnt), so the wave stays busy.
+            unsigned j = 0, lbase = 0, len = 0, cnt = 0, info = 0;
+            int32_t nb = tv.root_base, node = 0;
+            uint64_t seq = 0;
+            M mask = 0;
+            auto start = [&](unsigned uu) {
                 unsigned gs = 0;
 #pragma unroll
                 for (int g = 1; g < NG; g++) gs += uu >= pre[g] ? 1u : 0u;
                 unsigned base = 0;
 #pragma unroll
                 for (int g = 0; g < NG; g++) base = (gs == (unsigned)g) ? pre[g] : base;
-                w.gsel = gs;
-                w.j = uu - base;
-                GL &L = grp(gs);
-                w.info = ainfo_get(L, w.j);
-                w.seq = atom_from_info<CH>(L.bytes, w.info, raw, w.cnt);
-#if A_PREFETCH
-                if (!(w.info & AInfo<CH>::STOP)) { w.ninfo = ainfo_get(L, w.j + 1); w.nseq = atom_from_info<CH>(L.bytes, w.ninfo, raw, w.ncnt); }
-#endif
-                w.nb = tv.root_base; w.node = 0; w.len = 0; w.mask = 0;
+                j = uu - base;
+                lbase = gs * (unsigned)group_lds_bytes<CH, G>();
+                const GL &L = *reinterpret_cast<const GL *>(smem + lbase);
+                info = ainfo_get(L, j);
+                seq = atom_from_info<CH, WIDE>(L.bytes, info, raw, cnt);
+                nb = tv.root_base; node = 0; len = 0; mask = 0;
             };
-            Walk W[A_WALKS];
-#pragma unroll
-            for (int q = 0; q < A_WALKS; q++) {
-                W[q].active = q * 64u + lane < total;
-                if (W[q].active) start(W[q], q * 64u + lane);
-            }
-            unsigned nxt = A_WALKS * 64u;
-            for (;;) {
-                bool any = false;
-#pragma unroll
-                for (int q = 0; q < A_WALKS; q++) any |= W[q].active;
-                if (!ballot(any)) break;
-                int2 ent[A_WALKS];
-#pragma unroll
-                for (int q = 0; q < A_WALKS; q++)   // issue every walk's load before using any
-                    ent[q] = tv.slots[W[q].active ? W[q].nb + (int32_t)(W[q].seq & 0xFFu) : 0];
-#pragma unroll
-                for (int q = 0; q < A_WALKS; q++) {
-                    Walk &w = W[q];
-                    bool done = false;
-                    if (w.active) {
-                        const int32_t t = w.nb + (int32_t)(w.seq & 0xFFu);
-                        w.seq >>= 8;
-                        w.cnt--;
-                        if (ent[q].y != w.node) {
-                            done = true;
-                        } else {
-                            w.node = t;
-                            w.nb = ent[q].x & BASE_MASK;
-                            const bool leaf = (ent[q].x & LEAF_BIT) != 0;
-                            if (w.cnt == 0) {   // atom j+len-1 ends: the span j..j+len is a candidate token
-                                w.len++;
-                                if (ent[q].x & TERM_BIT) w.mask |= (M)1 << (w.len - 1);
-                                if (leaf || (w.info & AInfo<CH>::STOP) || w.len == (unsigned)G) {
-                                    done = true;
-                                } else {
-#if A_PREFETCH
-                                    w.info = w.ninfo; w.seq = w.nseq; w.cnt = w.ncnt;
-                                    if (!(w.info & AInfo<CH>::STOP) && w.len + 1 < (unsigned)G) {
-                                        GL &L = grp(w.gsel);
-                                        w.ninfo = ainfo_get(L, w.j + w.len + 1);
-                                        w.nseq = atom_from_info<CH>(L.bytes, w.ninfo, raw, w.ncnt);
-                                    }
-#else
-                                    GL &L = grp(w.gsel);
-                                    w.info = ainfo_get(L, w.j + w.len);
-                                    w.seq = atom_from_info<CH>(L.bytes, w.info, raw, w.cnt);
-#endif
-                                }
-                            } else if (leaf) {
-                                done = true;   // no token continues inside this atom
+            bool active = lane < total;
+            if (active) start(lane);
+            unsigned nxt = 64;
+            while (ballot(active)) {
+                const int32_t t = nb + (int32_t)(seq & 0xFFu);
+                const int2 ent = trie_slot(tv, t);   // buffer load: inactive lanes read harmlessly
+                bool done = false;
+                if (active) {
+                    seq >>= 8;
+                    cnt--;
+                    if (ent.y != node) {
+                        done = true;
+                    } else {
+                        node = t;
+                        nb = ent.x & BASE_MASK;
+                        const bool leaf = (ent.x & LEAF_BIT) != 0;
+                        if (cnt == 0) {   // atom j+len-1 ends: the span j..j+len is a candidate token
+                            len++;
+                            if (ent.x & TERM_BIT) mask |= (M)1 << (len - 1);
+                            if (leaf || (info & AInfo<CH>::STOP) || len == (unsigned)G) {
+                                done = true;
+                            } else {
+                                const GL &L = *reinterpret_cast<const GL *>(smem + lbase);
+                                info = ainfo_get(L, j + len);
+                                seq = atom_from_info<CH, WIDE>(L.bytes, info, raw, cnt);
                             }
+                        } else if (leaf) {
+                            done = true;   // no token continues inside this atom
                         }
                     }
-                    const uint64_t dm = ballot(done);
-                    if (done) {
-                        grp(w.gsel).rec[w.j].smask = G == 16 ? (M)~w.mask : w.mask;   // B (G = 16) reads it inverted
-                        if (!(w.mask & 1u)) SS[w.gsel].capb = 1;
-                        const unsigned rank = __builtin_amdgcn_mbcnt_hi((unsigned)(dm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)dm, 0u));
-                        const unsigned uu = nxt + rank;
-                        w.active = uu < total;
-                        if (w.active) start(w, uu);
-                    }
-                    nxt += (unsigned)__builtin_popcountll(dm);
                 }
+                const uint64_t dm = ballot(done);
+                if (done) {
+                    GL &L = *reinterpret_cast<GL *>(smem + lbase);
+                    L.rec[j].smask = G == 16 ? (M)~mask : mask;   // B (G = 16) reads it inverted
+                    if (!(mask & 1u)) SS[lbase / (unsigned)group_lds_bytes<CH, G>()].capb = 1;
+                    const unsigned rank = __builtin_amdgcn_mbcnt_hi((unsigned)(dm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)dm, 0u));
+                    const unsigned uu = nxt + rank;
+                    active = uu < total;
+                    if (active) start(uu);
+                }
+                nxt += (unsigned)__builtin_popcountll(dm);
             }
         }
 #if DPT_DOUBLE == 1
@@ -977,10 +965,10 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                     for (unsigned jj = j0; jj < j1; jj++) {
                         const unsigned p0 = L.aoff[jj], la = L.atom_len(jj);
                         unsigned cnt;
-                        uint64_t seq = atom_from_info<CH>(L.bytes, AInfo<CH>::pack(p0, la, 0, first && jj == 0), raw, cnt);
+                        uint64_t seq = atom_from_info<CH, WIDE>(L.bytes, AInfo<CH>::pack(p0, la, 0, first && jj == 0), raw, cnt);
                         for (; cnt; cnt--, seq >>= 8) {
                             const int32_t sl = nb + (int32_t)(seq & 0xFFu);
-                            const int4 ent = tv.slots4[sl];
+                            const int4 ent = trie_slot4(tv, sl);
                             ok &= ent.y == node;
                             node = sl;
                             nb = ent.x & BASE_MASK;
@@ -1100,12 +1088,12 @@ static_assert(block_lds_bytes<SMALL_CH, 64>() <= 64 * 1024, "small LDS");
 static_assert(block_lds_bytes<BIG_CH, 64>() <= 160 * 1024, "big LDS");
 
 // Resident waves per CU for an instantiation (LDS / VGPR limited); DPT_WAVES_PER_CU overrides.
-template <int CH, int G, bool BIG>
+template <int CH, int G, bool BIG, bool WIDE>
 static unsigned resident_per_cu() {
     static unsigned cached = 0;
     if (cached) return cached;
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, tokenize_kernel<CH, G, BIG>, 64, block_lds_bytes<CH, G>()) != hipSuccess || nb <= 0)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, tokenize_kernel<CH, G, BIG, WIDE>, 64, block_lds_bytes<CH, G>()) != hipSuccess || nb <= 0)
         nb = 8;
     if (const char *e = getenv("DPT_WAVES_PER_CU")) {
         const int v = atoi(e);
@@ -1116,13 +1104,13 @@ static unsigned resident_per_cu() {
 }
 
 // Persistent grid: every resident wave pulls strings from the work counter until it runs dry.
-template <int CH, int G, bool BIG>
+template <int CH, int G, bool BIG, bool WIDE>
 static void launch_tok(const EncodeArgs &a, const TrieView &tv, uint64_t n_units, unsigned n_cu, hipStream_t stream) {
     constexpr int lds = block_lds_bytes<CH, G>();
-    uint64_t blocks = (uint64_t)n_cu * resident_per_cu<CH, G, BIG>();
+    uint64_t blocks = (uint64_t)n_cu * resident_per_cu<CH, G, BIG, WIDE>();
     if (blocks > (uint64_t)n_cu * 64u) blocks = (uint64_t)n_cu * 64u;   // the scratch is sized for 64 per CU
     if (blocks > n_units) blocks = n_units ? n_units : 1;
-    hipLaunchKernelGGL((tokenize_kernel<CH, G, BIG>), dim3((unsigned)blocks), dim3(64), lds, stream, a, tv);
+    hipLaunchKernelGGL((tokenize_kernel<CH, G, BIG, WIDE>), dim3((unsigned)blocks), dim3(64), lds, stream, a, tv);
 }
 
 hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t ev[6]) {
@@ -1134,7 +1122,8 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     a.edges = p.edges;
     a.work_next = p.retry_count + 1;
     a.wsl_scratch = p.wsl_scratch;
-    TrieView tv{p.slots, p.slot_ids, p.slots4, p.root_base};
+    TrieView tv{p.slots, p.slot_ids, p.slots4, p.root_base, p.n_slots};
+    const bool wide = (p.mode & DPT_MODE_MASK) == DPT_MODE_ATOMS;   // atoms of up to 8 bytes
 
     hipLaunchKernelGGL(zero_first, dim3(1), dim3(64), 0, stream, p.id_off, p.retry_count);
     if (ev) hipEventRecord(ev[0], stream);
@@ -1145,14 +1134,20 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
             launch_lane(p, (unsigned)blocks, stream);
         } else {
             const unsigned n_cu = p.max_blocks / 64;
-            if (p.variant == KERNEL_ROWS16) launch_tok<SMALL_CH, 16, false>(a, tv, (p.n_str + 3) / 4, n_cu, stream);
-            else launch_tok<SMALL_CH, 64, false>(a, tv, p.n_str, n_cu, stream);
+            if (p.variant == KERNEL_ROWS16) {
+                if (wide) launch_tok<SMALL_CH, 16, false, true>(a, tv, (p.n_str + 3) / 4, n_cu, stream);
+                else launch_tok<SMALL_CH, 16, false, false>(a, tv, (p.n_str + 3) / 4, n_cu, stream);
+            } else {
+                if (wide) launch_tok<SMALL_CH, 64, false, true>(a, tv, p.n_str, n_cu, stream);
+                else launch_tok<SMALL_CH, 64, false, false>(a, tv, p.n_str, n_cu, stream);
+            }
         }
         // second pass over the strings whose single word (or expansion) did not fit the small window
         EncodeArgs b = a;
         b.work_list = p.retry_list; b.work_count = p.retry_count;
         b.work_next = p.retry_count + 2;
-        launch_tok<BIG_CH, 64, true>(b, tv, p.n_str, p.max_blocks / 64, stream);
+        if (wide) launch_tok<BIG_CH, 64, true, true>(b, tv, p.n_str, p.max_blocks / 64, stream);
+        else launch_tok<BIG_CH, 64, true, false>(b, tv, p.n_str, p.max_blocks / 64, stream);
     }
     if (ev) hipEventRecord(ev[1], stream);
     if (p.n_str > 0) {
@@ -1193,8 +1188,11 @@ hipError_t launch_histogram(const uint64_t *id_off, const int32_t *status, uint6
 hipError_t kernel_init() {
     static bool done = false;
     if (done) return hipSuccess;
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&tokenize_kernel<BIG_CH, 64, true>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&tokenize_kernel<BIG_CH, 64, true, false>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, block_lds_bytes<BIG_CH, 64>());
+    if (e == hipSuccess)
+        e = hipFuncSetAttribute(reinterpret_cast<const void *>(&tokenize_kernel<BIG_CH, 64, true, true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, block_lds_bytes<BIG_CH, 64>());
     if (e == hipSuccess) done = true;
     return e;
 }
