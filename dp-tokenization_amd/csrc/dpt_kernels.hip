@@ -945,39 +945,62 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 firstmask |= (uni64(SS[g].pos) == 0 ? 1u : 0u) << g;
             }
             const unsigned total = pre[NG];
-            for (unsigned t0 = 0; t0 < total; t0 += 64) {
-                const unsigned t = t0 + lane;
-                if (t < total) {
-                    unsigned g = 0;
+            // One token walk per lane; a lane whose token is resolved writes the id and takes the
+            // next token (ballot + mbcnt), so each iteration is one trie step for 64 tokens.
+            unsigned jj = 0, j1 = 0, cnt = 0, lbase = 0;
+            int32_t node = 0, nb = 0, id = -1;
+            bool ok = true;
+            uint64_t seq = 0;
+            int32_t *out = nullptr;
+            auto tstart = [&](unsigned t) {
+                unsigned g = 0;
 #pragma unroll
-                    for (int k = 1; k < NG; k++) g += t >= pre[k] ? 1u : 0u;
-                    unsigned base = 0, na = 0, ntk = 0;
+                for (int k = 1; k < NG; k++) g += t >= pre[k] ? 1u : 0u;
+                unsigned base = 0, na = 0, ntk = 0, fw = 0;
 #pragma unroll
-                    for (int k = 0; k < NG; k++)
-                        if (g == (unsigned)k) { base = pre[k]; na = na_g[k]; ntk = pre[k + 1] - pre[k]; }
-                    GL &L = grp(g);
-                    const unsigned k = t - base;
-                    const unsigned j0 = (unsigned)L.rec[k].smask;
-                    const unsigned j1 = k + 1 < ntk ? (unsigned)L.rec[k + 1].smask : na;
-                    const bool first = raw && j0 == 0 && ((firstmask >> g) & 1u);
-                    int32_t node = 0, nb = tv.root_base, id = -1;
-                    bool ok = true;
-                    for (unsigned jj = j0; jj < j1; jj++) {
-                        const unsigned p0 = L.aoff[jj], la = L.atom_len(jj);
-                        unsigned cnt;
-                        uint64_t seq = atom_from_info<CH, WIDE>(L.bytes, AInfo<CH>::pack(p0, la, 0, first && jj == 0), raw, cnt);
-                        for (; cnt; cnt--, seq >>= 8) {
-                            const int32_t sl = nb + (int32_t)(seq & 0xFFu);
-                            const int4 ent = trie_slot4(tv, sl);
-                            ok &= ent.y == node;
-                            node = sl;
-                            nb = ent.x & BASE_MASK;
-                            id = ent.z;
+                for (int k = 0; k < NG; k++)
+                    if (g == (unsigned)k) { base = pre[k]; na = na_g[k]; ntk = pre[k + 1] - pre[k]; fw = (firstmask >> k) & 1u; }
+                lbase = g * (unsigned)group_lds_bytes<CH, G>();
+                const GL &L = *reinterpret_cast<const GL *>(smem + lbase);
+                const unsigned k = t - base;
+                jj = (unsigned)L.rec[k].smask;
+                j1 = k + 1 < ntk ? (unsigned)L.rec[k + 1].smask : na;
+                seq = atom_from_info<CH, WIDE>(L.bytes, AInfo<CH>::pack(L.aoff[jj], L.atom_len(jj), 0, raw && fw && jj == 0), raw, cnt);
+                node = 0; nb = tv.root_base; id = -1; ok = true;
+                const SlotState &S = SS[g];
+                out = a.staging + S.sb + S.ntok + k;
+            };
+            bool active = lane < total;
+            if (active) tstart(lane);
+            unsigned nxt = 64;
+            while (ballot(active)) {
+                const int32_t sl = nb + (int32_t)(seq & 0xFFu);
+                const int4 ent = trie_slot4(tv, sl);   // buffer load: inactive lanes read harmlessly
+                bool done = false;
+                if (active) {
+                    ok &= ent.y == node;
+                    node = sl;
+                    nb = ent.x & BASE_MASK;
+                    id = ent.z;
+                    seq >>= 8;
+                    if (--cnt == 0) {
+                        if (++jj == j1) {
+                            done = true;
+                        } else {
+                            const GL &L = *reinterpret_cast<const GL *>(smem + lbase);
+                            seq = atom_from_info<CH, WIDE>(L.bytes, AInfo<CH>::pack(L.aoff[jj], L.atom_len(jj), 0, 0), raw, cnt);
                         }
                     }
-                    const SlotState &S = SS[g];
-                    a.staging[S.sb + S.ntok + k] = ok ? id : -1;
                 }
+                const uint64_t dm = ballot(done);
+                if (done) {
+                    *out = ok ? id : -1;
+                    const unsigned rank = __builtin_amdgcn_mbcnt_hi((unsigned)(dm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)dm, 0u));
+                    const unsigned uu = nxt + rank;
+                    active = uu < total;
+                    if (active) tstart(uu);
+                }
+                nxt += (unsigned)__builtin_popcountll(dm);
             }
         }
 #if DPT_DOUBLE == 4
