@@ -60,7 +60,8 @@ extern "C" {
 #define DPT_STATUS_OK 0
 #define DPT_STATUS_NO_TOKENIZATION 1 /* reference: ipdb.set_trace / ValueError (dp_tokenize.py:84) */
 #define DPT_STATUS_EMPTY_WORD 2      /* reference: IndexError (dp_tokenize.py:49) */
-#define DPT_STATUS_TOO_LONG 3        /* a single word longer than the engine's window (4096 bytes) */
+#define DPT_STATUS_TOO_LONG 3        /* outside the engine's limits: a word > 2048 bytes, an atom > 8 bytes
+                                        (ATOMS) or a UTF-8 run > 4 bytes (RAW / PRESPLIT, malformed input) */
 #define DPT_STATUS_INTERNAL 4        /* engine invariant violated (never expected) */
 
 typedef struct dpt_vocab dpt_vocab;
@@ -104,7 +105,10 @@ int dpt_ctx_reserve(dpt_ctx *c, uint64_t n_bytes, uint64_t n_str);
  *   status[s]                      DPT_STATUS_*
  *   capped_len[s] (nullable)       sum over words of the reference's len_dp[-1] (dp_tokenize.py:70), -1 if unknown
  * ids_cap must be >= n_bytes (a string never yields more ids than bytes).
- * cut_mask (PRESPLIT only, n_bytes bytes): 1 where a word starts; byte 0 of every string always starts one.
+ * cut_mask (n_bytes bytes, PRESPLIT and ATOMS only): PRESPLIT: != 0 where a word starts (byte 0 of
+ * every string always starts one); ATOMS: bit 1 where an atom starts, bit 0 where a word starts.
+ * Limits: every string < 4 GiB, n_str < 2^31; RAW / PRESPLIT text is UTF-8 (code points are the
+ * atoms); words longer than 2048 bytes get DPT_STATUS_TOO_LONG.
  * Stream-ordered on hip_stream (hipStream_t, NULL = default stream); no host synchronisation.
  */
 int dpt_encode(dpt_ctx *c, const dpt_vocab *v, int mode, const uint8_t *text, uint64_t n_bytes,
