@@ -131,7 +131,7 @@ template <int G> struct Group;
 template <> struct Group<16> {
     using M = uint16_t;  // span mask: bit L-1 = an L-atom token starts here
     struct Rec { uint16_t cpos; uint16_t smask; };
-    struct Fin { uint16_t v; };
+    struct Fin { uint8_t v; };   // dg | de << 4
     static __device__ __forceinline__ unsigned dg(const Fin &x) { return x.v & 15u; }
     static __device__ __forceinline__ unsigned de(const Fin &x) { return (x.v >> 4) & 15u; }
 };
@@ -301,15 +301,16 @@ template <int CH> struct AInfo {
     static __device__ __forceinline__ unsigned len(unsigned x) { return (x >> PB) & 15u; }
 };
 
+// G = 16 derives it from the atom offsets and the next atom's word-start bit (its u8 fin[]
+// has no room; LDS per slot bounds the resident waves); G = 64 parks it in fin[].d
 template <int CH, int G>
-__device__ __forceinline__ unsigned ainfo_get(const GroupLDS<CH, G> &L, unsigned j) {
-    if constexpr (G == 16) return L.fin[j].v;
+__device__ __forceinline__ unsigned ainfo_get(const GroupLDS<CH, G> &L, unsigned j, bool first) {
+    if constexpr (G == 16) return AInfo<CH>::pack(L.aoff[j], L.atom_len(j), L.rec[j + 1].cpos >> 15, first && j == 0);
     else return L.fin[j].d;
 }
 template <int CH, int G>
 __device__ __forceinline__ void ainfo_set(GroupLDS<CH, G> &L, unsigned j, unsigned v) {
-    if constexpr (G == 16) L.fin[j].v = (uint16_t)v;
-    else L.fin[j].d = v;
+    if constexpr (G != 16) L.fin[j].d = v;
 }
 
 // la (<= 8) window bytes from offset p: three aligned dword reads and a funnel shift
@@ -625,6 +626,9 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
 #pragma unroll
             for (int g = 0; g < NG; g++) pre[g + 1] = pre[g] + uni(SS[g].n_atoms);
             const unsigned total = pre[NG];
+            unsigned fwmask = 0;   // slots whose window starts the string (raw: '▁' + first atom)
+#pragma unroll
+            for (int g = 0; g < NG; g++) fwmask |= (uni(SS[g].pos) == 0 ? 1u : 0u) << g;
             // One walk per lane.  Walk state: start atom j, the LDS byte offset of its slot's group,
             // atoms matched so far (len), the trie node, the expanded bytes left of the current atom
             // (seq, cnt) and its descriptor (info).  Finished walks take the next start (ballot +
@@ -643,7 +647,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 j = uu - base;
                 lbase = gs * (unsigned)group_lds_bytes<CH, G>();
                 const GL &L = *reinterpret_cast<const GL *>(smem + lbase);
-                info = ainfo_get(L, j);
+                info = ainfo_get(L, j, raw && ((fwmask >> gs) & 1u));
                 seq = atom_from_info<CH, WIDE>(L.bytes, info, raw, cnt);
                 nb = tv.root_base; node = 0; len = 0; mask = 0;
             };
@@ -670,7 +674,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                                 done = true;
                             } else {
                                 const GL &L = *reinterpret_cast<const GL *>(smem + lbase);
-                                info = ainfo_get(L, j + len);
+                                info = ainfo_get(L, j + len, false);
                                 seq = atom_from_info<CH, WIDE>(L.bytes, info, raw, cnt);
                             }
                         } else if (leaf) {
@@ -753,7 +757,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                             // lowest set bit of the row; bits of other rows only land in fields
                             // of positions C1 never reads (see Group<16>)
                             const unsigned dg = ffbl(gs), de = ffbl(es);
-                            L.fin[i].v = (uint16_t)(dg | (de << 4));
+                            L.fin[i].v = (uint8_t)(dg | (de << 4));
                             L.rec[i].smask = Wfin<G>::pack(r);   // rec[i] was consumed at step i-1
                             if constexpr (edges)
                                 if (i <= na) a.edges[SS[mg].sb + SS[mg].abase + i - 1] = es & 0xFFFFu;
