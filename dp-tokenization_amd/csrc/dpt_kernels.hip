@@ -211,17 +211,21 @@ struct GroupLDS {
         if constexpr (WSLG) gw[w] = (uint8_t)v;
         else wsl[w] = (Idx)v;
     }
-    alignas(16) uint8_t bytes[CH + 16];         // the window's input bytes (expanded on the fly)
+    // the window's input bytes (expanded on the fly); the dword reads of the last atoms run up to
+    // 12 bytes past the end, into the next group or the slot states -- masked off, never used
+    alignas(16) uint8_t bytes[CH];
 };
 
 // strings are < 4 GiB (dpt.h); abase: atoms of the string's earlier windows
+// (48 bytes: LDS per slot is what bounds the resident waves)
 struct SlotState {
     uint64_t sb;
-    uint32_t s, slen, pos, active;
-    uint32_t status, ntok, capsum, wlen;
-    uint32_t n_atoms, n_words, wtok, inval;
-    uint32_t abase, capb;   // capb: some atom of the window is not a token by itself (the cap can bind)
+    uint32_t s, slen, pos, ntok, capsum, wtok;
+    uint32_t abase;
+    uint16_t wlen, n_atoms, n_words;
+    uint8_t active, status, inval, capb;   // capb: some atom of the window is not a token by itself (the cap can bind)
 };
+static_assert(sizeof(SlotState) == 48, "slot state layout");
 
 template <int CH, int G>
 constexpr int group_lds_bytes() { return (int)((sizeof(GroupLDS<CH, G>) + 15) & ~size_t(15)); }
