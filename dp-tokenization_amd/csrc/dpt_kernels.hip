@@ -342,14 +342,18 @@ __device__ __forceinline__ uint64_t atom_from_info(const uint8_t *bytes, uint32_
         v = (__builtin_amdgcn_alignbyte(w[1], w[0], off & 3u) << sh) >> sh;
     }
     const unsigned b0 = (unsigned)(v & 0xFFu);
-    // branch-free selects (lanes of one wave take different cases)
+    // expansions (raw mode only); the selects run only when some lane of the wave needs one
     const bool fi = raw && (info & AInfo<CH>::FIRST) != 0;
     const bool sp = raw && !fi && b0 == ' ';
     const bool nl = raw && !fi && b0 == '\n';
-    uint64_t seq = fi ? (0x8196E2ull | (v << 24)) : v;
-    seq = sp ? 0x8196E2ull : seq;
-    seq = nl ? 0x3E413078303Cull : seq;
-    cnt = fi ? 3 + la : (sp ? 3u : (nl ? 6u : la));
+    uint64_t seq = v;
+    cnt = la;
+    if (ballot(fi || sp || nl)) {
+        seq = fi ? (0x8196E2ull | (v << 24)) : seq;
+        seq = sp ? 0x8196E2ull : seq;
+        seq = nl ? 0x3E413078303Cull : seq;
+        cnt = fi ? 3 + la : (sp ? 3u : (nl ? 6u : la));
+    }
     return seq;
 }
 
