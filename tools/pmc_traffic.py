@@ -30,17 +30,18 @@ def source_hash(read=None) -> str:
     return h.hexdigest()
 
 
-def run_pass(counter: str, n: int, out: str) -> float:
+def run_pass(counter: str, n: int, out: str, rerun: bool = True) -> float:
     env = dict(os.environ, TMPDIR="/tmp")
     cmd = ["rocprofv3", "--kernel-trace", "--pmc", counter, "-d", out, "-o", "run", "--output-format", "csv",
            "--", sys.executable, os.path.join(ROOT, "tools", "prof_driver.py"), str(n), "3", "ascii"]
-    with open(out + ".log", "w") as log:
-        subprocess.run(cmd, check=True, stdout=log, stderr=subprocess.STDOUT, env=env, timeout=600)
+    if rerun:
+        with open(out + ".log", "w") as log:
+            subprocess.run(cmd, check=True, stdout=log, stderr=subprocess.STDOUT, env=env, timeout=600)
     vals = []
     for f in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
         for row in csv.DictReader(open(f)):
-            if "tokenize_kernel" in row.get("Kernel_Name", "") and "true>" not in row["Kernel_Name"] \
-                    and row["Counter_Name"] == counter:
+            name = row.get("Kernel_Name", "")
+            if "tokenize_kernel<256" in name and row["Counter_Name"] == counter:   # the first pass only
                 vals.append(float(row["Counter_Value"]))
     if not vals:
         raise RuntimeError("no %s samples for the tokenize kernel" % counter)
@@ -52,8 +53,9 @@ def main():
     tag = sys.argv[2] if len(sys.argv) > 2 else "traffic"
     out = os.path.join(ROOT, "gpurun_out", "pmc_" + tag)
     os.makedirs(out, exist_ok=True)
-    fetch = run_pass("FETCH_SIZE", n, os.path.join(out, "fetch"))
-    write = run_pass("WRITE_SIZE", n, os.path.join(out, "write"))
+    rerun = os.environ.get("PMC_REUSE") != "1"   # PMC_REUSE=1: re-read the CSVs of a previous run
+    fetch = run_pass("FETCH_SIZE", n, os.path.join(out, "fetch"), rerun)
+    write = run_pass("WRITE_SIZE", n, os.path.join(out, "write"), rerun)
     rec = {"source_sha256": source_hash(), "workload": "cfg2 %d x 256 B random ASCII" % n, "n_str": n,
            "fetch_bytes_raw": fetch, "fetch_bytes": 2 * fetch, "write_bytes": write,
            "traffic_bytes_per_launch": 2 * fetch + write,
