@@ -162,10 +162,6 @@ int dpt_vocab_create(const uint8_t *utf8_blob, const uint64_t *tok_off, const in
     dpt::DoubleArray da;
     const char *err = dpt::build_double_array(utf8_blob, tok_off, ids, n_tok, &da);
     if (err) return fail(DPT_E_VOCAB, err);
-    if (da.max_cp > 64) {
-        dpt::free_double_array(&da);
-        return fail(DPT_E_VOCAB, "vocabulary has a token longer than 64 code points (engine span limit)");
-    }
     DeviceGuard g(device);
     hipError_t e = dpt::kernel_init();
     if (e != hipSuccess) {
@@ -293,6 +289,7 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
     p.retry_list = c->retry_list;
     p.retry_count = c->retry_count;
     p.wsl_scratch = c->wsl_scratch;
+    p.long_span = v->stats.max_cp > 64 ? 1 : 0;
     p.scan_temp = c->scan_temp;
     p.scan_temp_bytes = c->scan_bytes;
     p.max_blocks = c->max_blocks;

@@ -25,6 +25,7 @@ struct EncodeLaunch {
     uint32_t *retry_list;
     uint32_t *retry_count;
     uint8_t *wsl_scratch;    // max_blocks x wsl_scratch_bytes(1) bytes
+    int long_span;           // vocabulary tokens longer than 64 code points: words over 64 atoms -> status 3
     void *scan_temp;
     size_t scan_temp_bytes;
     unsigned max_blocks;

@@ -276,6 +276,7 @@ struct EncodeArgs {
     const uint32_t *work_count;
     uint32_t *work_next;        // dynamic work distribution counter (zeroed per launch)
     uint8_t *wsl_scratch;       // word lists of the 256-byte pass: grid x NG x WSL_STRIDE bytes
+    int long_span;              // the vocabulary has tokens longer than 64 code points
     uint64_t *edges;            // nullable: per atom end, the E(i) & reachable back-distance mask
     int mode;                   // DPT_MODE_* | DPT_FLAG_*
 };
@@ -856,12 +857,16 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 unsigned wbase = 0;
 #pragma unroll
                 for (int k = 0; k < NG; k++) wbase = g == (unsigned)k ? pre[k] : wbase;
-                unsigned cost = 0, inv = 0;
+                unsigned cost = 0, inv = 0, lng = 0;
                 if (u < total) {
                     const GL &L = grp(g);
-                    const typename Wfin<G>::T F = L.wkey(L.word_end(wsl_of(g), u - wbase));
+                    const unsigned we = L.word_end(wsl_of(g), u - wbase);
+                    const typename Wfin<G>::T F = L.wkey(we);
                     cost = Wfin<G>::cost(F);
                     inv = Wfin<G>::invalid(F) ? 1u : 0u;
+                    // a vocabulary token longer than G code points could span more than G atoms,
+                    // beyond the walks: such a word is outside the engine's limits (status 3)
+                    if (a.long_span) lng = we - L.word_start(wsl_of(g), u - wbase) > (unsigned)G ? 1u : 0u;
                 }
                 // per-group sums over this chunk: groups own contiguous lane ranges
 #pragma unroll
@@ -871,7 +876,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                     const bool mine = lane >= lo && lane < (hi < 64u ? hi : 64u);
                     const unsigned cs = wave_incl_scan_add(mine ? cost : 0u);
                     const unsigned csum = __builtin_amdgcn_readlane(cs, 63);
-                    const unsigned anyinv = ballot(mine && inv) != 0 ? 1u : 0u;
+                    const unsigned anyinv = (ballot(mine && inv) != 0 ? 1u : 0u) | (ballot(mine && lng) != 0 ? 2u : 0u);
                     if (lane == 0) { SS[k].wtok += csum; SS[k].inval |= anyinv; }
                 }
             }
@@ -1025,7 +1030,8 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
             SlotState &S = SS[lane];
             if (S.active && S.n_atoms > 0) {
                 S.capsum += S.wtok;
-                if (S.inval && S.status == 0) S.status = 1;
+                if (S.status == 0 && (S.inval & 2)) S.status = 3;   // a word beyond the span limit
+                if (S.status == 0 && S.inval) S.status = 1;
                 if (S.status == 0 && !len_only) S.ntok += S.wtok;
                 S.pos += S.wlen;
                 S.abase += S.n_atoms;
@@ -1033,7 +1039,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                     const uint64_t s = S.s;
                     a.status[s] = (int32_t)S.status;
                     a.counts[s] = S.status == 0 ? (uint64_t)S.ntok : 0ull;
-                    if (a.capped) a.capped[s] = (int32_t)S.capsum;
+                    if (a.capped) a.capped[s] = S.status == 3 ? -1 : (int32_t)S.capsum;
                     S.active = 0;
                 }
             }
@@ -1157,6 +1163,7 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     a.edges = p.edges;
     a.work_next = p.retry_count + 1;
     a.wsl_scratch = p.wsl_scratch;
+    a.long_span = p.long_span;
     TrieView tv{p.slots, p.slot_ids, p.slots4, p.root_base, p.n_slots};
     const bool wide = (p.mode & DPT_MODE_MASK) == DPT_MODE_ATOMS;   // atoms of up to 8 bytes
 

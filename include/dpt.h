@@ -42,7 +42,7 @@ extern "C" {
 #define DPT_OK 0
 #define DPT_E_ARG (-1)      /* bad argument (null pointer, size) */
 #define DPT_E_HIP (-2)      /* HIP runtime error */
-#define DPT_E_VOCAB (-3)    /* vocabulary not supported (e.g. a token longer than 64 code points) */
+#define DPT_E_VOCAB (-3)    /* vocabulary not supported (e.g. a token longer than 65535 bytes) */
 #define DPT_E_CAP (-4)      /* output capacity too small */
 #define DPT_E_NODEV (-5)    /* no HIP device */
 
@@ -108,7 +108,8 @@ int dpt_ctx_reserve(dpt_ctx *c, uint64_t n_bytes, uint64_t n_str);
  * cut_mask (n_bytes bytes, PRESPLIT and ATOMS only): PRESPLIT: != 0 where a word starts (byte 0 of
  * every string always starts one); ATOMS: bit 1 where an atom starts, bit 0 where a word starts.
  * Limits: every string < 4 GiB, n_str < 2^31; RAW / PRESPLIT text is UTF-8 (code points are the
- * atoms); words longer than 2048 bytes get DPT_STATUS_TOO_LONG.
+ * atoms); words longer than 2048 bytes get DPT_STATUS_TOO_LONG, and so do words of more than 64
+ * atoms when the vocabulary has tokens longer than 64 code points (spans the engine does not walk).
  * Stream-ordered on hip_stream (hipStream_t, NULL = default stream); no host synchronisation.
  */
 int dpt_encode(dpt_ctx *c, const dpt_vocab *v, int mode, const uint8_t *text, uint64_t n_bytes,

@@ -199,3 +199,25 @@ def test_atoms_mode_limits():
     assert (ids, st) == ([0, 3], 0)
     assert st2 == 0 and ids2 == [0]          # 'ab'+'cdefgh' = one token 'abcdefgh'
     assert st3 == 3 and ids3 == []
+
+
+def test_tokens_longer_than_64_code_points():
+    """A vocabulary with tokens of 65..80 code points is accepted: words of up to 64 atoms are
+    exact; longer words (where such a token could match) get status 3 instead of a wrong answer."""
+    from dptok import Encoder, Vocab, synth
+    from oracle import oracle
+    t2i = dict(synth.llama_shaped_vocab())
+    rng = np.random.default_rng(4)
+    for L in (65, 70, 80):
+        for _ in range(10):
+            t2i.setdefault("".join(chr(c) for c in rng.integers(0x61, 0x64, size=L)), len(t2i))
+    v = Vocab(t2i, 0)
+    assert v.stats["max_cp"] >= 80
+    short = ["".join(chr(c) for c in rng.integers(0x61, 0x64, size=rng.integers(1, 64))) for _ in range(2000)]
+    short += [" ".join(short[k:k + 3]) for k in range(0, 300, 3)]
+    text, offs = _csr(short)
+    _cmp_csr(Encoder(v).encode_csr(text, offs), oracle.OracleVocab(t2i).encode_csr(text, offs))
+    long_ = ["x" + "".join(chr(c) for c in rng.integers(0x61, 0x64, size=rng.integers(65, 120))) for _ in range(50)]
+    text, offs = _csr(long_)
+    _, _, st, cap = Encoder(v).encode_csr(text, offs)
+    assert (st == 3).all() and (cap == -1).all()
