@@ -510,6 +510,9 @@ __device__ bool prep_window(GroupLDS<CH, G> &L, uint8_t *gw, const WinRegs<CH> &
 
 // ------------------------------------------------------------------ the tokenize kernel
 
+#ifndef A_REFILL
+#define A_REFILL 32   // phase A: idle lanes needed before a batched refill (1/8/16/32 within 2 %)
+#endif
 #ifndef DPT_DOUBLE   // diagnostic builds only: run one phase twice to measure its marginal cost
 #define DPT_DOUBLE 0
 #endif
@@ -660,10 +663,23 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 seq = atom_from_info<CH, WIDE>(L.bytes, info, raw, cnt);
                 nb = tv.root_base; node = 0; len = 0; mask = 0;
             };
-            bool active = lane < total;
-            if (active) start(lane);
-            unsigned nxt = 64;
-            while (ballot(active)) {
+            // Refills are batched: idle lanes take new starts only once A_REFILL of them are idle
+            // (or the remaining starts fit), so the refill code runs on a fraction of the steps.
+            bool active = false;
+            unsigned nxt = 0;
+            for (;;) {
+                {
+                    const uint64_t im = ballot(!active);
+                    const unsigned nidle = (unsigned)__builtin_popcountll(im);
+                    if (nxt < total && (nidle >= A_REFILL || total - nxt <= nidle)) {
+                        if (!active) {
+                            const unsigned uu = nxt + __builtin_amdgcn_mbcnt_hi((unsigned)(im >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)im, 0u));
+                            if (uu < total) { active = true; start(uu); }
+                        }
+                        nxt += nidle;
+                    }
+                }
+                if (!ballot(active)) break;
                 const int32_t t = nb + (int32_t)(seq & 0xFFu);
                 const int2 ent = trie_slot(tv, t);   // buffer load: inactive lanes read harmlessly
                 bool done = false;
@@ -691,17 +707,12 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                         }
                     }
                 }
-                const uint64_t dm = ballot(done);
                 if (done) {
                     GL &L = *reinterpret_cast<GL *>(smem + lbase);
                     L.rec[j].smask = G == 16 ? (M)~mask : mask;   // B (G = 16) reads it inverted
                     if (!(mask & 1u)) SS[lbase / (unsigned)group_lds_bytes<CH, G>()].capb = 1;
-                    const unsigned rank = __builtin_amdgcn_mbcnt_hi((unsigned)(dm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)dm, 0u));
-                    const unsigned uu = nxt + rank;
-                    active = uu < total;
-                    if (active) start(uu);
+                    active = false;
                 }
-                nxt += (unsigned)__builtin_popcountll(dm);
             }
         }
 #if DPT_DOUBLE == 1
