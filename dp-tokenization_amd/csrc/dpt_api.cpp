@@ -174,17 +174,34 @@ int dpt_vocab_create(const uint8_t *utf8_blob, const uint64_t *tok_off, const in
         return fail(DPT_E_ARG, "out of host memory");
     }
     v->device = device;
-    std::vector<int2> slots(da.n_slots);
+    // slots, then the two-byte root table: entry b0 << 8 | b1 describes the walk from the root over
+    // bytes b0 b1 -- .x = base word of the node reached (0 if none), .y = that node's slot (0 if
+    // none) | 1 << 30 if b0 is a root child | 1 << 31 if b0 alone is a token.  Phase A's first
+    // lookup of every walk consumes two bytes through it.
+    std::vector<int2> slots((size_t)da.n_slots + 65536);
     std::vector<int4> slots4(da.n_slots);
     for (uint32_t t = 0; t < da.n_slots; t++) {
         slots[t] = make_int2(da.base[t], da.check[t]);
         slots4[t] = make_int4(da.base[t], da.check[t], da.id[t], 0);
     }
-    e = hipMalloc((void **)&v->d_slots, sizeof(int2) * da.n_slots);
+    for (uint32_t b0 = 0; b0 < 256; b0++) {
+        const uint32_t s1 = (uint32_t)da.root_base + b0;
+        const bool e1 = s1 < da.n_slots && da.check[s1] == 0;
+        const bool term1 = e1 && (da.base[s1] & (int32_t)0x80000000);
+        const bool leaf1 = e1 && (da.base[s1] & 0x40000000);
+        const uint32_t base1 = e1 ? (uint32_t)(da.base[s1] & 0x3FFFFFFF) : 0u;
+        for (uint32_t b1 = 0; b1 < 256; b1++) {
+            const uint32_t s2 = base1 + b1;
+            const bool e2 = e1 && !leaf1 && s2 < da.n_slots && da.check[s2] == (int32_t)s1;
+            const uint32_t y = (e2 ? s2 : 0u) | (e1 ? 0x40000000u : 0u) | (term1 ? 0x80000000u : 0u);
+            slots[(size_t)da.n_slots + (b0 << 8) + b1] = make_int2(e2 ? da.base[s2] : 0, (int32_t)y);
+        }
+    }
+    e = hipMalloc((void **)&v->d_slots, sizeof(int2) * slots.size());
     if (e == hipSuccess) e = hipMalloc((void **)&v->d_slots4, sizeof(int4) * da.n_slots);
     if (e == hipSuccess) e = hipMemcpy(v->d_slots4, slots4.data(), sizeof(int4) * da.n_slots, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc((void **)&v->d_ids, sizeof(int32_t) * da.n_slots);
-    if (e == hipSuccess) e = hipMemcpy(v->d_slots, slots.data(), sizeof(int2) * da.n_slots, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(v->d_slots, slots.data(), sizeof(int2) * slots.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(v->d_ids, da.id, sizeof(int32_t) * da.n_slots, hipMemcpyHostToDevice);
     if (e != hipSuccess) {
         dpt::free_double_array(&da);
@@ -200,7 +217,7 @@ int dpt_vocab_create(const uint8_t *utf8_blob, const uint64_t *tok_off, const in
     v->stats.n_slots = da.n_slots;
     v->stats.max_bytes = da.max_bytes;
     v->stats.max_cp = da.max_cp;
-    v->stats.device_bytes = (uint64_t)da.n_slots * (sizeof(int2) + sizeof(int32_t) + sizeof(int4));
+    v->stats.device_bytes = (uint64_t)da.n_slots * (sizeof(int2) + sizeof(int32_t) + sizeof(int4)) + 65536 * sizeof(int2);
     dpt::free_double_array(&da);
     *out = v;
     return DPT_OK;

@@ -236,7 +236,9 @@ constexpr int block_lds_bytes() { return (64 / G) * (group_lds_bytes<CH, G>() + 
 // ------------------------------------------------------------------ trie access
 
 struct TrieView {
-    const int2 *__restrict__ slots;   // .x = base | TERM<<31 | LEAF<<30, .y = check (parent slot, -1 free)
+    // .x = base | TERM<<31 | LEAF<<30, .y = check (parent slot, -1 free); followed by the 65536-entry
+    // two-byte root table (entry b0 << 8 | b1 at slots[n_slots + ...], see dpt_api.cpp)
+    const int2 *__restrict__ slots;
     const int32_t *__restrict__ ids;  // token id of a terminal slot
     const int4 *__restrict__ slots4;  // {base, check, id, 0}: C2's walks get the id with the last node
     int32_t root_base;
@@ -246,7 +248,7 @@ struct TrieView {
 // Trie reads through buffer resources: 32-bit slot offsets (no 64-bit address arithmetic) and a
 // range check that makes any index safe (out of range reads {0, 0}: a failed transition).
 __device__ __forceinline__ int2 trie_slot(const TrieView &tv, int32_t t) {
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)tv.slots, (short)0, (int)(tv.n_slots * 8u), 0x00020000);
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)tv.slots, (short)0, (int)((tv.n_slots + 65536u) * 8u), 0x00020000);
     const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, (unsigned)t * 8u, 0, 0);
     return make_int2((int32_t)v[0], (int32_t)v[1]);
 }
@@ -645,7 +647,8 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
             // atoms matched so far (len), the trie node, the expanded bytes left of the current atom
             // (seq, cnt) and its descriptor (info).  Finished walks take the next start (ballot +
             // mbcnt), so the wave stays busy.
-            unsigned j = 0, lbase = 0, len = 0, cnt = 0, info = 0;
+            unsigned j = 0, lbase = 0, len = 0, cnt = 0, info = 0, t2 = 0;
+            bool split = false;
             int32_t nb = tv.root_base, node = 0;
             uint64_t seq = 0;
             M mask = 0;
@@ -662,6 +665,25 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 info = ainfo_get(L, j, raw && ((fwmask >> gs) & 1u));
                 seq = atom_from_info<CH, WIDE>(L.bytes, info, raw, cnt);
                 nb = tv.root_base; node = 0; len = 0; mask = 0;
+                // The first two expanded bytes go through one lookup of the two-byte root table
+                // (TrieView): within atom j, or across its end when the word continues (then
+                // atom j+1 is loaded now instead of at the first atom end).
+                const unsigned b0 = (unsigned)(seq & 0xFFu);
+                if (cnt >= 2) {
+                    t2 = tv.n_slots + (b0 << 8) + (unsigned)((seq >> 8) & 0xFFu);
+                    split = false;
+                    seq >>= 16;
+                    cnt -= 2;
+                } else if (!(info & AInfo<CH>::STOP)) {
+                    info = ainfo_get(L, j + 1, false);
+                    seq = atom_from_info<CH, WIDE>(L.bytes, info, raw, cnt);
+                    t2 = tv.n_slots + (b0 << 8) + (unsigned)(seq & 0xFFu);
+                    split = true;
+                    seq >>= 8;
+                    cnt -= 1;
+                } else {
+                    t2 = 0;
+                }
             };
             // Refills are batched: idle lanes take new starts only once A_REFILL of them are idle
             // (or the remaining starts fit), so the refill code runs on a fraction of the steps.
@@ -680,16 +702,32 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                     }
                 }
                 if (!ballot(active)) break;
-                const int32_t t = nb + (int32_t)(seq & 0xFFu);
+                const int32_t t = t2 ? (int32_t)t2 : nb + (int32_t)(seq & 0xFFu);
                 const int2 ent = trie_slot(tv, t);   // buffer load: inactive lanes read harmlessly
                 bool done = false;
                 if (active) {
-                    seq >>= 8;
-                    cnt--;
-                    if (ent.y != node) {
+                    bool ok;
+                    int32_t nn;
+                    if (t2) {
+                        // root-table entry: .y = node after two bytes (0: none) | first byte exists
+                        // << 30 | first byte ends a token << 31; .x = that node's base word
+                        ok = (ent.y & 0x40000000) && (ent.y & 0x3FFFFFFF);
+                        nn = ent.y & 0x3FFFFFFF;
+                        if (split) {   // atom j ended after the first byte
+                            len = 1;
+                            if ((ent.y & 0x40000000) && ent.y < 0) mask = 1;
+                        }
+                        t2 = 0;
+                    } else {
+                        seq >>= 8;
+                        cnt--;
+                        ok = ent.y == node;
+                        nn = t;
+                    }
+                    if (!ok) {
                         done = true;
                     } else {
-                        node = t;
+                        node = nn;
                         nb = ent.x & BASE_MASK;
                         const bool leaf = (ent.x & LEAF_BIT) != 0;
                         if (cnt == 0) {   // atom j+len-1 ends: the span j..j+len is a candidate token
