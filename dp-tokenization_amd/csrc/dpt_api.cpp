@@ -70,11 +70,11 @@ struct DeviceGuard {
     int prev = -1;
     explicit DeviceGuard(int dev) {
         if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-        if (prev != dev) hipSetDevice(dev);
+        if (prev != dev) (void)hipSetDevice(dev);
     }
     ~DeviceGuard() {
         int cur = -1;
-        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) hipSetDevice(prev);
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
     }
 };
 
@@ -82,7 +82,7 @@ template <typename T>
 hipError_t grow(T **p, uint64_t *cap, uint64_t need) {
     if (need <= *cap && *p) return hipSuccess;
     uint64_t n = need < 1024 ? 1024 : need + need / 4;
-    if (*p) hipFree(*p);
+    if (*p) (void)hipFree(*p);
     *p = nullptr;
     *cap = 0;
     hipError_t e = hipMalloc((void **)p, n * sizeof(T));
@@ -109,7 +109,7 @@ int ensure_workspace(dpt_ctx *c, uint64_t n_bytes, uint64_t n_str) {
         c->cap_str = cap < cap2 ? cap : cap2;
         size_t tb = dpt::scan_temp_bytes(c->cap_str);
         if (tb > c->scan_bytes) {
-            if (c->scan_temp) hipFree(c->scan_temp);
+            if (c->scan_temp) (void)hipFree(c->scan_temp);
             c->scan_temp = nullptr;
             e = hipMalloc(&c->scan_temp, tb);
             if (e != hipSuccess) return hip_fail(e, "hipMalloc(scan)");
@@ -205,9 +205,9 @@ int dpt_vocab_create(const uint8_t *utf8_blob, const uint64_t *tok_off, const in
     if (e == hipSuccess) e = hipMemcpy(v->d_ids, da.id, sizeof(int32_t) * da.n_slots, hipMemcpyHostToDevice);
     if (e != hipSuccess) {
         dpt::free_double_array(&da);
-        if (v->d_slots) hipFree(v->d_slots);
-        if (v->d_ids) hipFree(v->d_ids);
-        if (v->d_slots4) hipFree(v->d_slots4);
+        if (v->d_slots) (void)hipFree(v->d_slots);
+        if (v->d_ids) (void)hipFree(v->d_ids);
+        if (v->d_slots4) (void)hipFree(v->d_slots4);
         delete v;
         return hip_fail(e, "vocab upload");
     }
@@ -226,9 +226,9 @@ int dpt_vocab_create(const uint8_t *utf8_blob, const uint64_t *tok_off, const in
 int dpt_vocab_destroy(dpt_vocab *v) {
     if (!v) return DPT_OK;
     DeviceGuard g(v->device);
-    hipFree(v->d_slots);
-    hipFree(v->d_ids);
-    hipFree(v->d_slots4);
+    (void)hipFree(v->d_slots);
+    (void)hipFree(v->d_ids);
+    (void)hipFree(v->d_slots4);
     delete v;
     return DPT_OK;
 }
@@ -261,8 +261,8 @@ int dpt_ctx_destroy(dpt_ctx *c) {
     void *ps[] = {c->staging, c->rec, c->counts, c->retry_list, c->retry_count, c->wsl_scratch, c->scan_temp, c->h_text, c->h_cut,
                   c->h_ids, c->h_off, c->h_idoff, c->h_status, c->h_capped, c->h_edges};
     for (void *p : ps)
-        if (p) hipFree(p);
-    for (hipEvent_t e : c->events) hipEventDestroy(e);
+        if (p) (void)hipFree(p);
+    for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
     delete c;
     return DPT_OK;
 }
@@ -460,7 +460,7 @@ int dpt_ctx_profile_read(dpt_ctx *c, double *ms, uint64_t *launches) {
             ms[s] += t;
         }
     }
-    for (hipEvent_t e : c->events) hipEventDestroy(e);
+    for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
     c->events.clear();
     if (launches) *launches = c->launches;
     c->launches = 0;

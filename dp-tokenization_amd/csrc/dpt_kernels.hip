@@ -1217,7 +1217,10 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     const bool wide = (p.mode & DPT_MODE_MASK) == DPT_MODE_ATOMS;   // atoms of up to 8 bytes
 
     hipLaunchKernelGGL(zero_first, dim3(1), dim3(64), 0, stream, p.id_off, p.retry_count);
-    if (ev) hipEventRecord(ev[0], stream);
+    if (ev) {
+        const hipError_t er = hipEventRecord(ev[0], stream);
+        if (er != hipSuccess) return er;
+    }
     if (p.n_str > 0) {
         if (p.variant == KERNEL_LANE) {
             uint64_t blocks = (p.n_str + 63) / 64;
@@ -1240,19 +1243,28 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
         if (wide) launch_tok<BIG_CH, 64, true, true>(b, tv, p.n_str, p.max_blocks / 64, stream);
         else launch_tok<BIG_CH, 64, true, false>(b, tv, p.n_str, p.max_blocks / 64, stream);
     }
-    if (ev) hipEventRecord(ev[1], stream);
+    if (ev) {
+        const hipError_t er = hipEventRecord(ev[1], stream);
+        if (er != hipSuccess) return er;
+    }
     if (p.n_str > 0) {
         size_t tb = p.scan_temp_bytes;
         hipError_t e = hipcub::DeviceScan::InclusiveSum(p.scan_temp, tb, p.counts, p.id_off + 1, (int)p.n_str, stream);
         if (e != hipSuccess) return e;
     }
-    if (ev) hipEventRecord(ev[2], stream);
+    if (ev) {
+        const hipError_t er = hipEventRecord(ev[2], stream);
+        if (er != hipSuccess) return er;
+    }
     if (p.n_str > 0) {
         uint64_t blocks = (p.n_str + 255) / 256;   // 4 waves x 64 strings
         if (blocks > 4096) blocks = 4096;
         hipLaunchKernelGGL(compact_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, p.staging, p.str_off, p.id_off, p.n_str, p.ids);
     }
-    if (ev) hipEventRecord(ev[3], stream);
+    if (ev) {
+        const hipError_t er = hipEventRecord(ev[3], stream);
+        if (er != hipSuccess) return er;
+    }
     return hipGetLastError();
 }
 
@@ -1262,7 +1274,8 @@ size_t wsl_scratch_bytes(unsigned max_blocks) {
 
 size_t scan_temp_bytes(uint64_t n_str) {
     size_t tb = 0;
-    hipcub::DeviceScan::InclusiveSum(nullptr, tb, (uint64_t *)nullptr, (uint64_t *)nullptr, (int)(n_str ? n_str : 1), (hipStream_t)0);
+    if (hipcub::DeviceScan::InclusiveSum(nullptr, tb, (uint64_t *)nullptr, (uint64_t *)nullptr, (int)(n_str ? n_str : 1), (hipStream_t)0) != hipSuccess)
+        return 0;
     return tb;
 }
 
