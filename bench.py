@@ -48,6 +48,9 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=2048, help="strings for the reference-port CPU baseline")
     ap.add_argument("--cpu-budget", type=float, default=25.0, help="seconds of CPU-baseline wall time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (RCCL, the real path) or gloo -- gloo lets a rehearsal put several ranks "
+                         "on one GPU (device = local_rank mod visible GPUs)")
     return ap.parse_args()
 
 
@@ -152,10 +155,13 @@ def main():
                "sample": f"{nd} of the first {args.cpu_sample} {args.workload} strings in {cdt:.1f}s "
                          f"(enumerate-then-select, oracle/ref_port.py; {nto} hit the 10s per-string limit)"}
 
-    ddist.init_from_env("nccl")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    vocab = Vocab(t2i, device=local)
+    gpu = local % max(1, torch.cuda.device_count())
+    if gpu != local and args.dist_backend == "nccl":
+        raise SystemExit(f"local rank {local} has no GPU of its own; use --dist-backend gloo to share one")
+    ddist.init_from_env(args.dist_backend, device=gpu)
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
+    vocab = Vocab(t2i, device=gpu)
     enc = Encoder(vocab)
     n_bytes = len(text)
     d_text = torch.from_numpy(text).to(dev)

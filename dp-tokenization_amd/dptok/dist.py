@@ -42,7 +42,7 @@ def allreduce_histogram(hist, group=None):
     return hist
 
 
-def init_from_env(backend: str = "nccl"):
+def init_from_env(backend: str = "nccl", device=None):
     """Initialise the default process group from torch.distributed.run's environment
     (MASTER_ADDR defaults to 127.0.0.1: container host names may not resolve)."""
     import torch
@@ -52,8 +52,9 @@ def init_from_env(backend: str = "nccl"):
         return rank, world, local
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     if backend == "nccl":
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dev = local if device is None else device
+        torch.cuda.set_device(dev)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
     else:
         dist.init_process_group(backend)
     return rank, world, local
