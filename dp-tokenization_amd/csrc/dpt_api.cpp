@@ -104,7 +104,8 @@ int ensure_workspace(dpt_ctx *c, uint64_t n_bytes, uint64_t n_str) {
         uint64_t cap = c->cap_str, cap2 = c->cap_str;
         e = grow(&c->counts, &cap, n_str);
         if (e != hipSuccess) return hip_fail(e, "hipMalloc(counts)");
-        e = grow(&c->retry_list, &cap2, n_str);
+        e = grow(&c->retry_list, &cap2, 2 * n_str);   // the 2048-byte pass's list, then the unbounded pass's
+        cap2 /= 2;
         if (e != hipSuccess) return hip_fail(e, "hipMalloc(retry_list)");
         c->cap_str = cap < cap2 ? cap : cap2;
         size_t tb = dpt::scan_temp_bytes(c->cap_str);
@@ -121,7 +122,7 @@ int ensure_workspace(dpt_ctx *c, uint64_t n_bytes, uint64_t n_str) {
         if (e != hipSuccess) return hip_fail(e, "hipMalloc(wsl_scratch)");
     }
     if (!c->retry_count) {
-        e = hipMalloc((void **)&c->retry_count, 16);
+        e = hipMalloc((void **)&c->retry_count, 32);
         if (e != hipSuccess) return hip_fail(e, "hipMalloc(retry_count)");
     }
     return DPT_OK;
@@ -307,6 +308,7 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
     p.retry_count = c->retry_count;
     p.wsl_scratch = c->wsl_scratch;
     p.long_span = v->stats.max_cp > 64 ? 1 : 0;
+    p.max_tok_bytes = v->stats.max_bytes;
     p.scan_temp = c->scan_temp;
     p.scan_temp_bytes = c->scan_bytes;
     p.max_blocks = c->max_blocks;

@@ -22,10 +22,11 @@ struct EncodeLaunch {
     // workspace
     int32_t *staging;
     uint64_t *counts;
-    uint32_t *retry_list;
-    uint32_t *retry_count;
+    uint32_t *retry_list;    // 2 x n_str: the 2048-byte pass's list, then (at + n_str) the unbounded pass's list
+    uint32_t *retry_count;   // 8 counters: retry count, pass-1 / pass-2 work, long count, long work
     uint8_t *wsl_scratch;    // max_blocks x wsl_scratch_bytes(1) bytes
-    int long_span;           // vocabulary tokens longer than 64 code points: words over 64 atoms -> status 3
+    int long_span;           // vocabulary tokens longer than 64 code points: words over 64 atoms -> unbounded pass
+    uint32_t max_tok_bytes;  // longest vocabulary token, bytes
     void *scan_temp;
     size_t scan_temp_bytes;
     unsigned max_blocks;
@@ -43,6 +44,31 @@ struct EncodeLaunch {
 constexpr int KERNEL_LANE = 0;    // lane per string, register ring of 16 walks (vocab max_cp <= 16)
 constexpr int KERNEL_ROWS16 = 1;  // 4 strings per wave in 16-lane DPP rows, LDS windows (max_cp <= 16)
 constexpr int KERNEL_ROWS64 = 2;  // 1 string per wave, 64-lane DPP (max_cp <= 64)
+
+// the unbounded pass (dpt_long.hip): strings the windowed kernels routed to the long list
+struct LongLaunch {
+    int mode;
+    const uint8_t *text;
+    const uint64_t *str_off;
+    const uint8_t *cut_mask;
+    int32_t *staging;
+    uint4 *rec;              // 16 bytes of scratch per input byte
+    uint64_t *counts;
+    int32_t *status;
+    int32_t *capped;
+    uint64_t *edges;
+    const uint32_t *list;
+    const uint32_t *list_count;
+    uint32_t *work_next;
+    const int2 *slots;
+    const int4 *slots4;
+    uint32_t n_slots;
+    int32_t root_base;
+    uint32_t max_tok_bytes;
+    int long_span;
+    unsigned blocks;
+};
+void launch_long(const LongLaunch &p, hipStream_t stream);
 
 hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t ev[6]);
 void launch_lane(const EncodeLaunch &p, unsigned blocks, hipStream_t stream);

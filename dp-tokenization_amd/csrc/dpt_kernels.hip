@@ -274,6 +274,8 @@ struct EncodeArgs {
     int32_t *capped;            // nullable
     uint32_t *retry_list;       // strings for the 2048-byte pass
     uint32_t *retry_count;
+    uint32_t *long_list;        // strings for the unbounded pass (dpt_long.hip)
+    uint32_t *long_count;
     const uint32_t *work_list;  // 2048-byte pass: the retry list
     const uint32_t *work_count;
     uint32_t *work_next;        // dynamic work distribution counter (zeroed per launch)
@@ -606,13 +608,15 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                     busy++;
                     continue;
                 }
-                // the string ends here: empty, or a word too long for this pass
+                // the string ends here: empty, or a word (or atom) too long for this pass -- the
+                // 2048-byte pass retries it, then the unbounded pass (status 3 is overwritten there)
                 if (status != 2) status = 3;
                 if (lane == 0) {
                     const uint64_t s = S.s;
-                    if (status == 3 && !BIG) {
-                        const unsigned slot = atomicAdd(a.retry_count, 1u);
-                        a.retry_list[slot] = (uint32_t)s;
+                    if (status == 3) {
+                        uint32_t *cnt = BIG ? a.long_count : a.retry_count;
+                        uint32_t *lst = BIG ? a.long_list : a.retry_list;
+                        lst[atomicAdd(cnt, 1u)] = (uint32_t)s;
                     }
                     a.status[s] = (int32_t)status;
                     a.counts[s] = 0;
@@ -1077,9 +1081,13 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
         // ---------------------------------------------------------- advance slots, finish strings
         if (lane < (unsigned)NG) {
             SlotState &S = SS[lane];
-            if (S.active && S.n_atoms > 0) {
+            if (S.active && S.n_atoms > 0 && S.status == 0 && (S.inval & 2)) {
+                // a word of more than G atoms while the vocabulary has longer tokens: the
+                // unbounded pass redoes the whole string (and writes its status and count)
+                a.long_list[atomicAdd(a.long_count, 1u)] = S.s;
+                S.active = 0;
+            } else if (S.active && S.n_atoms > 0) {
                 S.capsum += S.wtok;
-                if (S.status == 0 && (S.inval & 2)) S.status = 3;   // a word beyond the span limit
                 if (S.status == 0 && S.inval) S.status = 1;
                 if (S.status == 0 && !len_only) S.ntok += S.wtok;
                 S.pos += S.wlen;
@@ -1140,7 +1148,7 @@ __global__ void __launch_bounds__(256) compact_kernel(const int32_t *__restrict_
 }
 
 __global__ void zero_first(uint64_t *p, uint32_t *rc) {
-    if (threadIdx.x < 4) rc[threadIdx.x] = 0;   // retry count, pass-1 / pass-2 work counters
+    if (threadIdx.x < 8) rc[threadIdx.x] = 0;   // retry count, pass-1 / pass-2 work, long count, long work
     if (threadIdx.x == 0) p[0] = 0;
 }
 
@@ -1208,6 +1216,7 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     a.text = p.text; a.str_off = p.str_off; a.cut_mask = p.cut_mask; a.n_str = p.n_str;
     a.staging = p.staging; a.counts = p.counts; a.status = p.status; a.capped = p.capped;
     a.retry_list = p.retry_list; a.retry_count = p.retry_count; a.work_list = nullptr; a.work_count = nullptr;
+    a.long_list = p.retry_list + p.n_str; a.long_count = p.retry_count + 3;
     a.mode = p.mode;
     a.edges = p.edges;
     a.work_next = p.retry_count + 1;
@@ -1242,6 +1251,17 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
         b.work_next = p.retry_count + 2;
         if (wide) launch_tok<BIG_CH, 64, true, true>(b, tv, p.n_str, p.max_blocks / 64, stream);
         else launch_tok<BIG_CH, 64, true, false>(b, tv, p.n_str, p.max_blocks / 64, stream);
+        // the unbounded pass over whatever the windowed passes could not hold (usually nothing:
+        // its waves read a zero count and exit)
+        LongLaunch l;
+        l.mode = p.mode; l.text = p.text; l.str_off = p.str_off; l.cut_mask = p.cut_mask;
+        l.staging = p.staging; l.rec = p.rec; l.counts = p.counts; l.status = p.status; l.capped = p.capped;
+        l.edges = p.edges; l.list = a.long_list; l.list_count = a.long_count; l.work_next = p.retry_count + 4;
+        l.slots = p.slots; l.slots4 = p.slots4; l.n_slots = p.n_slots; l.root_base = p.root_base;
+        l.max_tok_bytes = p.max_tok_bytes; l.long_span = p.long_span;
+        const uint64_t lb = p.n_str < (uint64_t)(p.max_blocks / 16) ? p.n_str : (uint64_t)(p.max_blocks / 16);
+        l.blocks = (unsigned)(lb ? lb : 1);
+        launch_long(l, stream);
     }
     if (ev) {
         const hipError_t er = hipEventRecord(ev[1], stream);

@@ -70,7 +70,7 @@ def raise_for_status(status: int, text: str = "") -> None:
         # reference: segment_index_dp[-1] on an empty word (dp_tokenize.py:49)
         raise IndexError("list index out of range (empty word)")
     if status == _lib.STATUS_TOO_LONG:
-        raise DptError("a single word exceeds the engine window (2048 bytes)")
+        raise DptError("input outside the engine's limits (status 3)")
     raise DptError("engine internal error (status %d)" % status)
 
 

@@ -56,7 +56,7 @@ def _uncapped_min(atoms, vocabulary) -> float:
     vocab = {t for t in vocabulary if isinstance(t, str) and t}
     if not vocab:
         return float("inf")
-    status, length, _ = _dp_edges(atoms, vocab, uncapped=True)
+    status, length, _ = _dp_edges(atoms, vocab, uncapped=True, edges=False)
     if status not in (0, 1) or length >= _INF_WORD:
         return float("inf")
     return length

@@ -48,11 +48,11 @@ def _engine_for(vocabulary) -> Encoder:
     return enc
 
 
-def _dp_edges(atoms: Sequence[str], vocabulary, uncapped: bool = False):
-    """GPU DP over one atom list: (status, length, per-end reachable-predecessor masks)."""
+def _dp_edges(atoms: Sequence[str], vocabulary, uncapped: bool = False, edges: bool = True):
+    """GPU DP over one atom list: (status, length, per-end reachable-predecessor masks or None)."""
     enc = _engine_for(vocabulary)
     text, offs, cut = atoms_to_csr([atoms])
-    status, lengths, edges = enc.dp(text, offs, mode="atoms", cut_mask=cut, uncapped=uncapped, edges=True)
+    status, lengths, edges = enc.dp(text, offs, mode="atoms", cut_mask=cut, uncapped=uncapped, edges=edges)
     # edges are indexed by the byte offset of the string + atom end - 1; one string at offset 0
     return int(status[0]), int(lengths[0]), edges
 
@@ -69,7 +69,10 @@ def compute_shortest_tokenizations(base_representation_s, vocabulary, disregard_
     vocab = {t for t in vocabulary if t}
     status, length, edges = _dp_edges(atoms, vocab)
     if status == 3:
-        raise DptError("input longer than the engine's 2048-byte window")
+        # an optimal predecessor more than 64 atoms back (a token of > 64 code points): the
+        # 64-bit per-end edge masks of dpt_dp_host cannot list it
+        raise DptError("a shortest tokenization uses a token spanning more than 64 atoms; "
+                       "enumeration is limited to 64-atom tokens")
     if status not in (0, 1):
         raise DptError("engine status %d" % status)
     if status == 1:

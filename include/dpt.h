@@ -60,8 +60,10 @@ extern "C" {
 #define DPT_STATUS_OK 0
 #define DPT_STATUS_NO_TOKENIZATION 1 /* reference: ipdb.set_trace / ValueError (dp_tokenize.py:84) */
 #define DPT_STATUS_EMPTY_WORD 2      /* reference: IndexError (dp_tokenize.py:49) */
-#define DPT_STATUS_TOO_LONG 3        /* outside the engine's limits: a word > 2048 bytes, an atom > 8 bytes
-                                        (ATOMS) or a UTF-8 run > 4 bytes (RAW / PRESPLIT, malformed input) */
+#define DPT_STATUS_TOO_LONG 3        /* outside the engine's limits: dpt_encode never returns it (words, atoms
+                                        and tokens of any length are exact -- the windowed kernels hand what
+                                        they cannot hold to the unbounded pass); dpt_dp_host with edges returns
+                                        it when an optimal predecessor lies more than 64 atoms back */
 #define DPT_STATUS_INTERNAL 4        /* engine invariant violated (never expected) */
 
 typedef struct dpt_vocab dpt_vocab;
@@ -108,8 +110,9 @@ int dpt_ctx_reserve(dpt_ctx *c, uint64_t n_bytes, uint64_t n_str);
  * cut_mask (n_bytes bytes, PRESPLIT and ATOMS only): PRESPLIT: != 0 where a word starts (byte 0 of
  * every string always starts one); ATOMS: bit 1 where an atom starts, bit 0 where a word starts.
  * Limits: every string < 4 GiB, n_str < 2^31; RAW / PRESPLIT text is UTF-8 (code points are the
- * atoms); words longer than 2048 bytes get DPT_STATUS_TOO_LONG, and so do words of more than 64
- * atoms when the vocabulary has tokens longer than 64 code points (spans the engine does not walk).
+ * atoms).  No limit on word, atom or token length: words over 256 bytes take a 2048-byte window
+ * pass, longer words (and atoms over 8 bytes, or words over 64 atoms when the vocabulary has
+ * tokens over 64 code points) an unbounded one-wave-per-string pass (dpt_long.hip).
  * Stream-ordered on hip_stream (hipStream_t, NULL = default stream); no host synchronisation.
  */
 int dpt_encode(dpt_ctx *c, const dpt_vocab *v, int mode, const uint8_t *text, uint64_t n_bytes,

@@ -77,27 +77,52 @@ def test_s2orc_and_arabic_vs_oracle(engines, oracles):
 
 
 def test_long_words_big_window(engines, oracles):
-    """Words longer than the 256-byte window take the 2048-byte pass; > 2048 -> status 3."""
+    """Words longer than the 256-byte window take the 2048-byte pass; longer ones the unbounded
+    pass (dpt_long.hip).  Every length is exact -- the reference has no length limit."""
     rng = np.random.default_rng(5)
     texts = []
-    for L in (255, 256, 257, 300, 700, 1500, 2047, 2048, 2049, 3000):
+    for L in (255, 256, 257, 300, 700, 1500, 2047, 2048, 2049, 3000, 5000, 20000):
         w = "".join(chr(c) for c in rng.integers(0x21, 0x7F, size=L))
         texts.append(w)
         texts.append("ab cd " + w + " ef")
         texts.append(w + " " + w[: L // 2])
+        texts.append(("\n" + w[:L // 3] + " x\n").join([w[:100], w[100:]]))
     text, offs = _csr(texts)
-    ids, id_off, st, capped = engines["llama32k"].encode_csr(text, offs)
-    rids, roff, rst, rcap = oracles["llama32k"].encode_csr(text, offs)
-    for i, t in enumerate(texts):
-        longest = max(len(x.encode()) + (1 if k else 0) for k, x in enumerate(t.split(" ")))
-        if st[i] == 3:
-            # only a word longer than the 2048-byte window may be refused (DPT_STATUS_TOO_LONG)
-            assert longest > 2048, (i, len(t))
-            assert id_off[i + 1] == id_off[i]
-            continue
-        assert st[i] == rst[i], i
-        assert ids[int(id_off[i]):int(id_off[i + 1])].tolist() == rids[int(roff[i]):int(roff[i + 1])].tolist(), i
-        assert capped[i] == rcap[i]
+    got = engines["llama32k"].encode_csr(text, offs)
+    ref = oracles["llama32k"].encode_csr(text, offs)
+    _cmp_csr(got, ref)
+    assert np.array_equal(got[3], ref[3])
+    assert (got[2] == 0).sum() > 0
+
+
+def test_long_words_unicode_and_toy(engines, oracles):
+    """The unbounded pass on multi-byte code points and on a vocabulary where many atoms are
+    not tokens (capped DP, status 1), mixed with ordinary strings in one batch."""
+    rng = np.random.default_rng(15)
+    pool = ["é", "ß", "ع", "中", "😀", "\n", "\t", "▁"] + [chr(c) for c in range(0x21, 0x7F)] * 2
+    texts = []
+    for k in range(60):
+        L = int(rng.integers(1, 4000)) if k % 3 else int(rng.integers(2000, 9000))
+        texts.append("".join(rng.choice(pool, size=L)))
+        texts.append("".join(rng.choice(pool + [" "] * 20, size=200)))
+    text, offs = _csr(texts)
+    for name in ("llama32k", "toy1k"):
+        got = engines[name].encode_csr(text, offs)
+        ref = oracles[name].encode_csr(text, offs)
+        _cmp_csr(got, ref)
+        assert np.array_equal(got[3], ref[3])
+
+
+def test_long_pass_presplit(engines, oracles):
+    """PRESPLIT strings with words longer than 2048 bytes go through the unbounded pass."""
+    from oracle import oracle
+    rng = np.random.default_rng(16)
+    texts = ["".join(chr(c) for c in rng.integers(0x21, 0x7F, size=int(rng.integers(100, 6000)))) for _ in range(40)]
+    text, offs = _csr(texts)
+    cut = (rng.random(len(text)) < 0.0004).astype(np.uint8)
+    got = engines["llama32k"].encode_csr(text, offs, mode="presplit", cut_mask=cut)
+    ref = oracles["llama32k"].encode_csr(text, offs, mode=oracle.PRESPLIT, cut_mask=cut)
+    _cmp_csr(got, ref)
 
 
 def test_empty_batch_and_empty_strings(engines):
@@ -188,36 +213,92 @@ def test_mixed_unicode_vs_oracle(engines, oracles):
         _cmp_csr(engines[name].encode_csr(text, offs), oracles[name].encode_csr(text, offs))
 
 
-def test_atoms_mode_limits():
-    """ATOMS mode: atoms of up to 8 bytes are walked exactly; a longer atom makes the string
-    status 3 (DptError through the compat layer) instead of a wrong answer."""
+def test_atoms_mode_long_atoms():
+    """ATOMS mode: atoms of up to 8 bytes are walked by the windowed kernels; a longer atom sends
+    the string to the unbounded pass, which walks atoms of any length."""
     from dptok import Encoder, Vocab
-    t2i = {"abcdefgh": 0, "ab": 1, "cdefgh": 2, "x": 3, "abcdefghi": 4, "i": 5}
+    t2i = {"abcdefgh": 0, "ab": 1, "cdefgh": 2, "x": 3, "abcdefghi": 4, "i": 5, "abcdefghijklmnopqrstu": 6, "v": 7}
     enc = Encoder(Vocab(t2i, 0))
-    (ids, st), (ids2, st2), (ids3, st3) = enc.encode_word_atoms([[["abcdefgh", "x"]], [["ab", "cdefgh"]],
-                                                                  [["abcdefghi"]]])
-    assert (ids, st) == ([0, 3], 0)
-    assert st2 == 0 and ids2 == [0]          # 'ab'+'cdefgh' = one token 'abcdefgh'
-    assert st3 == 3 and ids3 == []
+    res = enc.encode_word_atoms([[["abcdefgh", "x"]], [["ab", "cdefgh"]], [["abcdefghi"]],
+                                 [["abcdefghi", "x"], ["x"]], [["abcdefghijklmnopqrstu", "v"]], [["abcdefghij"]]])
+    assert res[0] == ([0, 3], 0)
+    assert res[1] == ([0], 0)          # 'ab'+'cdefgh' = one token 'abcdefgh'
+    assert res[2] == ([4], 0)
+    assert res[3] == ([4, 3, 3], 0)
+    assert res[4] == ([6, 7], 0)
+    assert res[5] == ([], 1)           # one atom that is not a token: no complete tokenization
 
 
 def test_tokens_longer_than_64_code_points():
-    """A vocabulary with tokens of 65..80 code points is accepted: words of up to 64 atoms are
-    exact; longer words (where such a token could match) get status 3 instead of a wrong answer."""
+    """A vocabulary with tokens of 65..300 code points: words of up to 64 atoms run in the windowed
+    kernels, longer words in the unbounded pass; all exact against the oracle."""
     from dptok import Encoder, Vocab, synth
     from oracle import oracle
     t2i = dict(synth.llama_shaped_vocab())
     rng = np.random.default_rng(4)
-    for L in (65, 70, 80):
+    long_toks = []
+    for L in (65, 70, 80, 150, 300):
         for _ in range(10):
-            t2i.setdefault("".join(chr(c) for c in rng.integers(0x61, 0x64, size=L)), len(t2i))
+            tok = "".join(chr(c) for c in rng.integers(0x61, 0x64, size=L))
+            long_toks.append(tok)
+            t2i.setdefault(tok, len(t2i))
     v = Vocab(t2i, 0)
-    assert v.stats["max_cp"] >= 80
+    assert v.stats["max_cp"] >= 300
     short = ["".join(chr(c) for c in rng.integers(0x61, 0x64, size=rng.integers(1, 64))) for _ in range(2000)]
     short += [" ".join(short[k:k + 3]) for k in range(0, 300, 3)]
     text, offs = _csr(short)
     _cmp_csr(Encoder(v).encode_csr(text, offs), oracle.OracleVocab(t2i).encode_csr(text, offs))
-    long_ = ["x" + "".join(chr(c) for c in rng.integers(0x61, 0x64, size=rng.integers(65, 120))) for _ in range(50)]
+    long_ = ["x" + "".join(chr(c) for c in rng.integers(0x61, 0x64, size=rng.integers(65, 400))) for _ in range(200)]
+    # words that contain the long tokens verbatim, so the > 64-atom spans are taken
+    for k in range(100):
+        a, b = long_toks[k % len(long_toks)], long_toks[(7 * k + 3) % len(long_toks)]
+        long_.append("x" + a + "ab" + b[: (k * 13) % len(b)] + " " + b)
     text, offs = _csr(long_)
-    _, _, st, cap = Encoder(v).encode_csr(text, offs)
-    assert (st == 3).all() and (cap == -1).all()
+    got = Encoder(v).encode_csr(text, offs)
+    ref = oracle.OracleVocab(t2i).encode_csr(text, offs)
+    _cmp_csr(got, ref)
+    assert np.array_equal(got[3], ref[3])
+    assert (got[2] == 0).sum() >= 100
+
+
+def _min_tokens_bounded(atoms, vocab, max_cp, capped=False):
+    """oracle/ref_port.min_tokens_for_string (inspect_tokenizer.py:77-86), or with ``capped`` the
+    len_dp[-1] of ref_port.forward_dp (dp_tokenize.py:28), with spans bounded by the longest token
+    (a span of L atoms has >= L code points, so longer spans are never tokens)."""
+    n = len(atoms)
+    best = list(range(n + 1)) if capped else [float("inf")] * (n + 1)
+    best[0] = 0
+    for i in range(1, n + 1):
+        for j in range(max(0, i - max_cp), i):
+            if best[j] + 1 < best[i] and "".join(atoms[j:i]) in vocab:
+                best[i] = best[j] + 1
+    return best[n]
+
+
+def test_long_pass_dp_lengths(vocabs):
+    """dpt_dp_host (len-only capped and uncapped) on atom lists of up to 5000 atoms: the uncapped
+    minimum matches the reference's min_tokens_for_string restatement, the capped length matches
+    the C oracle's capped sums through PRESPLIT."""
+    from dptok import Encoder, Vocab
+    from dptok.engine import atoms_to_csr
+    from oracle import ref_port
+    t2i = vocabs["toy1k"]
+    vocab = set(t2i)
+    enc = Encoder(Vocab(t2i, 0))
+    max_cp = max(len(t) for t in vocab)
+    rng = np.random.default_rng(17)
+    letters = sorted({c for t in vocab for c in t})
+    words = [list(rng.choice(letters, size=int(rng.integers(1, 60)))) for _ in range(200)]
+    words += [list(rng.choice(letters, size=int(rng.integers(2000, 5000)))) for _ in range(12)]
+    for w in words[:40]:
+        assert _min_tokens_bounded(w, vocab, max_cp) == ref_port.min_tokens_for_string(w, vocab)
+    text, offs, cut = atoms_to_csr(words)
+    st, lens, _ = enc.dp(text, offs, mode="atoms", cut_mask=cut, uncapped=True)
+    for k, w in enumerate(words):
+        want = _min_tokens_bounded(w, vocab, max_cp)
+        assert int(lens[k]) == (65535 if want == float("inf") else want), k
+    for w in words[:40]:
+        assert _min_tokens_bounded(w, vocab, max_cp, capped=True) == ref_port.forward_dp(w, vocab)[0][-1]
+    st, lens, _ = enc.dp(text, offs, mode="atoms", cut_mask=cut)
+    for k, w in enumerate(words):
+        assert int(lens[k]) == _min_tokens_bounded(w, vocab, max_cp, capped=True), k
