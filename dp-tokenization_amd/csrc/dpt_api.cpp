@@ -293,6 +293,8 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
     hipStream_t st = (hipStream_t)hip_stream;
     dpt::EncodeLaunch p;
     p.mode = mode_flags;
+    if (const char *e = getenv("DPT_B"))   // A/B diagnostic only
+        if (e[0] == 'r') p.mode |= dpt::DPT_FLAG_OLD_B;
     p.edges = edges;
     p.text = text;
     p.str_off = str_off;

@@ -40,6 +40,10 @@ struct EncodeLaunch {
     int32_t root_base;
 };
 
+// internal mode bit (never in the public API): A/B diagnostic, DPT_B=rows selects the 16-lane
+// row recurrence for capless windows instead of the lane-chunk one (dpt_api.cpp)
+constexpr int DPT_FLAG_OLD_B = 0x40000000;
+
 // kernel variants for the first pass (the 2048-byte window pass always follows for retries)
 constexpr int KERNEL_LANE = 0;    // lane per string, register ring of 16 walks (vocab max_cp <= 16)
 constexpr int KERNEL_ROWS16 = 1;  // 4 strings per wave in 16-lane DPP rows, LDS windows (max_cp <= 16)

@@ -129,7 +129,9 @@ template <int G> struct Group;
 // valid word's selected path (Appendix A: a reachable i has a reachable j attaining its key),
 // and C1 walks valid words only, so no "none" code is stored.
 template <> struct Group<16> {
-    using M = uint16_t;  // span mask: bit L-1 = an L-atom token starts here
+    using M = uint16_t;
+    // smask: until phase B, the inverted END mask of end position i: bit d clear = atoms
+    // i-1-d .. i-1 are a token (phase A clears the bits with LDS atomics)
     struct Rec { uint16_t cpos; uint16_t smask; };
     struct Fin { uint8_t v; };   // dg | de << 4
     static __device__ __forceinline__ unsigned dg(const Fin &x) { return x.v & 15u; }
@@ -480,7 +482,10 @@ __device__ bool prep_window(GroupLDS<CH, G> &L, uint8_t *gw, const WinRegs<CH> &
             const unsigned k = c0 + lane * 4 + u;
             if (ast[u]) {
                 L.aoff[ai] = (typename GroupLDS<CH, G>::Idx)k;
-                L.rec[ai].cpos = (uint16_t)(cp | (wst[u] ? CP_WS : 0));
+                if constexpr (G == 16)   // end masks start all-dead (inverted); phase A clears token bits
+                    reinterpret_cast<uint32_t *>(L.rec)[ai] = 0xFFFF0000u | cp | (wst[u] ? CP_WS : 0u);
+                else
+                    L.rec[ai].cpos = (uint16_t)(cp | (wst[u] ? CP_WS : 0));
                 if (wst[u]) { L.set_word_start(gw, wi, ai); wi++; }
                 ai++;
             }
@@ -492,7 +497,8 @@ __device__ bool prep_window(GroupLDS<CH, G> &L, uint8_t *gw, const WinRegs<CH> &
     }
     if (lane == 0) {
         L.aoff[n_atoms] = (typename GroupLDS<CH, G>::Idx)wlen;
-        L.rec[n_atoms].cpos = (uint16_t)(cp_tot | CP_WS);
+        if constexpr (G == 16) reinterpret_cast<uint32_t *>(L.rec)[n_atoms] = 0xFFFF0000u | cp_tot | CP_WS;
+        else L.rec[n_atoms].cpos = (uint16_t)(cp_tot | CP_WS);
         L.set_word_start(gw, n_words, n_atoms);
     }
     n_atoms_o = n_atoms;
@@ -655,7 +661,13 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
             bool split = false;
             int32_t nb = tv.root_base, node = 0;
             uint64_t seq = 0;
-            M mask = 0;
+            M mask = 0;   // G = 16: bit 0 only (the single-atom span is a token)
+            // G = 16: the span of len atoms ending at end position e is a token: clear bit len-1
+            // of e's inverted end mask (the high half of rec[e]; one LDS atomic, no return)
+            auto end_token = [&](unsigned e, unsigned ln) {
+                uint32_t *r32 = reinterpret_cast<uint32_t *>(smem + lbase);
+                __hip_atomic_fetch_and(&r32[e], ~(1u << (15u + ln)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            };
             auto start = [&](unsigned uu) {
                 unsigned gs = 0;
 #pragma unroll
@@ -719,7 +731,10 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                         nn = ent.y & 0x3FFFFFFF;
                         if (split) {   // atom j ended after the first byte
                             len = 1;
-                            if ((ent.y & 0x40000000) && ent.y < 0) mask = 1;
+                            if ((ent.y & 0x40000000) && ent.y < 0) {
+                                mask = 1;
+                                if constexpr (G == 16) end_token(j + 1, 1);
+                            }
                         }
                         t2 = 0;
                     } else {
@@ -736,7 +751,10 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                         const bool leaf = (ent.x & LEAF_BIT) != 0;
                         if (cnt == 0) {   // atom j+len-1 ends: the span j..j+len is a candidate token
                             len++;
-                            if (ent.x & TERM_BIT) mask |= (M)1 << (len - 1);
+                            if (ent.x & TERM_BIT) {
+                                if constexpr (G == 16) { if (len == 1) mask = 1u; end_token(j + len, len); }
+                                else mask |= (M)1 << (len - 1);
+                            }
                             if (leaf || (info & AInfo<CH>::STOP) || len == (unsigned)G) {
                                 done = true;
                             } else {
@@ -751,7 +769,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 }
                 if (done) {
                     GL &L = *reinterpret_cast<GL *>(smem + lbase);
-                    L.rec[j].smask = G == 16 ? (M)~mask : mask;   // B (G = 16) reads it inverted
+                    if constexpr (G != 16) L.rec[j].smask = mask;   // G = 16: end masks, set by end_token
                     if (!(mask & 1u)) SS[lbase / (unsigned)group_lds_bytes<CH, G>()].capb = 1;
                     active = false;
                 }
@@ -786,10 +804,10 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 unsigned st = d == 0 ? ST0 : 0u;
                 unsigned cpj = 0;
                 if constexpr (G == 16) {
-                    // Lane d carries x = rec[j] = {cpos[j], ~smask[j]} (one DPP shift moves both) and
-                    // its state in key form: (cost[j]+1) << 16 | invalid[j] << 15 | (0x7FFF - G[j]),
-                    // so the candidate key is min(st, (st | 0x7FFF) - span) and a dead span is one
-                    // sign-extended bit of x.
+                    // Lane d carries x = rec[j] (its cpos) and its state in key form:
+                    // (cost[j]+1) << 16 | invalid[j] << 15 | (0x7FFF - G[j]), so the candidate key is
+                    // min(st, (st | 0x7FFF) - span); a dead span is one sign-extended bit of the
+                    // inverted end mask of i (read by every lane of the row).
                     constexpr unsigned SK0 = 0x17FFFu;   // word start in key form
                     const uint32_t *rec32 = reinterpret_cast<const uint32_t *>(L.rec);
                     const unsigned sbit = 16u + d;
@@ -805,7 +823,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                         const unsigned span = (cur - xI) & 0x7FFFu;  // cp(j..i); borrows only move up
                         unsigned kv = (skI | 0x7FFFu) - span;
                         kv = skI < kv ? skI : kv;
-                        const unsigned key = kv | (unsigned)__builtin_amdgcn_sbfe((int)xI, sbit, 1);
+                        const unsigned key = kv | (unsigned)__builtin_amdgcn_sbfe((int)cur, sbit, 1);
                         unsigned r = row_min_u32(key);
                         if constexpr (capm == 0) {
                             const unsigned capkey = ((i << 16) | 0xFFFFu) - wsh;
@@ -877,6 +895,128 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                     }
                 }
             };
+            // Capless windows without edge recording (the common case, G = 16): lanes take
+            // chunks of end positions cut at "cut points" -- boundaries no token span crosses,
+            // through which every tokenization of the word passes -- and run the recurrence
+            // sequentially over their own chunk, one position per iteration for 64 lanes.
+            // A chunk that starts inside a word starts from a local state (cost 0, G 0); a row
+            // scan of the chunks' transfers gives each chunk its incoming state, and a fix-up
+            // corrects the two things that depend on it: the final key of the word that ends
+            // first in the chunk (cost offset, max with the incoming G) and dg at the positions
+            // before that word end (dg = de wherever the incoming G already attains G[i]:
+            // every j in E(i) then ties on max(G[j], cp(span))).  de and E(i) are local.
+            auto forward_lanes = [&]() {
+              if constexpr (G == 16) {
+                uint32_t *rec32 = reinterpret_cast<uint32_t *>(L.rec);
+                constexpr unsigned FRESH = 31u;   // key16 of a fresh start: cost 0, reachable, G 0
+                // key16 = cost << 6 | invalid << 5 | 31 - G (the Wfin<16> form)
+                auto relax = [](unsigned sj, unsigned span) {   // cost + 1, G = max(G, cp(span)); span <= 16
+                    const unsigned a1 = sj + 64u;
+                    const unsigned a2 = (a1 | 31u) - span;
+                    return a1 < a2 ? a1 : a2;
+                };
+                // ---- cut points: boundary p is one iff min_{i > p} lo_i >= p, lo_i = the first atom
+                //      of the longest token ending at i (i-1 - highest bit of its end mask)
+                const unsigned C = (na + 15u) >> 4;   // boundaries per lane (na <= 256)
+                const unsigned c0 = min(d * C, na), c1 = min(c0 + C, na);
+                unsigned lo[16];
+                unsigned cmin = 0xFFFFu;
+#pragma unroll
+                for (int k = 0; k < 16; k++) {
+                    const unsigned i = c0 + 1u + (unsigned)k;
+                    unsigned v = 0xFFFFu;
+                    if (i <= c1) {
+                        const unsigned em = (~rec32[i] >> 16) | 1u;   // bit 0 is set in a capless window
+                        v = i - 1u - (31u - (unsigned)__builtin_clz(em));
+                    }
+                    lo[k] = v;
+                    cmin = min(cmin, v);
+                }
+                // suffix min over the later lanes of the row (row_shl: lane l reads lane l+k)
+                unsigned sm = cmin;
+                sm = min(sm, (unsigned)__builtin_amdgcn_update_dpp((int)0xFFFFu, (int)sm, 0x101, 0xF, 0xF, false));
+                sm = min(sm, (unsigned)__builtin_amdgcn_update_dpp((int)0xFFFFu, (int)sm, 0x102, 0xF, 0xF, false));
+                sm = min(sm, (unsigned)__builtin_amdgcn_update_dpp((int)0xFFFFu, (int)sm, 0x104, 0xF, 0xF, false));
+                sm = min(sm, (unsigned)__builtin_amdgcn_update_dpp((int)0xFFFFu, (int)sm, 0x108, 0xF, 0xF, false));
+                unsigned mm = (unsigned)__builtin_amdgcn_update_dpp((int)0xFFFFu, (int)sm, 0x101, 0xF, 0xF, false);
+                unsigned cut = 0;
+#pragma unroll
+                for (int k = 15; k >= 0; k--) {
+                    mm = min(mm, lo[k]);
+                    const unsigned p = c0 + (unsigned)k;
+                    if (p < c1 && mm >= p) cut |= 1u << k;
+                }
+                // rs = the first cut at or after c0 (in this lane's chunk or a later one; na is a cut)
+                unsigned rs = cut ? c0 + ffbl(cut) : na;
+                rs = min(rs, (unsigned)__builtin_amdgcn_update_dpp((int)na, (int)rs, 0x101, 0xF, 0xF, false));
+                rs = min(rs, (unsigned)__builtin_amdgcn_update_dpp((int)na, (int)rs, 0x102, 0xF, 0xF, false));
+                rs = min(rs, (unsigned)__builtin_amdgcn_update_dpp((int)na, (int)rs, 0x104, 0xF, 0xF, false));
+                rs = min(rs, (unsigned)__builtin_amdgcn_update_dpp((int)na, (int)rs, 0x108, 0xF, 0xF, false));
+                const unsigned re = (unsigned)__builtin_amdgcn_update_dpp((int)na, (int)rs, 0x101, 0xF, 0xF, false);
+
+                // ---- the recurrence over ends (rs, re], one position per iteration
+                unsigned i = rs, ws = rs, sprev = FRESH, pe = 0;
+                unsigned cprev = rec32[rs] & 0x7FFFu;
+                unsigned nxt = rec32[rs + 1u];   // rs + 1 <= na + 1 < NA
+                while (ballot(i < re)) {
+                    if (i < re) {
+                        i++;
+                        const unsigned r = nxt;
+                        nxt = rec32[i + 1u];
+                        const unsigned cpi = r & 0x7FFFu;
+                        unsigned best = relax(sprev, cpi - cprev);   // j = i-1: the single atom
+                        unsigned dg = 0, de = 0;
+                        unsigned m = (~r >> 17) & 0x7FFFu;          // longer tokens ending at i: bit d-1
+                        while (m) {
+                            const unsigned dd = ffbl(m) + 1u;
+                            m &= m - 1u;
+                            const unsigned j = i - 1u - dd;          // j >= ws: spans cross no cut
+                            const unsigned rj = rec32[j];
+                            const unsigned sj = j == ws ? FRESH : (rj >> 16);
+                            const unsigned kk = relax(sj, cpi - (rj & 0x7FFFu));
+                            // ascending d = descending j: the first strict improvement is the largest j
+                            if ((kk >> 5) < (best >> 5)) de = dd;
+                            if (kk < best) dg = dd;
+                            best = kk < best ? kk : best;
+                        }
+                        L.rec[i].smask = (uint16_t)best;   // this end's mask was read above
+                        L.fin[i].v = (uint8_t)(dg | (de << 4));
+                        const bool wend = (r & CP_WS) != 0;
+                        if (wend && !pe) pe = i;
+                        ws = wend ? i : ws;
+                        sprev = wend ? FRESH : best;
+                        cprev = cpi;
+                    }
+                }
+                // ---- row scan of the chunk transfers: (reset, value) -- a chunk with a word start
+                //      ignores its input; otherwise out = in (+) local, (+) = costs add, G max
+                unsigned x = (pe ? 0x10000u : 0u) | sprev;
+                auto compose = [&](unsigned y) {   // y (the earlier lanes) then x
+                    const unsigned comb = (y & 0xFFC0u) + (x & 0xFFC0u) + min(y & 31u, x & 31u);
+                    x = (x >> 16) ? x : ((y & 0x10000u) | comb);
+                };
+                compose((unsigned)__builtin_amdgcn_update_dpp((int)FRESH, (int)x, 0x111, 0xF, 0xF, false));   // row_shr:1
+                compose((unsigned)__builtin_amdgcn_update_dpp((int)FRESH, (int)x, 0x112, 0xF, 0xF, false));   // row_shr:2
+                compose((unsigned)__builtin_amdgcn_update_dpp((int)FRESH, (int)x, 0x114, 0xF, 0xF, false));   // row_shr:4
+                compose((unsigned)__builtin_amdgcn_update_dpp((int)FRESH, (int)x, 0x118, 0xF, 0xF, false));   // row_shr:8
+                const unsigned in = (unsigned)__builtin_amdgcn_update_dpp((int)FRESH, (int)x, 0x111, 0xF, 0xF, false) & 0xFFFFu;
+                const unsigned gin = 31u - (in & 31u);   // G at rs
+                if (gin) {
+                    const unsigned lim = pe ? pe : re;
+                    for (unsigned q = rs + 1u; q <= lim; q++) {
+                        const unsigned kl = L.rec[q].smask;
+                        if (gin >= 31u - (kl & 31u)) {
+                            const unsigned f = L.fin[q].v;
+                            L.fin[q].v = (uint8_t)((f & 0xF0u) | (f >> 4));
+                        }
+                    }
+                    if (pe) {
+                        const unsigned kl = L.rec[pe].smask;
+                        L.rec[pe].smask = (uint16_t)((in & 0xFFC0u) + (kl & 0xFFC0u) + min(in & 31u, kl & 31u));
+                    }
+                }
+              }
+            };
             using T_ = std::true_type;
             using F_ = std::false_type;
             using C0_ = std::integral_constant<int, 0>;
@@ -888,7 +1028,14 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
             if (a.edges) {
                 if (!capb) forward(T_{}, C2_{}); else if (uncapped) forward(T_{}, C1_{}); else forward(T_{}, C0_{});
             } else {
-                if (!capb) forward(F_{}, C2_{}); else if (uncapped) forward(F_{}, C1_{}); else forward(F_{}, C0_{});
+                if (!capb) {
+                    if constexpr (G == 16) {
+                        if (a.mode & dpt::DPT_FLAG_OLD_B) forward(F_{}, C2_{});
+                        else forward_lanes();
+                    } else {
+                        forward(F_{}, C2_{});
+                    }
+                } else if (uncapped) forward(F_{}, C1_{}); else forward(F_{}, C0_{});
             }
         }
         wave_sync();
