@@ -527,8 +527,9 @@ __device__ bool prep_window(GroupLDS<CH, G> &L, uint8_t *gw, const WinRegs<CH> &
 #define DPT_DOUBLE 0
 #endif
 
+// 256-byte 16-lane rows: 6 waves per SIMD by VGPRs (<= 80), so LDS (22 waves per CU) binds
 template <int CH, int G, bool BIG, bool WIDE>
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CH == 256 && G == 16) ? 6 : 1)))
 tokenize_kernel(EncodeArgs a, TrieView tv) {
     constexpr int NG = 64 / G;
     using GL = GroupLDS<CH, G>;
@@ -919,33 +920,28 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 //      of the longest token ending at i (i-1 - highest bit of its end mask)
                 const unsigned C = (na + 15u) >> 4;   // boundaries per lane (na <= 256)
                 const unsigned c0 = min(d * C, na), c1 = min(c0 + C, na);
-                unsigned lo[16];
-                unsigned cmin = 0xFFFFu;
-#pragma unroll
-                for (int k = 0; k < 16; k++) {
+                // one backward pass over the chunk's ends (c0, c1]: the local suffix min of lo
+                // decides the cuts as far as this chunk's ends go; the later chunks' ends (min S)
+                // then only cap them: p is a cut iff both mins are >= p, i.e. p <= S
+                unsigned mloc = 0xFFFFu, lcut = 0;
+#pragma unroll 4
+                for (int k = 15; k >= 0; k--) {
                     const unsigned i = c0 + 1u + (unsigned)k;
-                    unsigned v = 0xFFFFu;
                     if (i <= c1) {
-                        const unsigned em = (~rec32[i] >> 16) | 1u;   // bit 0 is set in a capless window
-                        v = i - 1u - (31u - (unsigned)__builtin_clz(em));
+                        const unsigned hb = 31u - (unsigned)__builtin_clz((~rec32[i] >> 16) | 1u);   // bit 0 is set in a capless window
+                        mloc = min(mloc, i - 1u - hb);
+                        if (mloc >= i - 1u) lcut |= 1u << k;   // boundary p = i-1 = c0+k < c1
                     }
-                    lo[k] = v;
-                    cmin = min(cmin, v);
                 }
-                // suffix min over the later lanes of the row (row_shl: lane l reads lane l+k)
-                unsigned sm = cmin;
+                // min lo over the later lanes of the row (row_shl: lane l reads lane l+k)
+                unsigned sm = mloc;
                 sm = min(sm, (unsigned)__builtin_amdgcn_update_dpp((int)0xFFFFu, (int)sm, 0x101, 0xF, 0xF, false));
                 sm = min(sm, (unsigned)__builtin_amdgcn_update_dpp((int)0xFFFFu, (int)sm, 0x102, 0xF, 0xF, false));
                 sm = min(sm, (unsigned)__builtin_amdgcn_update_dpp((int)0xFFFFu, (int)sm, 0x104, 0xF, 0xF, false));
                 sm = min(sm, (unsigned)__builtin_amdgcn_update_dpp((int)0xFFFFu, (int)sm, 0x108, 0xF, 0xF, false));
-                unsigned mm = (unsigned)__builtin_amdgcn_update_dpp((int)0xFFFFu, (int)sm, 0x101, 0xF, 0xF, false);
-                unsigned cut = 0;
-#pragma unroll
-                for (int k = 15; k >= 0; k--) {
-                    mm = min(mm, lo[k]);
-                    const unsigned p = c0 + (unsigned)k;
-                    if (p < c1 && mm >= p) cut |= 1u << k;
-                }
+                const unsigned S = (unsigned)__builtin_amdgcn_update_dpp((int)0xFFFFu, (int)sm, 0x101, 0xF, 0xF, false);
+                // boundaries c0 + k <= S
+                const unsigned cut = S < c0 ? 0u : (S - c0 >= 15u ? lcut : lcut & ((2u << (S - c0)) - 1u));
                 // rs = the first cut at or after c0 (in this lane's chunk or a later one; na is a cut)
                 unsigned rs = cut ? c0 + ffbl(cut) : na;
                 rs = min(rs, (unsigned)__builtin_amdgcn_update_dpp((int)na, (int)rs, 0x101, 0xF, 0xF, false));
