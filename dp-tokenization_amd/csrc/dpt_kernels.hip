@@ -287,6 +287,10 @@ struct EncodeArgs {
     int mode;                   // DPT_MODE_* | DPT_FLAG_*
 };
 
+#ifdef DPT_LANEDBG
+// diagnostic build only: lane-mode chunk values of string 0's first window
+__device__ unsigned g_lanedbg[16 * 16 + 4];
+#endif
 #ifdef DPT_STAMPS
 // diagnostic build only: cycles per phase summed over waves (never in the product build)
 __device__ unsigned long long g_stamps[8];
@@ -635,7 +639,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
             wave_sync();
             if (!refill || exhausted) break;
         }
-        if (lane < (unsigned)NG && !((prepared >> lane) & 1u)) { SS[lane].n_atoms = 0; SS[lane].n_words = 0; }
+        if (lane < (unsigned)NG && !((prepared >> lane) & 1u)) { SS[lane].n_atoms = 0; SS[lane].n_words = 0; SS[lane].capb = 0; }
         wave_sync();
         if (busy == 0) break;
         STAMP(0);
@@ -783,6 +787,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
         STAMP(1);
 
         // ---------------------------------------------------------- B: forward recurrence
+        bool lane_mode = false;   // B ran per chunk and did C0 and C1 itself (G = 16, capless, no edges)
         {
             GL &L = grp(mg);
             const unsigned na = SS[mg].n_atoms;
@@ -952,14 +957,15 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
 
                 // ---- the recurrence over ends (rs, re], one position per iteration
                 unsigned i = rs, ws = rs, sprev = FRESH, pe = 0;
-                unsigned cprev = rec32[rs] & 0x7FFFu;
+                unsigned cprev = rec32[rs] & 0x7FFu;
                 unsigned nxt = rec32[rs + 1u];   // rs + 1 <= na + 1 < NA
+                unsigned T = 0;                  // tokens of the chunk: the pieces' costs
                 while (ballot(i < re)) {
                     if (i < re) {
                         i++;
                         const unsigned r = nxt;
                         nxt = rec32[i + 1u];
-                        const unsigned cpi = r & 0x7FFFu;
+                        const unsigned cpi = r & 0x7FFu;             // bits 11..14: see below
                         unsigned best = relax(sprev, cpi - cprev);   // j = i-1: the single atom
                         unsigned dg = 0, de = 0;
                         unsigned m = (~r >> 17) & 0x7FFFu;          // longer tokens ending at i: bit d-1
@@ -969,7 +975,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                             const unsigned j = i - 1u - dd;          // j >= ws: spans cross no cut
                             const unsigned rj = rec32[j];
                             const unsigned sj = j == ws ? FRESH : (rj >> 16);
-                            const unsigned kk = relax(sj, cpi - (rj & 0x7FFFu));
+                            const unsigned kk = relax(sj, cpi - (rj & 0x7FFu));
                             // ascending d = descending j: the first strict improvement is the largest j
                             if ((kk >> 5) < (best >> 5)) de = dd;
                             if (kk < best) dg = dd;
@@ -978,12 +984,25 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                         L.rec[i].smask = (uint16_t)best;   // this end's mask was read above
                         L.fin[i].v = (uint8_t)(dg | (de << 4));
                         const bool wend = (r & CP_WS) != 0;
-                        if (wend && !pe) pe = i;
+                        if (wend) {
+                            // the word ending at i: its G (the longest token to select, L*) - 1 goes
+                            // into bits 11..14 of rec[i].cpos (code-point prefixes are < 2048 in a
+                            // 256-byte window), where C1 finds it (the mask halves take its tokens)
+                            L.rec[i].cpos = (uint16_t)((r & 0x87FFu) | ((30u - (best & 31u)) << 11));
+                            T += best >> 6;
+                            if (!pe) pe = i;
+                        }
                         ws = wend ? i : ws;
                         sprev = wend ? FRESH : best;
                         cprev = cpi;
                     }
                 }
+                // P1 = the piece walked first in C1 (the one ending at re); p1in: no word start in
+                // (rs, re), so P1 is the chunk's first piece too and starts from the incoming state
+                const bool re_ws = i > rs && sprev == FRESH;   // re is a word start (its word ended)
+                const bool p1in = pe == 0 || pe == re;
+                if (!re_ws) T += sprev >> 6;
+                unsigned gl1 = 31u - ((re_ws ? L.rec[re].smask : sprev) & 31u);   // local G of P1 at re
                 // ---- row scan of the chunk transfers: (reset, value) -- a chunk with a word start
                 //      ignores its input; otherwise out = in (+) local, (+) = costs add, G max
                 unsigned x = (pe ? 0x10000u : 0u) | sprev;
@@ -1009,6 +1028,103 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                     if (pe) {
                         const unsigned kl = L.rec[pe].smask;
                         L.rec[pe].smask = (uint16_t)((in & 0xFFC0u) + (kl & 0xFFC0u) + min(in & 31u, kl & 31u));
+                        if (gin > 31u - (kl & 31u)) L.rec[pe].cpos = (uint16_t)((L.rec[pe].cpos & 0x87FFu) | ((gin - 1u) << 11));
+                    }
+                }
+                const unsigned gre = p1in ? max(gin, gl1) : gl1;   // G at re of P1's word (its L* if re_ws)
+
+                // ---- C1 (replaces C0 + C1 for the wave): the selection walks, one chunk per lane.
+                // Every tokenization passes through the cuts, so a chunk's tokens are the ones its
+                // own walk from re down to rs emits; their count T is fixed (the pieces' costs).
+                // The walk rule is C1's (dg while the longest token so far A is below the word's
+                // L*, de after).  What a chunk needs from the right: P1's L* (a copy scan from
+                // the chunk holding its word end) and whether A has reached L* on entry.  Left of
+                // q (the first cut where G reaches L*: gre < L*) it has -- the L* token lies in the
+                // segment ending at q; right of q, dg == de everywhere (every j in E(i) is at or
+                // after q, so G[j] == L*), so it does not matter; in q's chunk it has iff a chunk
+                // to the right selected an L* token by chance -- the flag scan after the walks,
+                // and that chunk re-walks P1 in de mode.
+                // token base: exclusive prefix sum of T over the row; the window's count to wtok
+                unsigned tb = T;
+                tb += (unsigned)__builtin_amdgcn_update_dpp(0, (int)tb, 0x111, 0xF, 0xF, false);
+                tb += (unsigned)__builtin_amdgcn_update_dpp(0, (int)tb, 0x112, 0xF, 0xF, false);
+                tb += (unsigned)__builtin_amdgcn_update_dpp(0, (int)tb, 0x114, 0xF, 0xF, false);
+                tb += (unsigned)__builtin_amdgcn_update_dpp(0, (int)tb, 0x118, 0xF, 0xF, false);
+                if (d == 15) SS[mg].wtok = tb;
+                tb -= T;
+                // P1's L*: from rec[re] when its word ends at re, else from the right (the first
+                // word end of the next chunk that has one)
+                unsigned lsr = pe ? (0x10000u | (((unsigned)L.rec[pe].cpos >> 11) & 15u)) : 0u;
+                auto copy_r = [&](unsigned y) { lsr = (lsr >> 16) ? lsr : y; };
+                copy_r((unsigned)__builtin_amdgcn_update_dpp(0, (int)lsr, 0x101, 0xF, 0xF, false));   // row_shl:1
+                copy_r((unsigned)__builtin_amdgcn_update_dpp(0, (int)lsr, 0x102, 0xF, 0xF, false));   // row_shl:2
+                copy_r((unsigned)__builtin_amdgcn_update_dpp(0, (int)lsr, 0x104, 0xF, 0xF, false));   // row_shl:4
+                copy_r((unsigned)__builtin_amdgcn_update_dpp(0, (int)lsr, 0x108, 0xF, 0xF, false));   // row_shl:8
+                // (DPP reads outside any branch: a lane masked off in EXEC reads as 0)
+                const unsigned lsn = (unsigned)__builtin_amdgcn_update_dpp(0, (int)lsr, 0x101, 0xF, 0xF, false);
+                const unsigned ls1 = re_ws ? gre : (lsn & 15u) + 1u;
+                const bool walk = !len_only && SS[mg].status == 0;   // per row (not uniform)
+                const bool left_of_q = gre < ls1;
+                unsigned n1 = 0;   // tokens of P1
+                unsigned afin = 0, lsm = ls1;   // after the walk: A and L* of the last piece
+                {
+                    unsigned ii = re, k = walk ? tb + T : tb, A = left_of_q ? ls1 : 0u, Ls = ls1;
+                    unsigned pend = rec32[re] & 0x7FFu;
+                    bool inp1 = true;
+                    while (ballot(k > tb)) {
+                        if (k > tb) {
+                            const unsigned rr = rec32[ii];
+                            const unsigned cpi = rr & 0x7FFu;
+                            if (ii < re && (rr & CP_WS)) {   // into the word ending at ii
+                                Ls = ((rr >> 11) & 15u) + 1u;
+                                A = 0;
+                                pend = cpi;
+                                inp1 = false;
+                            }
+                            n1 += inp1 ? 1u : 0u;
+                            const unsigned f = L.fin[ii].v;
+                            const unsigned sp = pend - cpi;
+                            A = A > sp ? A : sp;
+                            const unsigned dd = A < Ls ? (f & 15u) : (f >> 4);
+                            const unsigned j = ii - 1u - dd;
+                            k--;
+                            L.rec[k].smask = (uint16_t)j;   // k < rs or a position this walk has left
+                            pend = cpi;
+                            ii = j;
+                        }
+                    }
+                    const unsigned sp = pend - (rec32[rs] & 0x7FFu);
+                    afin = A > sp ? A : sp;
+                    lsm = Ls;
+                }
+                // flag scan, right to left: the chunk's last piece reached its L* (sel); a chunk
+                // whose last piece is P1 also passes on what came in; none crosses a word start
+                unsigned fl = ((T > 0 && afin >= lsm) ? 1u : 0u) | ((!p1in || re_ws) ? 2u : 0u);
+                auto flag_r = [&](unsigned y) { fl = (fl & 2u) ? fl : (fl | (y & 3u)); };
+                flag_r((unsigned)__builtin_amdgcn_update_dpp(0, (int)fl, 0x101, 0xF, 0xF, false));   // row_shl:1
+                flag_r((unsigned)__builtin_amdgcn_update_dpp(0, (int)fl, 0x102, 0xF, 0xF, false));   // row_shl:2
+                flag_r((unsigned)__builtin_amdgcn_update_dpp(0, (int)fl, 0x104, 0xF, 0xF, false));   // row_shl:4
+                flag_r((unsigned)__builtin_amdgcn_update_dpp(0, (int)fl, 0x108, 0xF, 0xF, false));   // row_shl:8
+                const unsigned fln = (unsigned)__builtin_amdgcn_update_dpp(0, (int)fl, 0x101, 0xF, 0xF, false);
+                const bool fin_in = !re_ws && (fln & 1u) != 0;
+#ifdef DPT_LANEDBG
+                if (lane == 0) atomicAdd(&g_lanedbg[16 * 16 + 2], 1u);
+                if (SS[mg].s == 0 && na > 0) {
+                    unsigned *o = g_lanedbg + d * 16;
+                    o[0] = rs; o[1] = re; o[2] = pe; o[3] = T; o[4] = tb; o[5] = gin; o[6] = gre; o[7] = ls1;
+                    o[8] = left_of_q; o[9] = fl; o[10] = fin_in; o[11] = n1; o[12] = afin; o[13] = lsm;
+                    o[14] = re_ws | (p1in << 1) | (walk << 2); o[15] = in;
+                }
+#endif
+                // q's chunk with a chance L* token to the right: P1 again in de mode (A = L*);
+                // P1 starts below L* only from rs with gin < L* or from a word start inside
+                if (walk && fin_in && !left_of_q && (!p1in || gin < ls1)) {
+                    unsigned ii = re, k = tb + T;
+                    for (unsigned c = 0; c < n1; c++) {
+                        const unsigned j = ii - 1u - (unsigned)(L.fin[ii].v >> 4);
+                        k--;
+                        L.rec[k].smask = (uint16_t)j;
+                        ii = j;
                     }
                 }
               }
@@ -1027,11 +1143,17 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 if (!capb) {
                     if constexpr (G == 16) {
                         if (a.mode & dpt::DPT_FLAG_OLD_B) forward(F_{}, C2_{});
-                        else forward_lanes();
+                        else { forward_lanes(); lane_mode = true; }
+#ifdef DPT_LANEDBG
+                        if (lane == 0) atomicAdd(&g_lanedbg[16 * 16 + 1], 1u);
+#endif
                     } else {
                         forward(F_{}, C2_{});
                     }
                 } else if (uncapped) forward(F_{}, C1_{}); else forward(F_{}, C0_{});
+#ifdef DPT_LANEDBG
+                if (capb && lane == 0) atomicAdd(&g_lanedbg[16 * 16], 1u);
+#endif
             }
         }
         wave_sync();
@@ -1039,7 +1161,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
 
         // ---------------------------------------------------------- C0: per-window token counts and validity
         // (word w ends at atom word_end(w); its final state is in fin[word_end(w)])
-        {
+        if (!lane_mode) {
             unsigned pre[NG + 1];
             pre[0] = 0;
 #pragma unroll
@@ -1084,7 +1206,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
         for (int rep_ = 0; rep_ < 2; rep_++) {
             if (rep_) wave_sync();
 #endif
-        {
+        if (!lane_mode) {
             unsigned pre[NG + 1], tokpre[NG + 1], inv_g[NG];
             pre[0] = 0; tokpre[0] = 0;
 #pragma unroll
@@ -1467,6 +1589,11 @@ hipError_t kernel_init() {
 int small_window_bytes() { return SMALL_CH; }
 int big_window_bytes() { return BIG_CH; }
 
+#ifdef DPT_LANEDBG
+extern "C" int dpt_debug_lanes(unsigned *out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lanedbg), sizeof(unsigned) * (16 * 16 + 4)) == hipSuccess ? 0 : -1;
+}
+#endif
 #ifdef DPT_STAMPS
 extern "C" int dpt_debug_stamps(unsigned long long *out, int reset) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 8) != hipSuccess) return -1;

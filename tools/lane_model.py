@@ -1,0 +1,193 @@
+"""Diagnostic: a CPU model of the lane-mode B + C1 of tokenize_kernel (G = 16, capless windows),
+phase by phase over the 16 lanes of a row, for checking the chunk algorithm against the oracle's
+selection on single windows (raw mode, strings <= 256 bytes)."""
+import os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "dp-tokenization_amd"), os.path.join(ROOT, "tests")]
+from oracle import ref_port
+
+FRESH = 31
+
+def relax(sj, span):
+    a1 = sj + 64
+    a2 = (a1 | 31) - span
+    return min(a1, a2)
+
+def window(text):
+    """atoms (expanded strings), word-start flags per atom, cpos (code-point prefix) per boundary"""
+    words = ref_port.raw_words(text)
+    atoms, ws = [], []
+    for w in words:
+        for k, a in enumerate(w):
+            atoms.append(a); ws.append(k == 0)
+    cpos = [0]
+    for a in atoms:
+        cpos.append(cpos[-1] + len(a))
+    return atoms, ws + [True], cpos
+
+def model(text, vocab, verbose=False):
+    atoms, wsf, cpos = window(text)
+    na = len(atoms)
+    # end masks: bit d of em[i] = atoms i-1-d .. i-1 form a token (within a word)
+    em = [0] * (na + 1)
+    for j in range(na):
+        s = ""
+        for L in range(1, 17):
+            if j + L > na or (L > 1 and wsf[j + L - 1]):
+                break
+            s += atoms[j + L - 1]
+            if s in vocab:
+                em[j + L] |= 1 << (L - 1)
+    assert all(em[i] & 1 for i in range(1, na + 1)), "not capless"
+    key = [0] * (na + 2); fin = [0] * (na + 2); lstar = [0] * (na + 2)
+    C = (na + 15) >> 4
+    lanes = []
+    for d in range(16):
+        c0 = min(d * C, na); c1 = min(c0 + C, na)
+        mloc, lcut = 0xFFFF, 0
+        for k in range(15, -1, -1):
+            i = c0 + 1 + k
+            if i <= c1:
+                hb = em[i].bit_length() - 1
+                mloc = min(mloc, i - 1 - hb)
+                if mloc >= i - 1:
+                    lcut |= 1 << k
+        lanes.append(dict(c0=c0, c1=c1, mloc=mloc, lcut=lcut))
+    for d in range(16):
+        S = min([l["mloc"] for l in lanes[d + 1:]] + [0xFFFF])
+        c0 = lanes[d]["c0"]; lcut = lanes[d]["lcut"]
+        cut = 0 if S < c0 else (lcut if S - c0 >= 15 else lcut & ((2 << (S - c0)) - 1))
+        lanes[d]["fc"] = c0 + ((cut & -cut).bit_length() - 1) if cut else na
+    for d in range(16):
+        lanes[d]["rs"] = min([l["fc"] for l in lanes[d:]])
+    for d in range(16):
+        lanes[d]["re"] = lanes[d + 1]["rs"] if d < 15 else na
+    # B loop
+    for d, l in enumerate(lanes):
+        rs, re = l["rs"], l["re"]
+        i = rs; ws = rs; sprev = FRESH; pe = 0; T = 0
+        while i < re:
+            i += 1
+            best = relax(sprev, cpos[i] - cpos[i - 1]); dg = de = 0
+            for dd in range(1, 16):
+                if em[i] >> dd & 1:
+                    j = i - 1 - dd
+                    assert j >= ws
+                    sj = FRESH if j == ws else key[j]
+                    kk = relax(sj, cpos[i] - cpos[j])
+                    if (kk >> 5) < (best >> 5): de = dd
+                    if kk < best: dg = dd
+                    best = min(best, kk)
+            key[i] = best; fin[i] = dg | de << 4
+            if wsf[i]:
+                lstar[i] = 31 - (best & 31)
+                T += best >> 6
+                if not pe: pe = i
+                ws = i; sprev = FRESH
+            else:
+                sprev = best
+        re_ws = i > rs and sprev == FRESH
+        p1in = pe == 0 or pe == re
+        if not re_ws: T += sprev >> 6
+        gl1 = 31 - ((key[re] if re_ws else sprev) & 31)
+        l.update(pe=pe, T=T, sprev=sprev, re_ws=re_ws, p1in=p1in, gl1=gl1)
+    # transfer scan (left to right)
+    inn = FRESH
+    for d, l in enumerate(lanes):
+        l["in"] = inn
+        x = l["sprev"]
+        if l["pe"]:
+            inn = x
+        else:
+            inn = (inn & 0xFFC0) + (x & 0xFFC0) + min(inn & 31, x & 31)
+    for d, l in enumerate(lanes):
+        rs, re, pe, inn = l["rs"], l["re"], l["pe"], l["in"]
+        gin = 31 - (inn & 31)
+        l["gin"] = gin
+        if gin:
+            lim = pe if pe else re
+            for q in range(rs + 1, lim + 1):
+                if gin >= 31 - (key[q] & 31):
+                    fin[q] = (fin[q] & 0xF0) | (fin[q] >> 4)
+            if pe:
+                kl = key[pe]
+                key[pe] = (inn & 0xFFC0) + (kl & 0xFFC0) + min(inn & 31, kl & 31)
+                if gin > 31 - (kl & 31):
+                    lstar[pe] = gin
+        l["gre"] = max(gin, l["gl1"]) if l["p1in"] else l["gl1"]
+    # token bases
+    tb = 0
+    for l in lanes:
+        l["tb"] = tb; tb += l["T"]
+    # P1 L*: from the right
+    for d, l in enumerate(lanes):
+        if l["re_ws"]:
+            l["ls1"] = l["gre"]
+        else:
+            nxt = [m for m in lanes[d + 1:] if m["pe"]]
+            l["ls1"] = lstar[nxt[0]["pe"]] if nxt else 1
+    starts = [None] * tb
+    for d, l in enumerate(lanes):
+        rs, re, T, tbd, ls1 = l["rs"], l["re"], l["T"], l["tb"], l["ls1"]
+        left = l["gre"] < ls1
+        l["left"] = left
+        ii = re; k = tbd + T; A = ls1 if left else 0; Ls = ls1; pend = cpos[re]; inp1 = True; n1 = 0
+        while k > tbd:
+            if ii < re and wsf[ii]:
+                Ls = lstar[ii]; A = 0; pend = cpos[ii]; inp1 = False
+            n1 += inp1
+            f = fin[ii]
+            sp = pend - cpos[ii]; A = max(A, sp)
+            dd = (f & 15) if A < Ls else (f >> 4)
+            j = ii - 1 - dd
+            k -= 1; starts[k] = j
+            pend = cpos[ii]; ii = j
+        assert ii == rs, (d, ii, rs)
+        afin = max(A, pend - cpos[rs])
+        l.update(n1=n1, sel=T > 0 and afin >= Ls, stop=(not l["p1in"]) or l["re_ws"])
+    for d, l in enumerate(lanes):
+        f = False
+        if not l["re_ws"]:
+            for m in lanes[d + 1:]:
+                f = f or m["sel"]
+                if m["stop"]:
+                    break
+        l["fin_in"] = f
+        if f and not l["left"] and (not l["p1in"] or l["gin"] < l["ls1"]):
+            ii = l["re"]; k = l["tb"] + l["T"]
+            for c in range(l["n1"]):
+                j = ii - 1 - (fin[ii] >> 4)
+                k -= 1; starts[k] = j; ii = j
+    toks = []
+    for k in range(tb):
+        e = starts[k + 1] if k + 1 < tb else na
+        toks.append("".join(atoms[starts[k]:e]))
+    if verbose:
+        for d, l in enumerate(lanes):
+            print(d, {k: l[k] for k in ("rs", "re", "pe", "T", "tb", "gin", "gre", "ls1", "left", "sel", "stop", "fin_in", "n1", "p1in", "re_ws")})
+    return toks
+
+def ref_tokens(text, vocab):
+    out = []
+    for w in ref_port.raw_words(text):
+        toks, _ = ref_port.enumerate_shortest(w, vocab)
+        out += ref_port.longest_token_choice(toks)
+    return out
+
+if __name__ == "__main__":
+    from dptok import synth
+    from conftest import load_golden
+    vocab = set(synth.llama_shaped_vocab())
+    g = load_golden("cfg2_llama32k.json.gz")
+    bad = 0
+    for n, c in enumerate(g["cases"][:int(sys.argv[1]) if len(sys.argv) > 1 else 40]):
+        inv = {v: k for k, v in synth.llama_shaped_vocab().items()}
+        want = [inv[i] for i in c["ids"]]
+        got = model(c["text"], vocab)
+        if got != want:
+            bad += 1
+            k = next(k for k in range(min(len(got), len(want))) if got[k] != want[k])
+            print("case", n, "diff at", k, got[k-3:k+4], want[k-3:k+4])
+            if bad == 1:
+                model(c["text"], vocab, verbose=True)
+    print("bad", bad)
