@@ -302,3 +302,22 @@ def test_long_pass_dp_lengths(vocabs):
     st, lens, _ = enc.dp(text, offs, mode="atoms", cut_mask=cut)
     for k, w in enumerate(words):
         assert int(lens[k]) == _min_tokens_bounded(w, vocab, max_cp, capped=True), k
+
+
+def test_tie_heavy_long_words_vs_oracle():
+    """Lane-mode B + C1 (chunks cut inside words) on tie-heavy capless vocabularies over {a,b,c}:
+    long words, many equal-cost tokenizations, several L*-length tokens per word (the chance-flag
+    re-walk), batches that fill every row of every wave."""
+    from dptok import Encoder, Vocab, pack_strings
+    from oracle import oracle
+    from test_lane_model import tie_heavy_case
+    rng = np.random.default_rng(21)
+    for _ in range(30):
+        vocab, _ = tie_heavy_case(rng)
+        t2i = {t: i for i, t in enumerate(vocab)}
+        texts = [tie_heavy_case(rng, max_len=256)[1] for _ in range(400)]
+        text, offs = pack_strings(texts)
+        got = Encoder(Vocab(t2i, 0)).encode_csr(text, offs)
+        ref = oracle.OracleVocab(t2i).encode_csr(text, offs)
+        _cmp_csr(got, ref)
+        assert np.array_equal(got[3], ref[3])
