@@ -923,14 +923,17 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 };
                 // ---- cut points: boundary p is one iff min_{i > p} lo_i >= p, lo_i = the first atom
                 //      of the longest token ending at i (i-1 - highest bit of its end mask)
-                const unsigned C = (na + 15u) >> 4;   // boundaries per lane (na <= 256)
+                // boundaries per lane (na <= 256), odd: lanes stepping through their chunks together
+                // then hit distinct LDS banks (ds_read_b32: 32 banks per 32-lane group; a stride of
+                // 16 dwords put 8 lanes on a bank)
+                const unsigned C = ((na + 15u) >> 4) | 1u;   // <= 17
                 const unsigned c0 = min(d * C, na), c1 = min(c0 + C, na);
                 // one backward pass over the chunk's ends (c0, c1]: the local suffix min of lo
                 // decides the cuts as far as this chunk's ends go; the later chunks' ends (min S)
                 // then only cap them: p is a cut iff both mins are >= p, i.e. p <= S
                 unsigned mloc = 0xFFFFu, lcut = 0;
 #pragma unroll 4
-                for (int k = 15; k >= 0; k--) {
+                for (int k = 16; k >= 0; k--) {
                     const unsigned i = c0 + 1u + (unsigned)k;
                     if (i <= c1) {
                         const unsigned hb = 31u - (unsigned)__builtin_clz((~rec32[i] >> 16) | 1u);   // bit 0 is set in a capless window
@@ -946,7 +949,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 sm = min(sm, (unsigned)__builtin_amdgcn_update_dpp((int)0xFFFFu, (int)sm, 0x108, 0xF, 0xF, false));
                 const unsigned S = (unsigned)__builtin_amdgcn_update_dpp((int)0xFFFFu, (int)sm, 0x101, 0xF, 0xF, false);
                 // boundaries c0 + k <= S
-                const unsigned cut = S < c0 ? 0u : (S - c0 >= 15u ? lcut : lcut & ((2u << (S - c0)) - 1u));
+                const unsigned cut = S < c0 ? 0u : (S - c0 >= 16u ? lcut : lcut & ((2u << (S - c0)) - 1u));
                 // rs = the first cut at or after c0 (in this lane's chunk or a later one; na is a cut)
                 unsigned rs = cut ? c0 + ffbl(cut) : na;
                 rs = min(rs, (unsigned)__builtin_amdgcn_update_dpp((int)na, (int)rs, 0x101, 0xF, 0xF, false));

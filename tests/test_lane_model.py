@@ -33,8 +33,8 @@ def test_lane_model_matches_oracle(seed):
     from oracle import oracle
     from dptok import pack_strings
     rng = np.random.default_rng(100 + seed)
-    for _ in range(60):
-        vocab, text = tie_heavy_case(rng)
+    for n in range(150):
+        vocab, text = tie_heavy_case(rng, max_len=256 if n % 2 else 120)
         t2i = {t: i for i, t in enumerate(vocab)}
         txt, offs = pack_strings([text])
         ids, off, st, _ = oracle.OracleVocab(t2i).encode_csr(txt, offs)

@@ -40,12 +40,12 @@ def model(text, vocab, verbose=False):
                 em[j + L] |= 1 << (L - 1)
     assert all(em[i] & 1 for i in range(1, na + 1)), "not capless"
     key = [0] * (na + 2); fin = [0] * (na + 2); lstar = [0] * (na + 2)
-    C = (na + 15) >> 4
+    C = ((na + 15) >> 4) | 1
     lanes = []
     for d in range(16):
         c0 = min(d * C, na); c1 = min(c0 + C, na)
         mloc, lcut = 0xFFFF, 0
-        for k in range(15, -1, -1):
+        for k in range(16, -1, -1):
             i = c0 + 1 + k
             if i <= c1:
                 hb = em[i].bit_length() - 1
@@ -56,7 +56,7 @@ def model(text, vocab, verbose=False):
     for d in range(16):
         S = min([l["mloc"] for l in lanes[d + 1:]] + [0xFFFF])
         c0 = lanes[d]["c0"]; lcut = lanes[d]["lcut"]
-        cut = 0 if S < c0 else (lcut if S - c0 >= 15 else lcut & ((2 << (S - c0)) - 1))
+        cut = 0 if S < c0 else (lcut if S - c0 >= 16 else lcut & ((2 << (S - c0)) - 1))
         lanes[d]["fc"] = c0 + ((cut & -cut).bit_length() - 1) if cut else na
     for d in range(16):
         lanes[d]["rs"] = min([l["fc"] for l in lanes[d:]])
