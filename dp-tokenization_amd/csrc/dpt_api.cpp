@@ -179,11 +179,23 @@ int dpt_vocab_create(const uint8_t *utf8_blob, const uint64_t *tok_off, const in
     // bytes b0 b1 -- .x = base word of the node reached (0 if none), .y = that node's slot (0 if
     // none) | 1 << 30 if b0 is a root child | 1 << 31 if b0 alone is a token.  Phase A's first
     // lookup of every walk consumes two bytes through it.
+    // slots4: {base, check, id, child filter} per slot, then the root table again as
+    // {.x, .y, 0, child filter of the node reached} -- phase A of tokenize_kernel reads only these
+    // (a filter bit per possible next byte, dpt::child_bit: a walk whose next byte has no bit ends
+    // without the failing lookup)
     std::vector<int2> slots((size_t)da.n_slots + 65536);
-    std::vector<int4> slots4(da.n_slots);
+    std::vector<int4> slots4((size_t)da.n_slots + 65536);
+    std::vector<uint32_t> filt(da.n_slots, 0u);
+    for (uint32_t t = 0; t < da.n_slots; t++) {
+        const int32_t p = da.check[t];
+        if (p >= 0 && (uint32_t)p < da.n_slots) {
+            const uint32_t b = t - (uint32_t)(da.base[p] & 0x3FFFFFFF);
+            if (b < 256) filt[p] |= 1u << dpt::child_bit(b);
+        }
+    }
     for (uint32_t t = 0; t < da.n_slots; t++) {
         slots[t] = make_int2(da.base[t], da.check[t]);
-        slots4[t] = make_int4(da.base[t], da.check[t], da.id[t], 0);
+        slots4[t] = make_int4(da.base[t], da.check[t], da.id[t], (int32_t)filt[t]);
     }
     for (uint32_t b0 = 0; b0 < 256; b0++) {
         const uint32_t s1 = (uint32_t)da.root_base + b0;
@@ -196,11 +208,12 @@ int dpt_vocab_create(const uint8_t *utf8_blob, const uint64_t *tok_off, const in
             const bool e2 = e1 && !leaf1 && s2 < da.n_slots && da.check[s2] == (int32_t)s1;
             const uint32_t y = (e2 ? s2 : 0u) | (e1 ? 0x40000000u : 0u) | (term1 ? 0x80000000u : 0u);
             slots[(size_t)da.n_slots + (b0 << 8) + b1] = make_int2(e2 ? da.base[s2] : 0, (int32_t)y);
+            slots4[(size_t)da.n_slots + (b0 << 8) + b1] = make_int4(e2 ? da.base[s2] : 0, (int32_t)y, 0, e2 ? (int32_t)filt[s2] : 0);
         }
     }
     e = hipMalloc((void **)&v->d_slots, sizeof(int2) * slots.size());
-    if (e == hipSuccess) e = hipMalloc((void **)&v->d_slots4, sizeof(int4) * da.n_slots);
-    if (e == hipSuccess) e = hipMemcpy(v->d_slots4, slots4.data(), sizeof(int4) * da.n_slots, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc((void **)&v->d_slots4, sizeof(int4) * slots4.size());
+    if (e == hipSuccess) e = hipMemcpy(v->d_slots4, slots4.data(), sizeof(int4) * slots4.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc((void **)&v->d_ids, sizeof(int32_t) * da.n_slots);
     if (e == hipSuccess) e = hipMemcpy(v->d_slots, slots.data(), sizeof(int2) * slots.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(v->d_ids, da.id, sizeof(int32_t) * da.n_slots, hipMemcpyHostToDevice);
@@ -218,7 +231,7 @@ int dpt_vocab_create(const uint8_t *utf8_blob, const uint64_t *tok_off, const in
     v->stats.n_slots = da.n_slots;
     v->stats.max_bytes = da.max_bytes;
     v->stats.max_cp = da.max_cp;
-    v->stats.device_bytes = (uint64_t)da.n_slots * (sizeof(int2) + sizeof(int32_t) + sizeof(int4)) + 65536 * sizeof(int2);
+    v->stats.device_bytes = (uint64_t)da.n_slots * (sizeof(int2) + sizeof(int32_t) + sizeof(int4)) + 65536 * (sizeof(int2) + sizeof(int4));
     dpt::free_double_array(&da);
     *out = v;
     return DPT_OK;

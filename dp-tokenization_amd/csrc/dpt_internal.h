@@ -40,6 +40,10 @@ struct EncodeLaunch {
     int32_t root_base;
 };
 
+// child filter bit of next byte b (slots4[].w, host and device): XOR with b >> 5 permutes the
+// low five bits inside each 32-byte block, so the 26 lowercase letters get distinct bits
+__host__ __device__ inline unsigned child_bit(unsigned b) { return (b ^ (b >> 5)) & 31u; }
+
 // internal mode bit (never in the public API): A/B diagnostic, DPT_B=rows selects the 16-lane
 // row recurrence for capless windows instead of the lane-chunk one (dpt_api.cpp)
 constexpr int DPT_FLAG_OLD_B = 0x40000000;

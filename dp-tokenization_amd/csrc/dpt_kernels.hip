@@ -254,6 +254,12 @@ __device__ __forceinline__ int2 trie_slot(const TrieView &tv, int32_t t) {
     const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, (unsigned)t * 8u, 0, 0);
     return make_int2((int32_t)v[0], (int32_t)v[1]);
 }
+// phase A: {base, check, id, child filter} per slot, then the root table as {.x, .y, 0, child
+// filter} (dpt_api.cpp), so one 16-byte load serves both
+__device__ __forceinline__ int4 trie_slotA(const TrieView &tv, int32_t t) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)tv.slots4, (short)0, (int)((tv.n_slots + 65536u) * 16u), 0x00020000);
+    return __builtin_bit_cast(int4, __builtin_amdgcn_raw_buffer_load_b128(r, (unsigned)t * 16u, 0, 0));
+}
 __device__ __forceinline__ int4 trie_slot4(const TrieView &tv, int32_t t) {
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)tv.slots4, (short)0, (int)(tv.n_slots * 16u), 0x00020000);
     return __builtin_bit_cast(int4, __builtin_amdgcn_raw_buffer_load_b128(r, (unsigned)t * 16u, 0, 0));
@@ -724,7 +730,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 }
                 if (!ballot(active)) break;
                 const int32_t t = t2 ? (int32_t)t2 : nb + (int32_t)(seq & 0xFFu);
-                const int2 ent = trie_slot(tv, t);   // buffer load: inactive lanes read harmlessly
+                const int4 ent = trie_slotA(tv, t);   // buffer load: inactive lanes read harmlessly
                 bool done = false;
                 if (active) {
                     bool ok;
@@ -766,9 +772,12 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                                 const GL &L = *reinterpret_cast<const GL *>(smem + lbase);
                                 info = ainfo_get(L, j + len, false);
                                 seq = atom_from_info<CH, WIDE>(L.bytes, info, raw, cnt);
+                                // the node has no child for the next byte: over without the lookup
+                                done = !((ent.w >> child_bit((unsigned)(seq & 0xFFu))) & 1);
                             }
-                        } else if (leaf) {
-                            done = true;   // no token continues inside this atom
+                        } else {
+                            // no token continues inside this atom (leaf, or no child for its next byte)
+                            done = leaf || !((ent.w >> child_bit((unsigned)(seq & 0xFFu))) & 1);
                         }
                     }
                 }
