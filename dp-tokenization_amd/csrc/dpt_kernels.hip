@@ -1293,13 +1293,17 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
             }
             const unsigned total = pre[NG];
             // One token walk per lane; a lane whose token is resolved writes the id and takes the
-            // next token (ballot + mbcnt), so each iteration is one trie step for 64 tokens.
-            unsigned jj = 0, j1 = 0, cnt = 0, lbase = 0;
-            int32_t node = 0, nb = 0, id = -1;
-            bool ok = true;
-            uint64_t seq = 0;
-            int32_t *out = nullptr;
-            auto tstart = [&](unsigned t) {
+            // next token (ballot + mbcnt), so each iteration is one trie step for 64 tokens.  A
+            // token's bytes do not depend on the trie, so each iteration issues the trie load
+            // first and does the LDS work of the next byte / atom / token (known before the
+            // load returns: the token ends when its last atom's bytes run out) under it.
+            struct Tok {
+                unsigned jj, j1, cnt, lbase;
+                uint64_t seq;
+                int32_t *out;
+            };
+            auto tstart = [&](unsigned t) -> Tok {
+                Tok T;
                 unsigned g = 0;
 #pragma unroll
                 for (int k = 1; k < NG; k++) g += t >= pre[k] ? 1u : 0u;
@@ -1307,47 +1311,55 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
 #pragma unroll
                 for (int k = 0; k < NG; k++)
                     if (g == (unsigned)k) { base = pre[k]; na = na_g[k]; ntk = pre[k + 1] - pre[k]; fw = (firstmask >> k) & 1u; }
-                lbase = g * (unsigned)group_lds_bytes<CH, G>();
-                const GL &L = *reinterpret_cast<const GL *>(smem + lbase);
+                T.lbase = g * (unsigned)group_lds_bytes<CH, G>();
+                const GL &L = *reinterpret_cast<const GL *>(smem + T.lbase);
                 const unsigned k = t - base;
-                jj = (unsigned)L.rec[k].smask;
-                j1 = k + 1 < ntk ? (unsigned)L.rec[k + 1].smask : na;
-                seq = atom_from_info<CH, WIDE>(L.bytes, AInfo<CH>::pack(L.aoff[jj], L.atom_len(jj), 0, raw && fw && jj == 0), raw, cnt);
-                node = 0; nb = tv.root_base; id = -1; ok = true;
+                T.jj = (unsigned)L.rec[k].smask;
+                T.j1 = k + 1 < ntk ? (unsigned)L.rec[k + 1].smask : na;
+                T.seq = atom_from_info<CH, WIDE>(L.bytes, AInfo<CH>::pack(L.aoff[T.jj], L.atom_len(T.jj), 0, raw && fw && T.jj == 0), raw, T.cnt);
                 const SlotState &S = SS[g];
-                out = a.staging + S.sb + S.ntok + k;
+                T.out = a.staging + S.sb + S.ntok + k;
+                return T;
             };
             bool active = lane < total;
-            if (active) tstart(lane);
+            Tok C;
+            C.jj = C.j1 = C.cnt = C.lbase = 0; C.seq = 0; C.out = nullptr;
+            if (active) C = tstart(lane);
+            int32_t node = 0, nb = tv.root_base;
+            bool ok = true;
             unsigned nxt = 64;
             while (ballot(active)) {
-                const int32_t sl = nb + (int32_t)(seq & 0xFFu);
+                const int32_t sl = nb + (int32_t)(C.seq & 0xFFu);
                 const int4 ent = trie_slot4(tv, sl);   // buffer load: inactive lanes read harmlessly
-                bool done = false;
-                if (active) {
-                    ok &= ent.y == node;
-                    node = sl;
-                    nb = ent.x & BASE_MASK;
-                    id = ent.z;
-                    seq >>= 8;
-                    if (--cnt == 0) {
-                        if (++jj == j1) {
-                            done = true;
-                        } else {
-                            const GL &L = *reinterpret_cast<const GL *>(smem + lbase);
-                            seq = atom_from_info<CH, WIDE>(L.bytes, AInfo<CH>::pack(L.aoff[jj], L.atom_len(jj), 0, 0), raw, cnt);
-                        }
-                    }
+                // ---- under the load: the next byte, atom or token
+                C.seq >>= 8;
+                const bool aend = active && --C.cnt == 0;
+                const bool done = aend && C.jj + 1 == C.j1;
+                if (aend && !done) {
+                    C.jj++;
+                    const GL &L = *reinterpret_cast<const GL *>(smem + C.lbase);
+                    C.seq = atom_from_info<CH, WIDE>(L.bytes, AInfo<CH>::pack(L.aoff[C.jj], L.atom_len(C.jj), 0, 0), raw, C.cnt);
                 }
                 const uint64_t dm = ballot(done);
+                Tok Nx = C;
+                bool nact = false;
                 if (done) {
-                    *out = ok ? id : -1;
                     const unsigned rank = __builtin_amdgcn_mbcnt_hi((unsigned)(dm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)dm, 0u));
                     const unsigned uu = nxt + rank;
-                    active = uu < total;
-                    if (active) tstart(uu);
+                    nact = uu < total;
+                    if (nact) Nx = tstart(uu);
                 }
                 nxt += (unsigned)__builtin_popcountll(dm);
+                // ---- the trie step
+                ok &= ent.y == node;
+                node = sl;
+                nb = ent.x & BASE_MASK;
+                if (done) {
+                    *C.out = ok ? ent.z : -1;   // the id arrives with the token's last node
+                    C = Nx;
+                    active = nact;
+                    node = 0; nb = tv.root_base; ok = true;
+                }
             }
         }
 #if DPT_DOUBLE == 4
