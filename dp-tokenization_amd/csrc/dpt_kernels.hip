@@ -556,6 +556,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
     const unsigned mg = lane / G;        // my group
     const unsigned d = lane % G;         // my back distance - 1
     const uint64_t n_work = BIG ? (uint64_t)(*a.work_count) : a.n_str;
+    if (BIG && n_work == 0) return;   // no retries: no counter traffic
     const uint64_t base_off = a.str_off[0];
     const int mode = a.mode & DPT_MODE_MASK;
     const bool raw = mode == 0;

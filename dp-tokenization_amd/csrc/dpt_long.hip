@@ -192,6 +192,7 @@ __global__ void __launch_bounds__(64) long_kernel(Args a) {
     const bool len_only = (a.mode & (DPT_FLAG_UNCAPPED | DPT_FLAG_LEN_ONLY)) != 0;
     const uint64_t base_off = a.str_off[0];
     const unsigned n_work = *a.list_count;
+    if (n_work == 0) return;   // the usual case: no counter traffic
 
     for (;;) {
         unsigned idx = 0;

@@ -60,8 +60,9 @@ def main():
            "fetch_bytes_raw": fetch, "fetch_bytes": 2 * fetch, "write_bytes": write,
            "traffic_bytes_per_launch": 2 * fetch + write,
            "method": "rocprofv3 --kernel-trace --pmc FETCH_SIZE | WRITE_SIZE (separate passes); FETCH_SIZE x2 (gfx950)"}
-    with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as fh:
-        json.dump(rec, fh, indent=1)
+    for path in (os.path.join(ROOT, "profiles", "pmc_traffic.json"), os.path.join(out, "pmc_traffic.json")):
+        with open(path, "w") as fh:   # the gpurun_out copy is what travels back from a GPU box
+            json.dump(rec, fh, indent=1)
     print(json.dumps(rec))
 
 
