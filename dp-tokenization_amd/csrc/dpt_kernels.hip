@@ -657,11 +657,30 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
             if (rep_) wave_sync();
 #endif
         {
-            unsigned pre[NG + 1];
-            pre[0] = 0;
+            // A0 (16-lane rows, raw mode): slots whose window is pure ASCII -- atoms are its bytes --
+            // get every walk's first lookup here, byte-parallel with four loads in flight per lane;
+            // the walks it cannot finish (word starts, the string's first atom, '\n', and walks that
+            // go on past the two-byte root entry: ~6 % in cfg2 with the child filters) are marked
+            // (bit 4g + u of `mark`: atom 4 * lane + u of slot g) and redone by the walker below,
+            // which also takes every atom of the other slots.
+            unsigned a0mask = 0;
+            uint32_t mark = 0;
+            if constexpr (G == 16 && !BIG) {
+                if (raw) {
 #pragma unroll
-            for (int g = 0; g < NG; g++) pre[g + 1] = pre[g] + uni(SS[g].n_atoms);
-            const unsigned total = pre[NG];
+                    for (int g = 0; g < NG; g++) {
+                        const unsigned wl = uni(SS[g].n_atoms) > 0 ? uni(SS[g].wlen) : 0u;
+                        const uint32_t *b32 = reinterpret_cast<const uint32_t *>(grp(g).bytes);
+                        const uint32_t w0 = 4u * lane < wl ? b32[lane] : 0u;
+                        const unsigned nv = wl > 4u * lane ? min(wl - 4u * lane, 4u) : 0u;   // valid bytes in w0
+                        const uint32_t hi = w0 & (nv >= 4u ? 0x80808080u : ((1u << (8u * nv)) - 1u) & 0x80808080u);
+                        if (wl && !ballot(hi != 0)) a0mask |= 1u << g;
+                    }
+                }
+            }
+            unsigned nstart[NG];   // walker starts per slot: all atoms, or A0's marked ones
+#pragma unroll
+            for (int g = 0; g < NG; g++) nstart[g] = uni(SS[g].n_atoms);
             unsigned fwmask = 0;   // slots whose window starts the string (raw: '▁' + first atom)
 #pragma unroll
             for (int g = 0; g < NG; g++) fwmask |= (uni(SS[g].pos) == 0 ? 1u : 0u) << g;
@@ -680,14 +699,8 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 uint32_t *r32 = reinterpret_cast<uint32_t *>(smem + lbase);
                 __hip_atomic_fetch_and(&r32[e], ~(1u << (15u + ln)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             };
-            auto start = [&](unsigned uu) {
-                unsigned gs = 0;
-#pragma unroll
-                for (int g = 1; g < NG; g++) gs += uu >= pre[g] ? 1u : 0u;
-                unsigned base = 0;
-#pragma unroll
-                for (int g = 0; g < NG; g++) base = (gs == (unsigned)g) ? pre[g] : base;
-                j = uu - base;
+            auto start_gj = [&](unsigned gs, unsigned jj) {
+                j = jj;
                 lbase = gs * (unsigned)group_lds_bytes<CH, G>();
                 const GL &L = *reinterpret_cast<const GL *>(smem + lbase);
                 info = ainfo_get(L, j, raw && ((fwmask >> gs) & 1u));
@@ -712,6 +725,106 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 } else {
                     t2 = 0;
                 }
+            };
+            if constexpr (G == 16 && !BIG) {
+                if (a0mask) {
+                    constexpr unsigned END = 0x100u;
+#pragma unroll
+                    for (int g = 0; g < NG; g++) {
+                        if (!((a0mask >> g) & 1u)) continue;
+                        const unsigned wl = uni(SS[g].wlen);
+                        const bool first = uni(SS[g].pos) == 0;
+                        const unsigned gbase = (unsigned)g * (unsigned)group_lds_bytes<CH, G>();
+                        const uint32_t *b32 = reinterpret_cast<const uint32_t *>(grp(g).bytes);
+                        const unsigned k0 = 4u * lane;
+                        // bytes k0 .. k0+7 (past the window: masked by wl below)
+                        const uint64_t w = (uint64_t)b32[lane] | ((uint64_t)b32[lane + 1u] << 32);
+                        auto byte_at = [&](unsigned q) -> unsigned {   // byte k0+q, END past the window
+                            return k0 + q < wl ? (unsigned)((w >> (8u * q)) & 0xFFu) : END;
+                        };
+#ifndef A0_INFLIGHT
+#define A0_INFLIGHT 4
+#endif
+                        uint32_t *r32 = reinterpret_cast<uint32_t *>(smem + gbase);
+                        auto etok = [&](unsigned e, unsigned ln) {
+                            __hip_atomic_fetch_and(&r32[e], ~(1u << (15u + ln)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        };
+                        bool nocap = false;
+#pragma unroll
+                        for (int u0 = 0; u0 < 4; u0 += A0_INFLIGHT) {
+                        int32_t idx[A0_INFLIGHT];
+#pragma unroll
+                        for (int uq = 0; uq < A0_INFLIGHT; uq++) {
+                            const int u = u0 + uq;
+                            const unsigned b = byte_at(u), n1 = byte_at(u + 1);
+                            const bool stop = n1 == END || n1 == ' ';
+                            const unsigned e1 = n1 == '\n' ? (unsigned)'<' : n1;
+                            // a one-byte atom at the word's end: its own slot; else the two-byte root entry
+                            idx[uq] = stop ? tv.root_base + (int32_t)(b & 0xFFu) : (int32_t)(tv.n_slots + ((b & 0xFFu) << 8) + (e1 & 0xFFu));
+                        }
+                        int4 ent[A0_INFLIGHT];
+#pragma unroll
+                        for (int uq = 0; uq < A0_INFLIGHT; uq++) ent[uq] = trie_slotA(tv, idx[uq]);
+#pragma unroll
+                        for (int uq = 0; uq < A0_INFLIGHT; uq++) {
+                            const int u = u0 + uq;
+                            const unsigned k = k0 + (unsigned)u;
+                            const unsigned b = byte_at(u), n1 = byte_at(u + 1);
+                            if (b == END) continue;
+                            if (b == ' ' || b == '\n' || (first && k == 0)) { mark |= 1u << (4 * g + u); continue; }
+                            const int4 e = ent[uq];
+                            if (n1 == END || n1 == ' ') {
+                                // the atom alone is the walk: a root child that ends a token
+                                if (e.y == 0 && (e.x & TERM_BIT)) etok(k + 1u, 1u); else nocap = true;
+                                continue;
+                            }
+                            const bool b0tok = (e.y & 0x40000000) && e.y < 0;
+                            if (b0tok) etok(k + 1u, 1u); else nocap = true;
+                            if (!((e.y & 0x40000000) && (e.y & 0x3FFFFFFF))) continue;   // no node after two bytes
+                            bool more;
+                            if (n1 == '\n') {
+                                // inside atom k+1 = "<0x0A>" after its '<'
+                                more = !(e.x & LEAF_BIT) && ((e.w >> child_bit('0')) & 1);
+                            } else {
+                                // atom k+1 consumed: the span k .. k+2
+                                if (e.x & TERM_BIT) etok(k + 2u, 2u);
+                                const unsigned n2 = byte_at(u + 2);
+                                const unsigned e2 = n2 == '\n' ? (unsigned)'<' : n2;
+                                more = !(e.x & LEAF_BIT) && n2 != END && n2 != ' ' && ((e.w >> child_bit(e2)) & 1);
+                            }
+                            if (more) mark |= 1u << (4 * g + u);
+                        }
+                        }
+                        if (nocap) SS[g].capb = 1;
+                        // the slot's marked atoms, in order, into its fin[] (free until phase B)
+                        const unsigned mg = (mark >> (4 * g)) & 15u;
+                        const unsigned c = (unsigned)__builtin_popcount(mg);
+                        const unsigned incl = wave_incl_scan_add(c);
+                        unsigned o = incl - c;
+                        GL &Lg = grp(g);
+#pragma unroll
+                        for (int u = 0; u < 4; u++)
+                            if ((mg >> u) & 1u) Lg.fin[o++].v = (uint8_t)(k0 + (unsigned)u);
+                        nstart[g] = __builtin_amdgcn_readlane(incl, 63);
+                    }
+                }
+            }
+            unsigned pre[NG + 1];
+            pre[0] = 0;
+#pragma unroll
+            for (int g = 0; g < NG; g++) pre[g + 1] = pre[g] + nstart[g];
+            const unsigned total = pre[NG];
+            auto start = [&](unsigned uu) {
+                unsigned gs = 0;
+#pragma unroll
+                for (int g = 1; g < NG; g++) gs += uu >= pre[g] ? 1u : 0u;
+                unsigned base = 0;
+#pragma unroll
+                for (int g = 0; g < NG; g++) base = (gs == (unsigned)g) ? pre[g] : base;
+                unsigned jj = uu - base;
+                if constexpr (G == 16 && !BIG)
+                    if ((a0mask >> gs) & 1u) jj = grp(gs).fin[jj].v;   // A0 slot: its marked list
+                start_gj(gs, jj);
             };
             // Refills are batched: idle lanes take new starts only once A_REFILL of them are idle
             // (or the remaining starts fit), so the refill code runs on a fraction of the steps.
