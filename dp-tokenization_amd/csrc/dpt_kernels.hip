@@ -449,6 +449,7 @@ __device__ bool prep_window(GroupLDS<CH, G> &L, uint8_t *gw, const WinRegs<CH> &
                             unsigned wlen, int mode, unsigned lane, unsigned &n_atoms_o, unsigned &n_words_o) {
     const bool raw = mode == 0;
     unsigned n_atoms = 0, cp_tot = 0, n_words = 0;
+    bool hi_byte = false;   // some byte >= 0x80: atoms may be longer than one byte
 #pragma unroll
     for (int c = 0; c < CH / 256; c++) {
         const unsigned c0 = c * 256u;
@@ -476,6 +477,7 @@ __device__ bool prep_window(GroupLDS<CH, G> &L, uint8_t *gw, const WinRegs<CH> &
                 cl = (in && (b & 0xC0) != 0x80) ? 1 : 0;   // code points, whatever the atoms
             }
             ast[u] = as; wst[u] = wsf; cpl[u] = cl;
+            hi_byte |= in && (b & 0x80u) != 0;
             a_sum += as; w_sum += wsf; cp_sum += cl;
         }
         // one packed scan: atoms (9 bits) | words (9 bits) << 9 | code points (14 bits) << 18
@@ -517,6 +519,9 @@ __device__ bool prep_window(GroupLDS<CH, G> &L, uint8_t *gw, const WinRegs<CH> &
     // per-atom walk descriptor for phase A (parked in fin[], which phase B overwrites):
     //   byte offset | byte length << 12 | "a word or the window ends after it" << 16 | "first atom of the string" << 17
     const unsigned lim = WIDE ? MAX_ATOM_BYTES : 4u;   // RAW / PRESPLIT: code points (and '▁' + one fits 8 bytes)
+    // RAW / PRESPLIT windows of ASCII bytes have one-byte atoms only: nothing to check, and
+    // 16-lane rows park no descriptors
+    if (G == 16 && !WIDE && !ballot(hi_byte)) return true;
     bool bad = false;
     for (unsigned j = lane; j < n_atoms; j += 64) {
         const unsigned p0 = L.aoff[j], la = L.atom_len(j);
