@@ -1401,6 +1401,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
 #endif
         {
             unsigned pre[NG + 1], na_g[NG];
+            int32_t *obase[NG];       // staging row of the window's first token, per slot
             unsigned firstmask = 0;   // groups whose window starts the string (raw '▁' + first atom)
             pre[0] = 0;
 #pragma unroll
@@ -1409,6 +1410,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 pre[g + 1] = pre[g] + (gv ? uni(SS[g].wtok) : 0u);
                 na_g[g] = uni(SS[g].n_atoms);
                 firstmask |= (uni64(SS[g].pos) == 0 ? 1u : 0u) << g;
+                obase[g] = a.staging + uni64(SS[g].sb) + uni(SS[g].ntok);
             }
             const unsigned total = pre[NG];
             // One token walk per lane; a lane whose token is resolved writes the id and takes the
@@ -1427,17 +1429,17 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
 #pragma unroll
                 for (int k = 1; k < NG; k++) g += t >= pre[k] ? 1u : 0u;
                 unsigned base = 0, na = 0, ntk = 0, fw = 0;
+                int32_t *ob = obase[0];
 #pragma unroll
                 for (int k = 0; k < NG; k++)
-                    if (g == (unsigned)k) { base = pre[k]; na = na_g[k]; ntk = pre[k + 1] - pre[k]; fw = (firstmask >> k) & 1u; }
+                    if (g == (unsigned)k) { base = pre[k]; na = na_g[k]; ntk = pre[k + 1] - pre[k]; fw = (firstmask >> k) & 1u; ob = obase[k]; }
                 T.lbase = g * (unsigned)group_lds_bytes<CH, G>();
                 const GL &L = *reinterpret_cast<const GL *>(smem + T.lbase);
                 const unsigned k = t - base;
                 T.jj = (unsigned)L.rec[k].smask;
                 T.j1 = k + 1 < ntk ? (unsigned)L.rec[k + 1].smask : na;
                 T.seq = atom_from_info<CH, WIDE>(L.bytes, AInfo<CH>::pack(L.aoff[T.jj], L.atom_len(T.jj), 0, raw && fw && T.jj == 0), raw, T.cnt);
-                const SlotState &S = SS[g];
-                T.out = a.staging + S.sb + S.ntok + k;
+                T.out = ob + k;
                 return T;
             };
             bool active = lane < total;
