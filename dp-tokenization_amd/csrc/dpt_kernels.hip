@@ -1442,44 +1442,64 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 T.out = ob + k;
                 return T;
             };
-            bool active = lane < total;
-            Tok C;
-            C.jj = C.j1 = C.cnt = C.lbase = 0; C.seq = 0; C.out = nullptr;
-            if (active) C = tstart(lane);
-            int32_t node = 0, nb = tv.root_base;
-            bool ok = true;
-            unsigned nxt = 64;
-            while (ballot(active)) {
-                const int32_t sl = nb + (int32_t)(C.seq & 0xFFu);
-                const int4 ent = trie_slot4(tv, sl);   // buffer load: inactive lanes read harmlessly
-                // ---- under the load: the next byte, atom or token
-                C.seq >>= 8;
-                const bool aend = active && --C.cnt == 0;
-                const bool done = aend && C.jj + 1 == C.j1;
-                if (aend && !done) {
-                    C.jj++;
-                    const GL &L = *reinterpret_cast<const GL *>(smem + C.lbase);
-                    C.seq = atom_from_info<CH, WIDE>(L.bytes, AInfo<CH>::pack(L.aoff[C.jj], L.atom_len(C.jj), 0, 0), raw, C.cnt);
+#ifndef C2_WALKS
+#define C2_WALKS 1
+#endif
+            // C2_WALKS token walks per lane (tokens lane, lane + 64, ... first), so that many trie
+            // loads are in flight per lane in every iteration
+            constexpr int NW = C2_WALKS;
+            bool active[NW];
+            Tok C[NW];
+            int32_t node[NW], nb[NW];
+            bool ok[NW];
+#pragma unroll
+            for (int w = 0; w < NW; w++) {
+                active[w] = lane + 64u * w < total;
+                C[w].jj = C[w].j1 = C[w].cnt = C[w].lbase = 0; C[w].seq = 0; C[w].out = nullptr;
+                if (active[w]) C[w] = tstart(lane + 64u * w);
+                node[w] = 0; nb[w] = tv.root_base; ok[w] = true;
+            }
+            unsigned nxt = 64u * NW;
+            for (;;) {
+                bool any = false;
+#pragma unroll
+                for (int w = 0; w < NW; w++) any |= active[w];
+                if (!ballot(any)) break;
+                int32_t sl[NW];
+                int4 ent[NW];
+#pragma unroll
+                for (int w = 0; w < NW; w++) {
+                    sl[w] = nb[w] + (int32_t)(C[w].seq & 0xFFu);
+                    ent[w] = trie_slot4(tv, sl[w]);   // buffer load: inactive walks read harmlessly
                 }
-                const uint64_t dm = ballot(done);
-                Tok Nx = C;
-                bool nact = false;
-                if (done) {
-                    const unsigned rank = __builtin_amdgcn_mbcnt_hi((unsigned)(dm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)dm, 0u));
-                    const unsigned uu = nxt + rank;
-                    nact = uu < total;
-                    if (nact) Nx = tstart(uu);
+                // ---- under the loads: the next byte or atom
+                bool done[NW];
+#pragma unroll
+                for (int w = 0; w < NW; w++) {
+                    C[w].seq >>= 8;
+                    const bool aend = active[w] && --C[w].cnt == 0;
+                    done[w] = aend && C[w].jj + 1 == C[w].j1;
+                    if (aend && !done[w]) {
+                        C[w].jj++;
+                        const GL &L = *reinterpret_cast<const GL *>(smem + C[w].lbase);
+                        C[w].seq = atom_from_info<CH, WIDE>(L.bytes, AInfo<CH>::pack(L.aoff[C[w].jj], L.atom_len(C[w].jj), 0, 0), raw, C[w].cnt);
+                    }
                 }
-                nxt += (unsigned)__builtin_popcountll(dm);
-                // ---- the trie step
-                ok &= ent.y == node;
-                node = sl;
-                nb = ent.x & BASE_MASK;
-                if (done) {
-                    *C.out = ok ? ent.z : -1;   // the id arrives with the token's last node
-                    C = Nx;
-                    active = nact;
-                    node = 0; nb = tv.root_base; ok = true;
+                // ---- the trie steps; finished walks write their id and take the next token
+#pragma unroll
+                for (int w = 0; w < NW; w++) {
+                    ok[w] &= ent[w].y == node[w];
+                    node[w] = sl[w];
+                    nb[w] = ent[w].x & BASE_MASK;
+                    const uint64_t dm = ballot(done[w]);
+                    if (done[w]) {
+                        *C[w].out = ok[w] ? ent[w].z : -1;   // the id arrives with the token's last node
+                        const unsigned uu = nxt + __builtin_amdgcn_mbcnt_hi((unsigned)(dm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)dm, 0u));
+                        active[w] = uu < total;
+                        if (active[w]) C[w] = tstart(uu);
+                        node[w] = 0; nb[w] = tv.root_base; ok[w] = true;
+                    }
+                    nxt += (unsigned)__builtin_popcountll(dm);
                 }
             }
         }
