@@ -321,3 +321,23 @@ def test_tie_heavy_long_words_vs_oracle():
         ref = oracle.OracleVocab(t2i).encode_csr(text, offs)
         _cmp_csr(got, ref)
         assert np.array_equal(got[3], ref[3])
+
+
+def test_ascii_windows_phase_a0(engines, oracles):
+    """Pure-ASCII raw windows take phase A0 (the byte-parallel first lookup): control bytes,
+    '\\n' next to spaces, runs of spaces, words cut by the 256-byte windows (later windows start
+    with a space), on the 32k vocabulary (capless windows: lane-mode B/C1) and the toy vocabulary
+    (many atoms are not tokens: the row recurrence), against the C oracle."""
+    rng = np.random.default_rng(23)
+    pool = [chr(c) for c in range(0x20, 0x7F)] * 3 + ["\n", "\t", "\x01", "\x7f", "  ", " \n", "\n "]
+    texts = []
+    for k in range(3000):
+        n = int(rng.integers(0, 900)) if k % 4 else int(rng.integers(200, 320))
+        texts.append("".join(rng.choice(pool, size=n)))
+    texts += ["\n" * 300, " " * 300, "a" * 600, ("ab " * 200), "\t" * 257]
+    text, offs = _csr(texts)
+    for name in ("llama32k", "toy1k"):
+        got = engines[name].encode_csr(text, offs)
+        ref = oracles[name].encode_csr(text, offs)
+        _cmp_csr(got, ref)
+        assert np.array_equal(got[3], ref[3])
