@@ -1413,6 +1413,22 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 obase[g] = a.staging + uni64(SS[g].sb) + uni(SS[g].ntok);
             }
             const unsigned total = pre[NG];
+            // per-slot token range, atom count, first-window flag and staging row, in the slot's
+            // fin[] (dead after C1): a token start reads its slot's record with one LDS load
+            // instead of selecting among NG sets of registers
+            struct C2Slot {
+                uint32_t base, ntk, na, fw;
+                int32_t *ob;
+            };
+            static_assert(sizeof(typename GR::Fin) * GL::NA >= sizeof(C2Slot), "C2Slot fits fin[]");
+            if (lane == 0) {
+#pragma unroll
+                for (int g = 0; g < NG; g++) {
+                    C2Slot &q = *reinterpret_cast<C2Slot *>(&grp(g).fin[0]);
+                    q.base = pre[g]; q.ntk = pre[g + 1] - pre[g]; q.na = na_g[g]; q.fw = (firstmask >> g) & 1u; q.ob = obase[g];
+                }
+            }
+            wave_sync();
             // One token walk per lane; a lane whose token is resolved writes the id and takes the
             // next token (ballot + mbcnt), so each iteration is one trie step for 64 tokens.  A
             // token's bytes do not depend on the trie, so each iteration issues the trie load
@@ -1428,18 +1444,14 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 unsigned g = 0;
 #pragma unroll
                 for (int k = 1; k < NG; k++) g += t >= pre[k] ? 1u : 0u;
-                unsigned base = 0, na = 0, ntk = 0, fw = 0;
-                int32_t *ob = obase[0];
-#pragma unroll
-                for (int k = 0; k < NG; k++)
-                    if (g == (unsigned)k) { base = pre[k]; na = na_g[k]; ntk = pre[k + 1] - pre[k]; fw = (firstmask >> k) & 1u; ob = obase[k]; }
                 T.lbase = g * (unsigned)group_lds_bytes<CH, G>();
                 const GL &L = *reinterpret_cast<const GL *>(smem + T.lbase);
-                const unsigned k = t - base;
+                const C2Slot q = *reinterpret_cast<const C2Slot *>(&L.fin[0]);
+                const unsigned k = t - q.base;
                 T.jj = (unsigned)L.rec[k].smask;
-                T.j1 = k + 1 < ntk ? (unsigned)L.rec[k + 1].smask : na;
-                T.seq = atom_from_info<CH, WIDE>(L.bytes, AInfo<CH>::pack(L.aoff[T.jj], L.atom_len(T.jj), 0, raw && fw && T.jj == 0), raw, T.cnt);
-                T.out = ob + k;
+                T.j1 = k + 1 < q.ntk ? (unsigned)L.rec[k + 1].smask : q.na;
+                T.seq = atom_from_info<CH, WIDE>(L.bytes, AInfo<CH>::pack(L.aoff[T.jj], L.atom_len(T.jj), 0, raw && q.fw && T.jj == 0), raw, T.cnt);
+                T.out = q.ob + k;
                 return T;
             };
 #ifndef C2_WALKS
