@@ -850,56 +850,51 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 if (!ballot(active)) break;
                 const int32_t t = t2 ? (int32_t)t2 : nb + (int32_t)(seq & 0xFFu);
                 const int4 ent = trie_slotA(tv, t);   // buffer load: inactive lanes read harmlessly
-                bool done = false;
-                if (active) {
-                    bool ok;
-                    int32_t nn;
-                    if (t2) {
-                        // root-table entry: .y = node after two bytes (0: none) | first byte exists
-                        // << 30 | first byte ends a token << 31; .x = that node's base word
-                        ok = (ent.y & 0x40000000) && (ent.y & 0x3FFFFFFF);
-                        nn = ent.y & 0x3FFFFFFF;
-                        if (split) {   // atom j ended after the first byte
-                            len = 1;
-                            if ((ent.y & 0x40000000) && ent.y < 0) {
-                                mask = 1;
-                                if constexpr (G == 16) end_token(j + 1, 1);
-                            }
-                        }
-                        t2 = 0;
-                    } else {
-                        seq >>= 8;
-                        cnt--;
-                        ok = ent.y == node;
-                        nn = t;
-                    }
-                    if (!ok) {
-                        done = true;
-                    } else {
-                        node = nn;
-                        nb = ent.x & BASE_MASK;
-                        const bool leaf = (ent.x & LEAF_BIT) != 0;
-                        if (cnt == 0) {   // atom j+len-1 ends: the span j..j+len is a candidate token
-                            len++;
-                            if (ent.x & TERM_BIT) {
-                                if constexpr (G == 16) { if (len == 1) mask = 1u; end_token(j + len, len); }
-                                else mask |= (M)1 << (len - 1);
-                            }
-                            if (leaf || (info & AInfo<CH>::STOP) || len == (unsigned)G) {
-                                done = true;
-                            } else {
-                                const GL &L = *reinterpret_cast<const GL *>(smem + lbase);
-                                info = ainfo_get(L, j + len, false);
-                                seq = atom_from_info<CH, WIDE>(L.bytes, info, raw, cnt);
-                                // the node has no child for the next byte: over without the lookup
-                                done = !((ent.w >> child_bit((unsigned)(seq & 0xFFu))) & 1);
-                            }
-                        } else {
-                            // no token continues inside this atom (leaf, or no child for its next byte)
-                            done = leaf || !((ent.w >> child_bit((unsigned)(seq & 0xFFu))) & 1);
-                        }
-                    }
+                // The step as selects (few exec-mask branches: their scalar bookkeeping costs issue
+                // slots like the vector work does).  Root-table entry (t2): .y = node after two
+                // bytes (0: none) | first byte exists << 30 | first byte ends a token << 31; .x =
+                // that node's base word.  Plain step: the slot is the child iff its check is node.
+                const bool isr = t2 != 0;
+                const bool rsplit = active && isr && split;   // atom j ended after the first byte
+                const bool rtok1 = rsplit && (ent.y & 0x40000000) && ent.y < 0;
+                const bool ok = active && (isr ? ((ent.y & 0x40000000) && (ent.y & 0x3FFFFFFF)) : ent.y == node);
+                len = rsplit ? 1u : len;
+                if constexpr (G == 16) {
+                    mask = rtok1 ? (M)1 : mask;
+                    if (rtok1) end_token(j + 1, 1);
+                } else {
+                    mask = rtok1 ? (M)1 : mask;
                 }
+                seq = isr ? seq : seq >> 8;
+                cnt = isr ? cnt : cnt - 1u;
+                t2 = 0;
+                node = isr ? (ent.y & 0x3FFFFFFF) : t;   // read only while ok
+                nb = ent.x & BASE_MASK;
+                const bool leaf = (ent.x & LEAF_BIT) != 0;
+                const bool aend = ok && cnt == 0;        // atom j+len-1 ends: span j..j+len is a candidate
+                len += aend ? 1u : 0u;
+                const bool term = aend && (ent.x & TERM_BIT);
+                if constexpr (G == 16) {
+                    mask = (term && len == 1) ? (M)1 : mask;
+                    if (term) end_token(j + len, len);
+                } else {
+                    mask |= term ? (M)1 << (len - 1) : (M)0;
+                }
+                const bool cont = aend && !(leaf || (info & AInfo<CH>::STOP) || len == (unsigned)G);
+                {
+                    // the next atom, read by every lane (j + len <= n_atoms: in the window's arrays)
+                    const GL &L = *reinterpret_cast<const GL *>(smem + lbase);
+                    unsigned cn;
+                    const unsigned inf = ainfo_get(L, j + len, false);
+                    const uint64_t sq = atom_from_info<CH, WIDE>(L.bytes, inf, raw, cn);
+                    info = cont ? inf : info;
+                    seq = cont ? sq : seq;
+                    cnt = cont ? cn : cnt;
+                }
+                // the walk ends at a failed lookup, at a leaf or a walk-ending atom, or when the
+                // node has no child for the next byte (over without that lookup)
+                const bool nochild = !((ent.w >> child_bit((unsigned)(seq & 0xFFu))) & 1);
+                const bool done = active && (!ok || (aend ? (!cont || nochild) : (leaf || nochild)));
                 if (done) {
                     GL &L = *reinterpret_cast<GL *>(smem + lbase);
                     if constexpr (G != 16) L.rec[j].smask = mask;   // G = 16: end masks, set by end_token
