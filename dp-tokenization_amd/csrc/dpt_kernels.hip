@@ -751,10 +751,8 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
 #define A0_INFLIGHT 4
 #endif
                         uint32_t *r32 = reinterpret_cast<uint32_t *>(smem + gbase);
-                        auto etok = [&](unsigned e, unsigned ln) {
-                            __hip_atomic_fetch_and(&r32[e], ~(1u << (15u + ln)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        };
                         bool nocap = false;
+                        unsigned tk1 = 0, tk2 = 0;
 #pragma unroll
                         for (int u0 = 0; u0 < 4; u0 += A0_INFLIGHT) {
                         int32_t idx[A0_INFLIGHT];
@@ -762,45 +760,56 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                         for (int uq = 0; uq < A0_INFLIGHT; uq++) {
                             const int u = u0 + uq;
                             const unsigned b = byte_at(u), n1 = byte_at(u + 1);
-                            const bool stop = n1 == END || n1 == ' ';
+                            // (flags as 0/1 integers combined with & and |: short-circuit forms become
+                            // exec-mask branches here)
+                            const unsigned stop = (unsigned)(n1 == END) | (unsigned)(n1 == ' ');
                             const unsigned e1 = n1 == '\n' ? (unsigned)'<' : n1;
                             // a one-byte atom at the word's end: its own slot; else the two-byte root entry
-                            idx[uq] = stop ? tv.root_base + (int32_t)(b & 0xFFu) : (int32_t)(tv.n_slots + ((b & 0xFFu) << 8) + (e1 & 0xFFu));
+                            const int32_t i1 = tv.root_base + (int32_t)(b & 0xFFu);
+                            const int32_t i2 = (int32_t)(tv.n_slots + ((b & 0xFFu) << 8) + (e1 & 0xFFu));
+                            idx[uq] = stop ? i1 : i2;
                         }
                         int4 ent[A0_INFLIGHT];
 #pragma unroll
                         for (int uq = 0; uq < A0_INFLIGHT; uq++) ent[uq] = trie_slotA(tv, idx[uq]);
+                        // Per byte: tk1 bit u = a one-atom token ends at k0+1+u, tk2 bit u = a two-atom
+                        // token ends at k0+2+u (the end masks are written once below)
 #pragma unroll
                         for (int uq = 0; uq < A0_INFLIGHT; uq++) {
                             const int u = u0 + uq;
                             const unsigned k = k0 + (unsigned)u;
-                            const unsigned b = byte_at(u), n1 = byte_at(u + 1);
-                            if (b == END) continue;
-                            if (b == ' ' || b == '\n' || (first && k == 0)) { mark |= 1u << (4 * g + u); continue; }
+                            const unsigned b = byte_at(u), n1 = byte_at(u + 1), n2 = byte_at(u + 2);
                             const int4 e = ent[uq];
-                            if (n1 == END || n1 == ' ') {
-                                // the atom alone is the walk: a root child that ends a token
-                                if (e.y == 0 && (e.x & TERM_BIT)) etok(k + 1u, 1u); else nocap = true;
-                                continue;
-                            }
-                            const bool b0tok = (e.y & 0x40000000) && e.y < 0;
-                            if (b0tok) etok(k + 1u, 1u); else nocap = true;
-                            if (!((e.y & 0x40000000) && (e.y & 0x3FFFFFFF))) continue;   // no node after two bytes
-                            bool more;
-                            if (n1 == '\n') {
-                                // inside atom k+1 = "<0x0A>" after its '<'
-                                more = !(e.x & LEAF_BIT) && ((e.w >> child_bit('0')) & 1);
-                            } else {
-                                // atom k+1 consumed: the span k .. k+2
-                                if (e.x & TERM_BIT) etok(k + 2u, 2u);
-                                const unsigned n2 = byte_at(u + 2);
-                                const unsigned e2 = n2 == '\n' ? (unsigned)'<' : n2;
-                                more = !(e.x & LEAF_BIT) && n2 != END && n2 != ' ' && ((e.w >> child_bit(e2)) & 1);
-                            }
-                            if (more) mark |= 1u << (4 * g + u);
+                            const unsigned valid = (unsigned)(b != END);
+                            const unsigned special = (unsigned)(b == ' ') | (unsigned)(b == '\n') | ((unsigned)first & (unsigned)(k == 0));   // the walker's
+                            const unsigned norm = valid & (special ^ 1u);
+                            // n1 ends the word: the lookup was the atom's own root slot
+                            const unsigned wend = (unsigned)(n1 == END) | (unsigned)(n1 == ' ');
+                            const unsigned y30 = ((unsigned)e.y >> 30) & 1u, y31 = (unsigned)e.y >> 31;
+                            const unsigned xterm = (unsigned)e.x >> 31, xleaf = ((unsigned)e.x >> 30) & 1u;
+                            const unsigned tok1 = wend ? ((unsigned)(e.y == 0) & xterm) : (y30 & y31);
+                            nocap |= (norm & (tok1 ^ 1u)) != 0;
+                            // a node after two bytes: n1 = '\n' leaves the walk inside "<0x0A>" after
+                            // its '<'; otherwise atom k+1 is consumed (the span k .. k+2)
+                            const unsigned has2 = norm & (wend ^ 1u) & y30 & (unsigned)((e.y & 0x3FFFFFFF) != 0);
+                            const unsigned nl1 = (unsigned)(n1 == '\n');
+                            const unsigned e2 = nl1 ? (unsigned)'0' : (n2 == '\n' ? (unsigned)'<' : n2);
+                            const unsigned more = has2 & (xleaf ^ 1u) & (nl1 | ((unsigned)(n2 != END) & (unsigned)(n2 != ' '))) &
+                                                  (((unsigned)e.w >> child_bit(e2)) & 1u);
+                            tk1 |= (norm & tok1) << u;
+                            tk2 |= (has2 & (nl1 ^ 1u) & xterm) << u;
+                            mark |= ((valid & special) | more) << (4 * g + u);
                         }
                         }
-                        if (nocap) SS[g].capb = 1;
+                        // end k0+1+u: tk1 bit u, and tk2 bit u-1 (u = 0: the previous lane's bit 3)
+                        const unsigned t2e = ((tk2 << 1) & 0xEu) | wave_shift_in((tk2 >> 3) & 1u, 0u);
+                        if (ballot((tk1 | t2e) != 0)) {
+#pragma unroll
+                            for (int u = 0; u < 4; u++)
+                                __hip_atomic_fetch_and(&r32[k0 + 1u + (unsigned)u], ~((((tk1 >> u) & 1u) << 16) | (((t2e >> u) & 1u) << 17)),
+                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        }
+                        if (ballot(nocap) && lane == 0) SS[g].capb = 1;
                         // the slot's marked atoms, in order, into its fin[] (free until phase B)
                         const unsigned mg = (mark >> (4 * g)) & 15u;
                         const unsigned c = (unsigned)__builtin_popcount(mg);
