@@ -863,33 +863,33 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 // slots like the vector work does).  Root-table entry (t2): .y = node after two
                 // bytes (0: none) | first byte exists << 30 | first byte ends a token << 31; .x =
                 // that node's base word.  Plain step: the slot is the child iff its check is node.
-                const bool isr = t2 != 0;
-                const bool rsplit = active && isr && split;   // atom j ended after the first byte
-                const bool rtok1 = rsplit && (ent.y & 0x40000000) && ent.y < 0;
-                const bool ok = active && (isr ? ((ent.y & 0x40000000) && (ent.y & 0x3FFFFFFF)) : ent.y == node);
+                // (flags as 0/1 integers: && / || chains become exec-mask branches here)
+                const unsigned act = active ? 1u : 0u;
+                const unsigned isr = (unsigned)(t2 != 0);
+                const unsigned y30 = ((unsigned)ent.y >> 30) & 1u, y31 = (unsigned)ent.y >> 31;
+                const unsigned rsplit = act & isr & (split ? 1u : 0u);   // atom j ended after the first byte
+                const unsigned rtok1 = rsplit & y30 & y31;
+                const unsigned ok = act & (isr ? (y30 & (unsigned)((ent.y & 0x3FFFFFFF) != 0)) : (unsigned)(ent.y == node));
                 len = rsplit ? 1u : len;
-                if constexpr (G == 16) {
-                    mask = rtok1 ? (M)1 : mask;
+                mask = rtok1 ? (M)1 : mask;
+                if constexpr (G == 16)
                     if (rtok1) end_token(j + 1, 1);
-                } else {
-                    mask = rtok1 ? (M)1 : mask;
-                }
                 seq = isr ? seq : seq >> 8;
                 cnt = isr ? cnt : cnt - 1u;
                 t2 = 0;
                 node = isr ? (ent.y & 0x3FFFFFFF) : t;   // read only while ok
                 nb = ent.x & BASE_MASK;
-                const bool leaf = (ent.x & LEAF_BIT) != 0;
-                const bool aend = ok && cnt == 0;        // atom j+len-1 ends: span j..j+len is a candidate
-                len += aend ? 1u : 0u;
-                const bool term = aend && (ent.x & TERM_BIT);
+                const unsigned leaf = ((unsigned)ent.x >> 30) & 1u;
+                const unsigned aend = ok & (unsigned)(cnt == 0);   // atom j+len-1 ends: span j..j+len is a candidate
+                len += aend;
+                const unsigned term = aend & ((unsigned)ent.x >> 31);
                 if constexpr (G == 16) {
-                    mask = (term && len == 1) ? (M)1 : mask;
+                    mask = (term & (unsigned)(len == 1)) ? (M)1 : mask;
                     if (term) end_token(j + len, len);
                 } else {
                     mask |= term ? (M)1 << (len - 1) : (M)0;
                 }
-                const bool cont = aend && !(leaf || (info & AInfo<CH>::STOP) || len == (unsigned)G);
+                const unsigned cont = aend & ((leaf | (unsigned)((info & AInfo<CH>::STOP) != 0) | (unsigned)(len == (unsigned)G)) ^ 1u);
                 {
                     // the next atom, read by every lane (j + len <= n_atoms: in the window's arrays)
                     const GL &L = *reinterpret_cast<const GL *>(smem + lbase);
@@ -902,8 +902,8 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 }
                 // the walk ends at a failed lookup, at a leaf or a walk-ending atom, or when the
                 // node has no child for the next byte (over without that lookup)
-                const bool nochild = !((ent.w >> child_bit((unsigned)(seq & 0xFFu))) & 1);
-                const bool done = active && (!ok || (aend ? (!cont || nochild) : (leaf || nochild)));
+                const unsigned nochild = (((unsigned)ent.w >> child_bit((unsigned)(seq & 0xFFu))) & 1u) ^ 1u;
+                const unsigned done = act & ((ok ^ 1u) | (aend ? ((cont ^ 1u) | nochild) : (leaf | nochild)));
                 if (done) {
                     GL &L = *reinterpret_cast<GL *>(smem + lbase);
                     if constexpr (G != 16) L.rec[j].smask = mask;   // G = 16: end masks, set by end_token
@@ -1453,8 +1453,9 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 const C2Slot q = *reinterpret_cast<const C2Slot *>(&L.fin[0]);
                 const unsigned k = t - q.base;
                 T.jj = (unsigned)L.rec[k].smask;
-                T.j1 = k + 1 < q.ntk ? (unsigned)L.rec[k + 1].smask : q.na;
-                T.seq = atom_from_info<CH, WIDE>(L.bytes, AInfo<CH>::pack(L.aoff[T.jj], L.atom_len(T.jj), 0, raw && q.fw && T.jj == 0), raw, T.cnt);
+                const unsigned nx = (unsigned)L.rec[k + 1].smask;   // k + 1 <= ntk < NA
+                T.j1 = k + 1 < q.ntk ? nx : q.na;
+                T.seq = atom_from_info<CH, WIDE>(L.bytes, AInfo<CH>::pack(L.aoff[T.jj], L.atom_len(T.jj), 0, (raw ? 1u : 0u) & q.fw & (unsigned)(T.jj == 0)), raw, T.cnt);
                 T.out = q.ob + k;
                 return T;
             };
@@ -1493,9 +1494,11 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
 #pragma unroll
                 for (int w = 0; w < NW; w++) {
                     C[w].seq >>= 8;
-                    const bool aend = active[w] && --C[w].cnt == 0;
-                    done[w] = aend && C[w].jj + 1 == C[w].j1;
-                    if (aend && !done[w]) {
+                    C[w].cnt -= 1u;
+                    const unsigned aend = (active[w] ? 1u : 0u) & (unsigned)(C[w].cnt == 0);
+                    const unsigned dn = aend & (unsigned)(C[w].jj + 1 == C[w].j1);
+                    done[w] = dn != 0;
+                    if (aend & (dn ^ 1u)) {
                         C[w].jj++;
                         const GL &L = *reinterpret_cast<const GL *>(smem + C[w].lbase);
                         C[w].seq = atom_from_info<CH, WIDE>(L.bytes, AInfo<CH>::pack(L.aoff[C[w].jj], L.atom_len(C[w].jj), 0, 0), raw, C[w].cnt);
