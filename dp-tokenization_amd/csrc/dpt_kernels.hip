@@ -543,8 +543,11 @@ __device__ bool prep_window(GroupLDS<CH, G> &L, uint8_t *gw, const WinRegs<CH> &
 #endif
 
 // 256-byte 16-lane rows: 6 waves per SIMD by VGPRs (<= 80), so LDS (22 waves per CU) binds
+#ifndef WPE16
+#define WPE16 6
+#endif
 template <int CH, int G, bool BIG, bool WIDE>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CH == 256 && G == 16) ? 6 : 1)))
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CH == 256 && G == 16) ? WPE16 : 1)))
 tokenize_kernel(EncodeArgs a, TrieView tv) {
     constexpr int NG = 64 / G;
     using GL = GroupLDS<CH, G>;

@@ -6,10 +6,11 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 tag=$1; out=gpurun_out/round_$tag; mkdir -p $out
+# traffic first: it rewrites profiles/pmc_traffic.json, which the bench line then reports
+timeout -k 10 600 python3 tools/pmc_traffic.py 1000000 $tag > $out/traffic.log 2>&1 || { tail -20 $out/traffic.log; exit 1; }
 timeout -k 10 400 python -u bench.py > $out/bench.log 2>&1 || { tail -20 $out/bench.log; exit 1; }
 tail -1 $out/bench.log > $out/bench.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 10 --warmup 3 > $out/trace.log 2>&1 || { tail -20 $out/trace.log; exit 1; }
-timeout -k 10 600 python3 tools/pmc_traffic.py 1000000 $tag > $out/traffic.log 2>&1 || { tail -20 $out/traffic.log; exit 1; }
 bash tools/pmc.sh $tag > $out/pmc.log 2>&1 || { tail -20 $out/pmc.log; exit 1; }
 cat $out/bench.json
 find $out/trace -name "*kernel_stats.csv" | head -1 | xargs cat | cut -c1-200 | head -12
