@@ -20,6 +20,7 @@ struct dpt_vocab {
     int32_t *d_ids = nullptr;
     int4 *d_slots4 = nullptr;         // {base | TERM, check, id, 0} for the lane kernel
     int32_t root_base = 0;
+    bool ids16 = false;               // every id in 0..32767: ids are staged as int16 (half the staging traffic)
     dpt_vocab_stats stats{};
 };
 
@@ -27,6 +28,7 @@ struct dpt_ctx {
     int device = 0;
     // workspace
     int32_t *staging = nullptr;
+    int16_t *staging16 = nullptr;     // int16 staging for vocabularies with ids16
     uint4 *rec = nullptr;             // lane kernel backtrace records (cap_bytes entries)
     uint64_t cap_bytes = 0;
     uint64_t *counts = nullptr;
@@ -98,7 +100,11 @@ int ensure_workspace(dpt_ctx *c, uint64_t n_bytes, uint64_t n_str) {
         if (e != hipSuccess) return hip_fail(e, "hipMalloc(staging)");
         e = grow(&c->rec, &cap2, n_bytes);
         if (e != hipSuccess) return hip_fail(e, "hipMalloc(rec)");
+        uint64_t cap3 = c->cap_bytes;
+        e = grow(&c->staging16, &cap3, n_bytes);
+        if (e != hipSuccess) return hip_fail(e, "hipMalloc(staging16)");
         c->cap_bytes = cap1 < cap2 ? cap1 : cap2;
+        c->cap_bytes = c->cap_bytes < cap3 ? c->cap_bytes : cap3;
     }
     if (n_str > c->cap_str || !c->counts) {
         uint64_t cap = c->cap_str, cap2 = c->cap_str;
@@ -226,6 +232,9 @@ int dpt_vocab_create(const uint8_t *utf8_blob, const uint64_t *tok_off, const in
         return hip_fail(e, "vocab upload");
     }
     v->root_base = da.root_base;
+    v->ids16 = true;
+    for (uint32_t t = 0; t < da.n_slots; t++)
+        if (da.check[t] >= 0 && (da.base[t] & (int32_t)0x80000000) && (da.id[t] < 0 || da.id[t] > 32767)) { v->ids16 = false; break; }
     v->stats.n_tokens = da.n_tokens;
     v->stats.n_nodes = da.n_nodes;
     v->stats.n_slots = da.n_slots;
@@ -272,7 +281,7 @@ int dpt_ctx_create(int device, dpt_ctx **out) {
 int dpt_ctx_destroy(dpt_ctx *c) {
     if (!c) return DPT_OK;
     DeviceGuard g(c->device);
-    void *ps[] = {c->staging, c->rec, c->counts, c->retry_list, c->retry_count, c->wsl_scratch, c->scan_temp, c->h_text, c->h_cut,
+    void *ps[] = {c->staging, c->staging16, c->rec, c->counts, c->retry_list, c->retry_count, c->wsl_scratch, c->scan_temp, c->h_text, c->h_cut,
                   c->h_ids, c->h_off, c->h_idoff, c->h_status, c->h_capped, c->h_edges};
     for (void *p : ps)
         if (p) (void)hipFree(p);
@@ -332,6 +341,8 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
     // the lane kernel implements the plain raw / pre-split encode only
     if (p.variant == dpt::KERNEL_LANE && ((mode_flags != DPT_MODE_RAW && mode_flags != DPT_MODE_PRESPLIT) || edges))
         p.variant = v->stats.max_cp <= 16 ? dpt::KERNEL_ROWS16 : dpt::KERNEL_ROWS64;
+    // int16 staging when every id fits (the lane kernel stages int32 only); DPT_WIDE_STAGING=1: A/B only
+    p.staging16 = (v->ids16 && p.variant != dpt::KERNEL_LANE && !getenv("DPT_WIDE_STAGING")) ? c->staging16 : nullptr;
     p.slots = v->d_slots;
     p.slot_ids = v->d_ids;
     p.n_slots = v->stats.n_slots;

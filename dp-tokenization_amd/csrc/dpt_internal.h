@@ -21,6 +21,7 @@ struct EncodeLaunch {
     int32_t *capped;
     // workspace
     int32_t *staging;
+    int16_t *staging16;      // non-null: ids staged as int16 here instead (every vocabulary id in 0..32767)
     uint64_t *counts;
     uint32_t *retry_list;    // 2 x n_str: the 2048-byte pass's list, then (at + n_str) the unbounded pass's list
     uint32_t *retry_count;   // 8 counters: retry count, pass-1 / pass-2 work, long count, long work
@@ -60,6 +61,7 @@ struct LongLaunch {
     const uint64_t *str_off;
     const uint8_t *cut_mask;
     int32_t *staging;
+    int16_t *staging16;      // as EncodeLaunch: the final ids go here when non-null
     uint4 *rec;              // 16 bytes of scratch per input byte
     uint64_t *counts;
     int32_t *status;

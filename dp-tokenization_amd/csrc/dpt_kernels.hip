@@ -265,8 +265,8 @@ __device__ __forceinline__ int4 trie_slot4(const TrieView &tv, int32_t t) {
     return __builtin_bit_cast(int4, __builtin_amdgcn_raw_buffer_load_b128(r, (unsigned)t * 16u, 0, 0));
 }
 
-constexpr int32_t TERM_BIT = (int32_t)0x80000000;
-constexpr int32_t LEAF_BIT = 0x40000000;       // no children: the walk ends here
+[[maybe_unused]] constexpr int32_t TERM_BIT = (int32_t)0x80000000;
+[[maybe_unused]] constexpr int32_t LEAF_BIT = 0x40000000;  // no children (dpt_long.hip ends walks on it; this kernel uses the child filters)
 constexpr int32_t BASE_MASK = 0x3FFFFFFF;
 
 // ------------------------------------------------------------------ arguments
@@ -277,6 +277,7 @@ struct EncodeArgs {
     const uint8_t *cut_mask;    // PRESPLIT / ATOMS only
     uint64_t n_str;
     int32_t *staging;           // ids staged at (str_off[s]-str_off[0]) + k
+    int16_t *staging16;         // non-null: the ids are staged here as int16 instead (half the bytes)
     uint64_t *counts;           // per string
     int32_t *status;
     int32_t *capped;            // nullable
@@ -1408,7 +1409,9 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
 #endif
         {
             unsigned pre[NG + 1], na_g[NG];
-            int32_t *obase[NG];       // staging row of the window's first token, per slot
+            uint8_t *obase[NG];       // staging row of the window's first token, per slot
+            const bool n16 = a.staging16 != nullptr;   // int16 staging (uniform)
+            const unsigned esh = n16 ? 1u : 2u;
             unsigned firstmask = 0;   // groups whose window starts the string (raw '▁' + first atom)
             pre[0] = 0;
 #pragma unroll
@@ -1417,7 +1420,8 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 pre[g + 1] = pre[g] + (gv ? uni(SS[g].wtok) : 0u);
                 na_g[g] = uni(SS[g].n_atoms);
                 firstmask |= (uni64(SS[g].pos) == 0 ? 1u : 0u) << g;
-                obase[g] = a.staging + uni64(SS[g].sb) + uni(SS[g].ntok);
+                const uint64_t e0 = uni64(SS[g].sb) + uni(SS[g].ntok);
+                obase[g] = n16 ? reinterpret_cast<uint8_t *>(a.staging16 + e0) : reinterpret_cast<uint8_t *>(a.staging + e0);
             }
             const unsigned total = pre[NG];
             // per-slot token range, atom count, first-window flag and staging row, in the slot's
@@ -1425,7 +1429,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
             // instead of selecting among NG sets of registers
             struct C2Slot {
                 uint32_t base, ntk, na, fw;
-                int32_t *ob;
+                uint8_t *ob;
             };
             static_assert(sizeof(typename GR::Fin) * GL::NA >= sizeof(C2Slot), "C2Slot fits fin[]");
             if (lane == 0) {
@@ -1444,7 +1448,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
             struct Tok {
                 unsigned jj, j1, cnt, lbase;
                 uint64_t seq;
-                int32_t *out;
+                uint8_t *out;
             };
             auto tstart = [&](unsigned t) -> Tok {
                 Tok T;
@@ -1459,7 +1463,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 const unsigned nx = (unsigned)L.rec[k + 1].smask;   // k + 1 <= ntk < NA
                 T.j1 = k + 1 < q.ntk ? nx : q.na;
                 T.seq = atom_from_info<CH, WIDE>(L.bytes, AInfo<CH>::pack(L.aoff[T.jj], L.atom_len(T.jj), 0, (raw ? 1u : 0u) & q.fw & (unsigned)(T.jj == 0)), raw, T.cnt);
-                T.out = q.ob + k;
+                T.out = q.ob + (k << esh);
                 return T;
             };
 #ifndef C2_WALKS
@@ -1515,7 +1519,9 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                     nb[w] = ent[w].x & BASE_MASK;
                     const uint64_t dm = ballot(done[w]);
                     if (done[w]) {
-                        *C[w].out = ok[w] ? ent[w].z : -1;   // the id arrives with the token's last node
+                        const int32_t idv = ok[w] ? ent[w].z : -1;   // the id arrives with the token's last node
+                        if (n16) *reinterpret_cast<int16_t *>(C[w].out) = (int16_t)idv;
+                        else *reinterpret_cast<int32_t *>(C[w].out) = idv;
                         const unsigned uu = nxt + __builtin_amdgcn_mbcnt_hi((unsigned)(dm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)dm, 0u));
                         active[w] = uu < total;
                         if (active[w]) C[w] = tstart(uu);
@@ -1563,7 +1569,8 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
 
 // One wave per 64 consecutive strings: their offsets arrive in one coalesced load per lane,
 // then the wave copies string after string with up to 256 ids (4 loads per lane) in flight.
-__global__ void __launch_bounds__(256) compact_kernel(const int32_t *__restrict__ staging, const uint64_t *__restrict__ str_off,
+template <typename ST>   // int32_t, or int16_t when every id fits (sign-extended: -1 stays -1)
+__global__ void __launch_bounds__(256) compact_kernel(const ST *__restrict__ staging, const uint64_t *__restrict__ str_off,
                                                       const uint64_t *__restrict__ id_off, uint64_t n_str,
                                                       int32_t *__restrict__ ids) {
     const uint64_t base_off = str_off[0];
@@ -1587,7 +1594,7 @@ __global__ void __launch_bounds__(256) compact_kernel(const int32_t *__restrict_
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     const unsigned k = k0 + q * 64 + lane;
-                    v[q] = k < nn ? staging[so + k] : 0;
+                    v[q] = k < nn ? (int32_t)staging[so + k] : 0;
                 }
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
@@ -1666,7 +1673,7 @@ static void launch_tok(const EncodeArgs &a, const TrieView &tv, uint64_t n_units
 hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t ev[6]) {
     EncodeArgs a;
     a.text = p.text; a.str_off = p.str_off; a.cut_mask = p.cut_mask; a.n_str = p.n_str;
-    a.staging = p.staging; a.counts = p.counts; a.status = p.status; a.capped = p.capped;
+    a.staging = p.staging; a.staging16 = p.staging16; a.counts = p.counts; a.status = p.status; a.capped = p.capped;
     a.retry_list = p.retry_list; a.retry_count = p.retry_count; a.work_list = nullptr; a.work_count = nullptr;
     a.long_list = p.retry_list + p.n_str; a.long_count = p.retry_count + 3;
     a.mode = p.mode;
@@ -1707,7 +1714,7 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
         // its waves read a zero count and exit)
         LongLaunch l;
         l.mode = p.mode; l.text = p.text; l.str_off = p.str_off; l.cut_mask = p.cut_mask;
-        l.staging = p.staging; l.rec = p.rec; l.counts = p.counts; l.status = p.status; l.capped = p.capped;
+        l.staging = p.staging; l.staging16 = p.staging16; l.rec = p.rec; l.counts = p.counts; l.status = p.status; l.capped = p.capped;
         l.edges = p.edges; l.list = a.long_list; l.list_count = a.long_count; l.work_next = p.retry_count + 4;
         l.slots = p.slots; l.slots4 = p.slots4; l.n_slots = p.n_slots; l.root_base = p.root_base;
         l.max_tok_bytes = p.max_tok_bytes; l.long_span = p.long_span;
@@ -1731,7 +1738,10 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     if (p.n_str > 0) {
         uint64_t blocks = (p.n_str + 255) / 256;   // 4 waves x 64 strings
         if (blocks > 4096) blocks = 4096;
-        hipLaunchKernelGGL(compact_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, p.staging, p.str_off, p.id_off, p.n_str, p.ids);
+        if (p.staging16)
+            hipLaunchKernelGGL(compact_kernel<int16_t>, dim3((unsigned)blocks), dim3(256), 0, stream, p.staging16, p.str_off, p.id_off, p.n_str, p.ids);
+        else
+            hipLaunchKernelGGL(compact_kernel<int32_t>, dim3((unsigned)blocks), dim3(256), 0, stream, p.staging, p.str_off, p.id_off, p.n_str, p.ids);
     }
     if (ev) {
         const hipError_t er = hipEventRecord(ev[3], stream);

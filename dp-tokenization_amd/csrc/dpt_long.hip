@@ -102,6 +102,7 @@ struct Args {
     const uint64_t *str_off;
     const uint8_t *cut_mask;
     int32_t *staging;
+    int16_t *staging16;   // non-null: the final ids go here as int16 (staging stays the scratch)
     uint4 *rec;
     uint64_t *counts;
     int32_t *status;
@@ -479,7 +480,10 @@ __global__ void __launch_bounds__(64) long_kernel(Args a) {
                     }
                 }
                 phase_sync();
-                if (in) S.stg[k] = ok ? id : -1;
+                if (in) {
+                    if (a.staging16) a.staging16[sb + k] = (int16_t)(ok ? id : -1);
+                    else S.stg[k] = ok ? id : -1;
+                }
             }
         }
         if (lane == 0) {
@@ -496,7 +500,7 @@ __global__ void __launch_bounds__(64) long_kernel(Args a) {
 void launch_long(const LongLaunch &p, hipStream_t stream) {
     lng::Args a;
     a.text = p.text; a.str_off = p.str_off; a.cut_mask = p.cut_mask;
-    a.staging = p.staging; a.rec = p.rec; a.counts = p.counts; a.status = p.status; a.capped = p.capped;
+    a.staging = p.staging; a.staging16 = p.staging16; a.rec = p.rec; a.counts = p.counts; a.status = p.status; a.capped = p.capped;
     a.edges = p.edges; a.list = p.list; a.list_count = p.list_count; a.work_next = p.work_next;
     a.slots = p.slots; a.slots4 = p.slots4; a.n_slots = p.n_slots; a.root_base = p.root_base;
     a.max_tok_bytes = p.max_tok_bytes; a.long_span = p.long_span; a.mode = p.mode;

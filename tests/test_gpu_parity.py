@@ -341,3 +341,27 @@ def test_ascii_windows_phase_a0(engines, oracles):
         ref = oracles[name].encode_csr(text, offs)
         _cmp_csr(got, ref)
         assert np.array_equal(got[3], ref[3])
+
+
+@pytest.mark.parametrize("shift", [40000, "edge"])
+def test_staging_width_by_id_range(shift, vocabs):
+    """Ids are staged as int16 when every id is in 0..32767 (the llama-shaped vocabularies) and as
+    int32 otherwise: the same corpus through both widths -- windowed passes and the unbounded pass
+    (3000-byte words) -- against the C oracle with the same ids."""
+    from dptok import Encoder, Vocab, synth
+    from oracle import oracle
+    base = vocabs["llama32k"]
+    if shift == "edge":   # the largest id is exactly 32767: still int16
+        top = max(base.values())
+        t2i = {t: i + (32767 - top) for t, i in base.items()}
+    else:
+        t2i = {t: i + shift for t, i in base.items()}
+    rng = np.random.default_rng(17)
+    texts = [synth.unpack(*synth.random_ascii_corpus(1, 256, seed=100 + k))[0] for k in range(64)]
+    texts += ["".join(chr(c) for c in rng.integers(97, 123, size=3000)) for _ in range(8)]
+    texts += ["", " ", "\n\n", "a"]
+    text, offs = _csr(texts)
+    got = Encoder(Vocab(t2i, 0)).encode_csr(text, offs)
+    ref = oracle.OracleVocab(t2i).encode_csr(text, offs)
+    _cmp_csr(got, ref)
+    assert int(got[0].max()) > 32767 if shift != "edge" else int(got[0].max()) <= 32767
