@@ -1606,6 +1606,56 @@ __global__ void __launch_bounds__(256) compact_kernel(const ST *__restrict__ sta
     }
 }
 
+// Flat compaction: one wave (block) per 64 consecutive strings, lanes over the batch's OUTPUT
+// ids (contiguous in ids[]: every store is a coalesced row), each lane tracking the string its
+// id falls in (offsets in LDS; strings usually hold more than 64 ids, so the string index
+// advances at most once per step), COMPACT_U independent loads in flight per lane -- no
+// per-string round trip.
+#ifndef COMPACT_U
+#define COMPACT_U 8
+#endif
+template <typename ST>
+__global__ void __launch_bounds__(64) compact_flat_kernel(const ST *__restrict__ staging, const uint64_t *__restrict__ str_off,
+                                                          const uint64_t *__restrict__ id_off, uint64_t n_str,
+                                                          int32_t *__restrict__ ids) {
+    __shared__ uint64_t s_rel[65];   // id_off of the batch's strings - id_off of its first, + end
+    __shared__ uint64_t s_src[64];   // staging element of each string's first id
+    const uint64_t base_off = str_off[0];
+    const unsigned lane = threadIdx.x;
+    const uint64_t n_batches = (n_str + 63) / 64;
+    for (uint64_t bt = blockIdx.x; bt < n_batches; bt += gridDim.x) {
+        const uint64_t s0 = bt * 64;
+        const unsigned cnt = (unsigned)min((uint64_t)64, n_str - s0);
+        const uint64_t o0 = uni64(id_off[s0]);
+        if (lane < cnt) {
+            s_rel[lane] = id_off[s0 + lane] - o0;
+            s_src[lane] = str_off[s0 + lane] - base_off;
+        }
+        if (lane == 0) s_rel[cnt] = id_off[s0 + cnt] - o0;
+        wave_sync();
+        const uint64_t total = s_rel[cnt];
+        unsigned j = 0;   // the string of this lane's current id (monotone in t)
+        for (uint64_t t0 = 0; t0 < total; t0 += 64u * COMPACT_U) {
+            int32_t v[COMPACT_U];
+#pragma unroll
+            for (int u = 0; u < COMPACT_U; u++) {
+                const uint64_t t = t0 + (uint64_t)u * 64u + lane;
+                v[u] = 0;
+                if (t < total) {
+                    while (s_rel[j + 1] <= t) j++;
+                    v[u] = (int32_t)staging[s_src[j] + (t - s_rel[j])];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < COMPACT_U; u++) {
+                const uint64_t t = t0 + (uint64_t)u * 64u + lane;
+                if (t < total) ids[o0 + t] = v[u];
+            }
+        }
+        wave_sync();   // s_rel / s_src are rewritten by the next batch
+    }
+}
+
 __global__ void zero_first(uint64_t *p, uint32_t *rc) {
     if (threadIdx.x < 8) rc[threadIdx.x] = 0;   // retry count, pass-1 / pass-2 work, long count, long work
     if (threadIdx.x == 0) p[0] = 0;
@@ -1738,7 +1788,15 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     if (p.n_str > 0) {
         uint64_t blocks = (p.n_str + 255) / 256;   // 4 waves x 64 strings
         if (blocks > 4096) blocks = 4096;
-        if (p.staging16)
+        static const bool flat = !getenv("DPT_COMPACT_OLD");   // A/B only
+        if (flat) {
+            uint64_t fb = (p.n_str + 63) / 64;
+            if (fb > (uint64_t)p.max_blocks / 2) fb = p.max_blocks / 2;   // 32 waves per CU
+            if (p.staging16)
+                hipLaunchKernelGGL(compact_flat_kernel<int16_t>, dim3((unsigned)fb), dim3(64), 0, stream, p.staging16, p.str_off, p.id_off, p.n_str, p.ids);
+            else
+                hipLaunchKernelGGL(compact_flat_kernel<int32_t>, dim3((unsigned)fb), dim3(64), 0, stream, p.staging, p.str_off, p.id_off, p.n_str, p.ids);
+        } else if (p.staging16)
             hipLaunchKernelGGL(compact_kernel<int16_t>, dim3((unsigned)blocks), dim3(256), 0, stream, p.staging16, p.str_off, p.id_off, p.n_str, p.ids);
         else
             hipLaunchKernelGGL(compact_kernel<int32_t>, dim3((unsigned)blocks), dim3(256), 0, stream, p.staging, p.str_off, p.id_off, p.n_str, p.ids);

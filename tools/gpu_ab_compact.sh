@@ -1,10 +1,7 @@
 #!/bin/bash
-# smoke, GPU parity tests, then an env A/B of the staging width and one default bench line
+# A/B of the compaction kernels: flat U=8 default, flat with 16-byte stores (U = 1, 2, 4)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && \
-timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 240 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 && \
-bash tools/gpu_ab_env.sh "narrow=" "wide=DPT_WIDE_STAGING=1" "narrow2=" "wide2=DPT_WIDE_STAGING=1" > gpurun_out/ab.log 2>&1 && \
-timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/bench_fullexact.log 2>&1
-rc=$?; tail -3 gpurun_out/pytest_gpu.log; cat gpurun_out/ab.log; tail -1 gpurun_out/bench_fullexact.log | cut -c1-300; exit $rc
+bash tools/ab_libs.sh dp-tokenization_amd/dptok/libdpt.so dp-tokenization_amd/csrc/build/var_v4u1/libdpt.so dp-tokenization_amd/csrc/build/var_v4u2/libdpt.so dp-tokenization_amd/csrc/build/var_v4u4/libdpt.so dp-tokenization_amd/dptok/libdpt.so > gpurun_out/ab.log 2>&1
+rc=$?; cat gpurun_out/ab.log; exit $rc
