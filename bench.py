@@ -211,7 +211,9 @@ def main():
 
     # roofline of the dominant kernel (tokenize): algorithmic bytes per launch
     k_ms = ms_stage[0] / max(launches, 1)
-    alg_bytes = n_bytes + 8 * (M + 1) + 4 * n_tok_rank + 8 * M + 4 * M
+    # staged ids are int16 when every vocabulary id is in 0..32767 (dpt_api.cpp ids16), else int32
+    id_bytes = 2 if 0 <= min(t2i.values()) and max(t2i.values()) <= 32767 else 4
+    alg_bytes = n_bytes + 8 * (M + 1) + id_bytes * n_tok_rank + 8 * M + 4 * M
     achieved = alg_bytes / (k_ms * 1e-3) / 1e9
 
     # exact match vs the CPU DP (C oracle) and the CPU baseline -- rank 0 only
@@ -274,7 +276,8 @@ def main():
                                   "compact": ms_stage[2] / max(launches, 1)},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic_for(M, Lb) if args.workload == "cfg2" else None,
-                         "kernel": "tokenize_kernel<256,16,false,false>", "alg_bytes_per_launch": alg_bytes},
+                         "kernel": "tokenize_kernel<256,16,false,false>", "alg_bytes_per_launch": alg_bytes,
+                         "staged_id_bytes": id_bytes},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -547,7 +547,7 @@ __device__ bool prep_window(GroupLDS<CH, G> &L, uint8_t *gw, const WinRegs<CH> &
 #ifndef WPE16
 #define WPE16 6
 #endif
-template <int CH, int G, bool BIG, bool WIDE>
+template <int CH, int G, bool BIG, bool WIDE, int SW = 0>   // SW: staged id width 0 = by a.staging16, 1 = int16, 2 = int32
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CH == 256 && G == 16) ? WPE16 : 1)))
 tokenize_kernel(EncodeArgs a, TrieView tv) {
     constexpr int NG = 64 / G;
@@ -1410,7 +1410,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
         {
             unsigned pre[NG + 1], na_g[NG];
             uint8_t *obase[NG];       // staging row of the window's first token, per slot
-            const bool n16 = a.staging16 != nullptr;   // int16 staging (uniform)
+            const bool n16 = SW == 1 || (SW == 0 && a.staging16 != nullptr);   // int16 staging (uniform)
             const unsigned esh = n16 ? 1u : 2u;
             unsigned firstmask = 0;   // groups whose window starts the string (raw '▁' + first atom)
             pre[0] = 0;
@@ -1695,12 +1695,12 @@ static_assert(block_lds_bytes<SMALL_CH, 64>() <= 64 * 1024, "small LDS");
 static_assert(block_lds_bytes<BIG_CH, 64>() <= 160 * 1024, "big LDS");
 
 // Resident waves per CU for an instantiation (LDS / VGPR limited); DPT_WAVES_PER_CU overrides.
-template <int CH, int G, bool BIG, bool WIDE>
+template <int CH, int G, bool BIG, bool WIDE, int SW = 0>
 static unsigned resident_per_cu() {
     static unsigned cached = 0;
     if (cached) return cached;
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, tokenize_kernel<CH, G, BIG, WIDE>, 64, block_lds_bytes<CH, G>()) != hipSuccess || nb <= 0)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, tokenize_kernel<CH, G, BIG, WIDE, SW>, 64, block_lds_bytes<CH, G>()) != hipSuccess || nb <= 0)
         nb = 8;
     if (const char *e = getenv("DPT_WAVES_PER_CU")) {
         const int v = atoi(e);
@@ -1711,13 +1711,13 @@ static unsigned resident_per_cu() {
 }
 
 // Persistent grid: every resident wave pulls strings from the work counter until it runs dry.
-template <int CH, int G, bool BIG, bool WIDE>
+template <int CH, int G, bool BIG, bool WIDE, int SW = 0>
 static void launch_tok(const EncodeArgs &a, const TrieView &tv, uint64_t n_units, unsigned n_cu, hipStream_t stream) {
     constexpr int lds = block_lds_bytes<CH, G>();
-    uint64_t blocks = (uint64_t)n_cu * resident_per_cu<CH, G, BIG, WIDE>();
+    uint64_t blocks = (uint64_t)n_cu * resident_per_cu<CH, G, BIG, WIDE, SW>();
     if (blocks > (uint64_t)n_cu * 64u) blocks = (uint64_t)n_cu * 64u;   // the scratch is sized for 64 per CU
     if (blocks > n_units) blocks = n_units ? n_units : 1;
-    hipLaunchKernelGGL((tokenize_kernel<CH, G, BIG, WIDE>), dim3((unsigned)blocks), dim3(64), lds, stream, a, tv);
+    hipLaunchKernelGGL((tokenize_kernel<CH, G, BIG, WIDE, SW>), dim3((unsigned)blocks), dim3(64), lds, stream, a, tv);
 }
 
 hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t ev[6]) {
@@ -1747,8 +1747,15 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
         } else {
             const unsigned n_cu = p.max_blocks / 64;
             if (p.variant == KERNEL_ROWS16) {
-                if (wide) launch_tok<SMALL_CH, 16, false, true>(a, tv, (p.n_str + 3) / 4, n_cu, stream);
-                else launch_tok<SMALL_CH, 16, false, false>(a, tv, (p.n_str + 3) / 4, n_cu, stream);
+                // the hot kernel gets the staged id width as a template constant
+                const uint64_t nu = (p.n_str + 3) / 4;
+                if (wide) {
+                    if (p.staging16) launch_tok<SMALL_CH, 16, false, true, 1>(a, tv, nu, n_cu, stream);
+                    else launch_tok<SMALL_CH, 16, false, true, 2>(a, tv, nu, n_cu, stream);
+                } else {
+                    if (p.staging16) launch_tok<SMALL_CH, 16, false, false, 1>(a, tv, nu, n_cu, stream);
+                    else launch_tok<SMALL_CH, 16, false, false, 2>(a, tv, nu, n_cu, stream);
+                }
             } else {
                 if (wide) launch_tok<SMALL_CH, 64, false, true>(a, tv, p.n_str, n_cu, stream);
                 else launch_tok<SMALL_CH, 64, false, false>(a, tv, p.n_str, n_cu, stream);
