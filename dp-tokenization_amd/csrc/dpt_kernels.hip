@@ -1663,20 +1663,45 @@ __global__ void zero_first(uint64_t *p, uint32_t *rc) {
 
 // ------------------------------------------------------------------ histogram
 
+// Token-count histogram: LDS-privatised int64 bins.  Strings of one corpus have similar token
+// counts, so per-lane LDS atomics would pile onto a few bins (and every lane onto status 0):
+// each wave instead peels off one distinct bin per round (readfirstlane + ballot) and adds its
+// lane count once; statuses are counted with one ballot per value.
 __global__ void __launch_bounds__(256) hist_kernel(const uint64_t *__restrict__ id_off, const int32_t *__restrict__ status,
                                                    uint64_t n_str, unsigned long long *hist, uint32_t n_bins) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long lh[];
     const uint32_t nb = n_bins + 8;
     for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) lh[b] = 0;
     __syncthreads();
+    const unsigned lane = threadIdx.x & 63u;
     unsigned long long tok = 0;
-    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n_str; s += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t n = id_off[s + 1] - id_off[s];
-        tok += n;
-        const uint32_t bin = n < n_bins - 1 ? (uint32_t)n : n_bins - 1;
-        atomicAdd(&lh[bin], 1ull);
-        const int32_t st = status[s];
-        atomicAdd(&lh[n_bins + 2 + (st >= 0 && st <= 4 ? st : 4)], 1ull);
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    // every lane of a wave runs the same number of rounds (ballots over the whole wave)
+    const uint64_t s_first = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u);
+    for (uint64_t s0 = s_first; s0 < n_str; s0 += stride) {
+        const uint64_t s = s0 + lane;
+        const bool in = s < n_str;
+        uint32_t bin = 0xFFFFFFFFu;
+        int32_t st = -1;
+        if (in) {
+            const uint64_t n = id_off[s + 1] - id_off[s];
+            tok += n;
+            bin = n < n_bins - 1 ? (uint32_t)n : n_bins - 1;
+            st = status[s];
+            st = st >= 0 && st <= 4 ? st : 4;
+        }
+        uint64_t left = __ballot(in);
+        while (left) {
+            const uint32_t b0 = __builtin_amdgcn_readlane(bin, (unsigned)__builtin_ctzll(left));
+            const uint64_t same = __ballot(bin == b0) & left;
+            if (lane == (unsigned)__builtin_ctzll(left)) atomicAdd(&lh[b0], (unsigned long long)__builtin_popcountll(same));
+            left &= ~same;
+        }
+#pragma unroll
+        for (int v = 0; v < 5; v++) {
+            const uint64_t m = __ballot(st == v);
+            if (lane == 0 && m) atomicAdd(&lh[n_bins + 2 + v], (unsigned long long)__builtin_popcountll(m));
+        }
     }
     atomicAdd(&lh[n_bins], tok);
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&lh[n_bins + 1], (unsigned long long)n_str);

@@ -365,3 +365,35 @@ def test_staging_width_by_id_range(shift, vocabs):
     ref = oracle.OracleVocab(t2i).encode_csr(text, offs)
     _cmp_csr(got, ref)
     assert int(got[0].max()) > 32767 if shift != "edge" else int(got[0].max()) <= 32767
+
+
+def test_histogram_statuses_and_overflow(engines, oracles):
+    """Histogram bins with mixed statuses (empty strings: status 2) and an overflow bin (n_bins 16:
+    every count >= 15 lands in bin 15), 70 001 strings (not a multiple of the block size)."""
+    torch = pytest.importorskip("torch")
+    from dptok import synth
+    rng = np.random.default_rng(5)
+    texts = synth.unpack(*synth.random_ascii_corpus(70001, 24, seed=23))
+    for k in rng.choice(len(texts), 3000, replace=False):
+        texts[k] = "" if k % 2 else texts[k][: int(k) % 7]
+    text, offs = _csr(texts)
+    n, nb = len(texts), 16
+    enc = engines["llama32k"]
+    dt = torch.from_numpy(np.array(text)).cuda()
+    do = torch.from_numpy(offs.view(np.int64)).cuda()
+    ids = torch.empty(max(len(text), 1), dtype=torch.int32, device="cuda")
+    id_off = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    st = torch.empty(n, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    enc.encode_device(dt.data_ptr(), len(text), do.data_ptr(), n, ids.data_ptr(), len(text), id_off.data_ptr(),
+                      st.data_ptr(), stream=s)
+    hist = torch.zeros(nb + 8, dtype=torch.int64, device="cuda")
+    enc.histogram_device(id_off.data_ptr(), st.data_ptr(), n, hist.data_ptr(), nb, stream=s)
+    torch.cuda.synchronize()
+    _, roff, rst, _ = oracles["llama32k"].encode_csr(text, offs)
+    h = hist.cpu().numpy()
+    counts = np.diff(roff.astype(np.int64))
+    assert np.array_equal(h[:nb], np.bincount(np.minimum(counts, nb - 1), minlength=nb))
+    assert h[nb] == counts.sum() and h[nb + 1] == n
+    assert np.array_equal(h[nb + 2: nb + 7], np.bincount(np.clip(rst, 0, 4), minlength=5))
+    assert h[nb + 4] > 0   # empty strings were counted under status 2
