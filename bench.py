@@ -276,7 +276,7 @@ def main():
                                   "compact": ms_stage[2] / max(launches, 1)},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic_for(M, Lb) if args.workload == "cfg2" else None,
-                         "kernel": "tokenize_kernel<256,16,false,false>", "alg_bytes_per_launch": alg_bytes,
+                         "kernel": "tokenize_kernel<256,16,false,false,1>" if id_bytes == 2 else "tokenize_kernel<256,16,false,false,2>", "alg_bytes_per_launch": alg_bytes,
                          "staged_id_bytes": id_bytes},
             "cpu_baseline": cpu,
         }
