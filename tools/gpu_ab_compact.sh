@@ -1,7 +1,10 @@
 #!/bin/bash
-# A/B of the compaction kernels: flat U=8 default, flat with 16-byte stores (U = 1, 2, 4)
+# A/B of the compaction kernels on cfg2 and cfg5: the flat kernel (default) and the per-string
+# kernel (DPT_COMPACT_OLD=1); stage times in each line
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-export TMPDIR=/tmp
 mkdir -p gpurun_out
-bash tools/ab_libs.sh dp-tokenization_amd/dptok/libdpt.so dp-tokenization_amd/csrc/build/var_v4u1/libdpt.so dp-tokenization_amd/csrc/build/var_v4u2/libdpt.so dp-tokenization_amd/csrc/build/var_v4u4/libdpt.so dp-tokenization_amd/dptok/libdpt.so > gpurun_out/ab.log 2>&1
-rc=$?; cat gpurun_out/ab.log; exit $rc
+L=dp-tokenization_amd/dptok/libdpt.so
+for wl in cfg2 cfg5; do
+  bash tools/ab_libs_wl.sh $wl $L || exit 1
+  DPT_COMPACT_OLD=1 bash tools/ab_libs_wl.sh $wl $L | sed 's/^/old: /' || exit 1
+done
