@@ -298,6 +298,13 @@ struct EncodeArgs {
 // diagnostic build only: lane-mode chunk values of string 0's first window
 __device__ unsigned g_lanedbg[16 * 16 + 4];
 #endif
+// A/B only: per-phase issue priority (PRIO_MODE 1: A and C2 -- the trie-walk phases -- at
+// priority 1; 2: B at priority 1; 0: none)
+#ifndef PRIO_MODE
+#define PRIO_MODE 0
+#endif
+#define PRIO_PHASE(k) do { if (PRIO_MODE == 1) __builtin_amdgcn_s_setprio((k) == 0 || (k) == 3 ? 1 : 0); \
+                           if (PRIO_MODE == 2) __builtin_amdgcn_s_setprio((k) == 1 ? 1 : 0); } while (0)
 #ifdef DPT_STAMPS
 // diagnostic build only: cycles per phase summed over waves (never in the product build)
 __device__ unsigned long long g_stamps[8];
@@ -659,6 +666,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
         wave_sync();
         if (busy == 0) break;
         STAMP(0);
+        PRIO_PHASE(0);
 
         // ---------------------------------------------------------- A: match discovery (all slots)
 #if DPT_DOUBLE == 1
@@ -921,6 +929,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
 #endif
         wave_sync();
         STAMP(1);
+        PRIO_PHASE(1);
 
         // ---------------------------------------------------------- B: forward recurrence
         bool lane_mode = false;   // B ran per chunk and did C0 and C1 itself (G = 16, capless, no edges)
@@ -1297,6 +1306,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
         }
         wave_sync();
         STAMP(2);
+        PRIO_PHASE(2);
 
         // ---------------------------------------------------------- C0: per-window token counts and validity
         // (word w ends at atom word_end(w); its final state is in fin[word_end(w)])
@@ -1401,6 +1411,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
 #endif
         wave_sync();
         STAMP(3);
+        PRIO_PHASE(3);
 
         // ---------------------------------------------------------- C2: ids (lanes over all slots' tokens)
 #if DPT_DOUBLE == 4
@@ -1561,6 +1572,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
         }
         wave_sync();
         STAMP(4);
+        PRIO_PHASE(4);
     }
     STAMP_FLUSH;
 }
