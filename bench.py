@@ -55,6 +55,27 @@ def parse():
     return ap.parse_args()
 
 
+def exact_matches(ids_h, off_h, st_h, rids, roff, rst, S: int) -> int:
+    """Strings among the first S whose ids and status equal the oracle's (CSR on both sides)."""
+    off_h = np.asarray(off_h, dtype=np.uint64)
+    roff = np.asarray(roff, dtype=np.uint64)
+    if np.array_equal(off_h[: S + 1] - off_h[0], roff[: S + 1] - roff[0]):
+        # every count agrees: one vectorised compare, mismatching ids mapped back to strings
+        n_id = int(roff[S] - roff[0])
+        a0, b0 = int(off_h[0]), int(roff[0])
+        diff = np.nonzero(ids_h[a0:a0 + n_id] != rids[b0:b0 + n_id])[0]
+        bad = np.zeros(S, dtype=bool)
+        bad[np.searchsorted(roff[: S + 1] - roff[0], diff.astype(np.uint64), side="right") - 1] = True
+        bad |= st_h[:S] != rst[:S]
+        return int(S - bad.sum())
+    same = 0
+    for i in range(S):
+        a = ids_h[int(off_h[i]):int(off_h[i + 1])]
+        b = rids[int(roff[i]):int(roff[i + 1])]
+        same += int(st_h[i] == rst[i] and np.array_equal(a, b))
+    return same
+
+
 # ------------------------------------------------------------------ CPU baseline (port of the reference)
 _PORT = {}
 
@@ -227,21 +248,7 @@ def main():
         ov = oracle.OracleVocab(t2i)
         sub_off = offs[: S + 1]
         rids, roff, rst, _ = ov.encode_csr(text, sub_off, nthreads=cores)
-        roff = np.asarray(roff, dtype=np.uint64)
-        if np.array_equal(off_h[: S + 1] - off_h[0], roff[: S + 1] - roff[0]):
-            # every count agrees: one vectorised compare, mismatching ids mapped back to strings
-            n_id = int(roff[S] - roff[0])
-            diff = np.nonzero(ids_h[int(off_h[0]):int(off_h[0]) + n_id] != rids[int(roff[0]):int(roff[0]) + n_id])[0]
-            bad = np.zeros(S, dtype=bool)
-            bad[np.searchsorted(roff[: S + 1] - roff[0], diff.astype(np.uint64), side="right") - 1] = True
-            bad |= st_h[:S] != rst[:S]
-            same = int(S - bad.sum())
-        else:
-            same = 0
-            for i in range(S):
-                a = ids_h[int(off_h[i]):int(off_h[i + 1])]
-                b = rids[int(roff[i]):int(roff[i + 1])]
-                same += int(st_h[i] == rst[i] and np.array_equal(a, b))
+        same = exact_matches(ids_h, off_h, st_h, rids, roff, rst, S)
         exact = {"rate": same / S, "sample": S, "checker": "oracle/dp_oracle.c"}
         if cpu is not None:
             t0c = time.perf_counter()

@@ -1,0 +1,49 @@
+"""Host logic of bench.py: the exact-match count (vectorised path and per-string fallback)."""
+import os
+import sys
+
+import numpy as np
+
+from conftest import ROOT
+
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402  (no GPU work at import)
+
+
+def _csr(rows):
+    off = np.zeros(len(rows) + 1, dtype=np.uint64)
+    off[1:] = np.cumsum([len(r) for r in rows])
+    ids = np.concatenate([np.asarray(r, dtype=np.int32) for r in rows]) if rows else np.zeros(0, np.int32)
+    return ids, off
+
+
+def _loop(a, b, S):
+    return sum(int(a[2][i] == b[2][i] and np.array_equal(a[0][int(a[1][i]):int(a[1][i + 1])], b[0][int(b[1][i]):int(b[1][i + 1])]))
+               for i in range(S))
+
+
+def test_exact_matches_vectorised_and_fallback():
+    rng = np.random.default_rng(3)
+    rows = [rng.integers(0, 32000, size=int(rng.integers(0, 9))).tolist() for _ in range(500)]
+    ids, off = _csr(rows)
+    st = np.zeros(500, dtype=np.int32)
+    ref = (ids.copy(), off.copy(), st.copy())
+    # identical
+    assert bench.exact_matches(ids, off, st, *ref, 500) == 500
+    # same counts, a few wrong ids and one wrong status: the vectorised path
+    ids2 = ids.copy()
+    hit = rng.choice(len(ids2), 7, replace=False)
+    ids2[hit] += 1
+    st2 = st.copy()
+    st2[11] = 2
+    got = (ids2, off, st2)
+    assert bench.exact_matches(*got, *ref, 500) == _loop(got, ref, 500)
+    # a count differs: the per-string fallback
+    rows3 = [r[:] for r in rows]
+    k = next(i for i, r in enumerate(rows3) if r)
+    rows3[k] = rows3[k][:-1]
+    ids3, off3 = _csr(rows3)
+    got3 = (ids3, off3, st)
+    assert bench.exact_matches(*got3, *ref, 500) == 499 == _loop(got3, ref, 500)
+    # a prefix sample
+    assert bench.exact_matches(*got, *ref, 100) == _loop(got, ref, 100)
