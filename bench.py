@@ -7,9 +7,11 @@ Llama-2 tokenizer file is available offline: SURVEY.md §0 finding 6).
 
 A step = one pass of the hot path (dpt_encode: tokenize kernel(s) + offset scan +
 CSR compaction, then the token-count histogram and, for N>1, ONE RCCL all-reduce
-of it) over the rank's resident shard of 1M strings (BASELINE.json configs[1];
-configs[2] at N=8).  Weak scaling: each rank owns 1M strings of a global corpus
-keyed by (seed, global index).
+of it) over the rank's resident shard (BASELINE.json configs[1] at N=1, configs[2] at N=8).
+Strong scaling (the default for N > 1): ONE global corpus of --strings
+(1M) strings keyed by (seed, global index) is split by dptok.dist.shard_range -- rank r
+takes [r*N/W, (r+1)*N/W) -- and `value` = the corpus bytes / max-over-ranks time.
+--scaling weak gives every rank its own --strings strings instead (labelled "weak").
 
 Launch: python bench.py --gpus 1 --steps K --warmup W
         python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -41,7 +43,11 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=["cfg2", "cfg4", "cfg5"], default="cfg2",
                     help="cfg2 (the metric's config): 256-byte random ASCII; cfg4: S2ORC-shaped; cfg5: Arabic-shaped")
-    ap.add_argument("--strings", type=int, default=None, help="strings per GPU (default: 1M; cfg4: 200k)")
+    ap.add_argument("--strings", type=int, default=None,
+                    help="strings of the global corpus (strong) or per GPU (weak); default 1M (cfg4: 200k)")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default=None,
+                    help="strong (default for N > 1; identical at N = 1): the global corpus is sharded over the "
+                         "ranks by dptok.dist.shard_range; weak: every rank owns --strings strings")
     ap.add_argument("--length", type=int, default=256)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--exact-sample", type=int, default=None,
@@ -138,6 +144,32 @@ def traffic_for(n_str: int, lb: int):
     return None
 
 
+def cpu_share() -> tuple:
+    """(threads the CPU legs use, host CPUs visible to this process).  The GPU box's CPU share is
+    exported as OMP_NUM_THREADS (16 per GPU); os.sched_getaffinity shows what the process may run
+    on, which on a shared box is the whole machine -- the share is what gets used and reported."""
+    vis = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        omp = int(os.environ.get("OMP_NUM_THREADS", "0"))
+    except ValueError:
+        omp = 0
+    return (max(1, min(vis, omp)) if omp > 0 else vis), vis
+
+
+def rank_strings(n_global: int, rank: int, world: int, scaling: str):
+    """Global string-index range [lo, hi) of this rank: its shard_range part of the one corpus
+    (strong) or its own n_global strings (weak)."""
+    from dptok.dist import shard_range
+    if scaling == "strong":
+        return shard_range(n_global, rank, world)
+    return rank * n_global, (rank + 1) * n_global
+
+
+def algorithmic_bytes(n_bytes: int, n_str: int, n_tok: int, id_bytes: int = 4) -> int:
+    """B = N_in + 4*N_tok + 8(N+1) [in offsets] + 8(N+1) [out offsets] + 4N [status]."""
+    return n_bytes + id_bytes * n_tok + 8 * (n_str + 1) + 8 * (n_str + 1) + 4 * n_str
+
+
 def main():
     args = parse()
     import torch
@@ -146,36 +178,40 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    scaling = args.scaling or "strong"   # N = 1: strong and weak are the same run
     from dptok import Encoder, Vocab, synth
     from dptok import dist as ddist
     t2i = synth.llama_shaped_vocab()
     Lb = args.length
+    cores, cpus_visible = cpu_share()
+    gen_procs = max(1, min(16, cores))
+    default_n = 200_000 if args.workload == "cfg4" else 1_000_000
+    N = args.strings or default_n
+    lo, hi = rank_strings(N, rank, world, scaling)
+    M = hi - lo
+    per = "corpus, sharded over the GPUs" if scaling == "strong" else "per GPU"
     if args.workload == "cfg2":
-        M = args.strings or 1_000_000
-        text, offs = synth.random_ascii_corpus(M, Lb, seed=args.seed, start=rank * M)
-        wl = f"cfg2: {M // 1000}k x {Lb}-byte random ASCII strings per GPU, raw pre-tokenization"
+        text, offs = synth.random_ascii_corpus(M, Lb, seed=args.seed, start=lo)
+        wl = f"cfg2: {N // 1000}k x {Lb}-byte random ASCII strings {per}, raw pre-tokenization"
         data = "synthetic random printable ASCII (Philox keyed by seed+global index); synthetic Llama-shaped 32k vocab"
     elif args.workload == "cfg4":
-        M = args.strings or 200_000
-        text, offs = synth.generate_parallel("s2orc", M, start=rank * M, procs=min(16, os.cpu_count() or 1), seed=4)
-        wl = f"cfg4: {M // 1000}k S2ORC-shaped abstracts per GPU (~1200 B, N(1200,400) clipped to [64,4096]), raw"
+        text, offs = synth.generate_parallel("s2orc", M, start=lo, procs=gen_procs, seed=4)
+        wl = f"cfg4: {N // 1000}k S2ORC-shaped abstracts {per} (~1200 B, N(1200,400) clipped to [64,4096]), raw"
         data = "synthetic S2ORC-shaped pseudo-English (dptok.synth.s2orc_like_corpus); synthetic Llama-shaped 32k vocab"
     else:
-        M = args.strings or 1_000_000
-        text, offs = synth.generate_parallel("arabic", M, start=rank * M, procs=min(16, os.cpu_count() or 1),
-                                             length=Lb, seed=5)
-        wl = f"cfg5: {M // 1000}k x ~{Lb}-byte Arabic-shaped strings per GPU (2-byte code points), raw"
+        text, offs = synth.generate_parallel("arabic", M, start=lo, procs=gen_procs, length=Lb, seed=5)
+        wl = f"cfg5: {N // 1000}k x ~{Lb}-byte Arabic-shaped strings {per} (2-byte code points), raw"
         data = "synthetic Arabic-shaped UTF-8 (dptok.synth.arabic_corpus); synthetic Llama-shaped 32k vocab + Arabic letters"
-    Lb = int(offs[-1]) // M
-    cores = max(1, min(16, os.cpu_count() or 1))
+    Lb = int(offs[-1]) // max(M, 1)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # before any GPU call: the pool forks plain CPU workers
         texts = synth.unpack(text[: int(offs[args.cpu_sample])], offs[: args.cpu_sample + 1])
         v, nd, nto, cdt = cpu_baseline(texts, args.cpu_budget, cores)
-        cpu = {"value": v, "unit": "bytes/s", "cores": cores, "kind": "port",
+        cpu = {"value": v, "unit": "bytes/s", "cores": cores, "host_cpus_visible": cpus_visible, "kind": "port",
                "sample": f"{nd} of the first {args.cpu_sample} {args.workload} strings in {cdt:.1f}s "
-                         f"(enumerate-then-select, oracle/ref_port.py; {nto} hit the 10s per-string limit)"}
+                         f"(enumerate-then-select, oracle/ref_port.py, {cores} processes = the box's CPU share "
+                         f"OMP_NUM_THREADS of {cpus_visible} visible CPUs; {nto} hit the 10s per-string limit)"}
 
     gpu = local % max(1, torch.cuda.device_count())
     if gpu != local and args.dist_backend == "nccl":
@@ -183,24 +219,38 @@ def main():
     ddist.init_from_env(args.dist_backend, device=gpu)
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
+    red_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
     vocab = Vocab(t2i, device=gpu)
     enc = Encoder(vocab)
-    n_bytes = len(text)
+    n_bytes = int(offs[-1] - offs[0])
     d_text = torch.from_numpy(text).to(dev)
     d_off = torch.from_numpy(offs.view(np.int64)).to(dev)
-    d_ids = torch.empty(n_bytes, dtype=torch.int32, device=dev)
+    d_ids = torch.empty(max(n_bytes, 1), dtype=torch.int32, device=dev)
     d_idoff = torch.empty(M + 1, dtype=torch.int64, device=dev)
-    d_status = torch.empty(M, dtype=torch.int32, device=dev)
+    d_status = torch.empty(max(M, 1), dtype=torch.int32, device=dev)
     d_hist = torch.zeros(N_BINS + 8, dtype=torch.int64, device=dev)
     enc.reserve(n_bytes, M)
     stream = torch.cuda.current_stream(dev).cuda_stream
 
     def step():
-        enc.encode_device(d_text.data_ptr(), n_bytes, d_off.data_ptr(), M, d_ids.data_ptr(), n_bytes,
+        enc.encode_device(d_text.data_ptr(), n_bytes, d_off.data_ptr(), M, d_ids.data_ptr(), max(n_bytes, 1),
                           d_idoff.data_ptr(), d_status.data_ptr(), stream=stream)
         d_hist.zero_()
         enc.histogram_device(d_idoff.data_ptr(), d_status.data_ptr(), M, d_hist.data_ptr(), N_BINS, stream=stream)
-        ddist.allreduce_histogram(d_hist)  # the single RCCL collective; no-op at N=1
+        if world > 1:   # the single collective: RCCL over xGMI with nccl, gloo in rehearsals
+            if red_dev.type == "cpu":
+                h = d_hist.cpu()
+                ddist.allreduce_histogram(h)
+                d_hist.copy_(h)
+            else:
+                ddist.allreduce_histogram(d_hist)
+
+    def all_sum(x: float) -> float:
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=red_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return float(t.item())
 
     for _ in range(args.warmup):
         step()
@@ -219,7 +269,7 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        t = torch.tensor([dt], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     ms_stage, launches = enc.profile_read()
@@ -229,35 +279,39 @@ def main():
     n_tok_rank = int(d_idoff[-1].item())
     n_tok_all = int(hist[N_BINS])          # after the all-reduce: all ranks' ids
     ok_strings = int(hist[N_BINS + 2])
+    bytes_all = all_sum(float(n_bytes))
+    strings_all = int(all_sum(float(M)))
 
-    # roofline of the dominant kernel (tokenize): algorithmic bytes per launch
+    # roofline of the dominant kernel (tokenize), SURVEY.md §8d bytes per launch (ids at 4 bytes)
     k_ms = ms_stage[0] / max(launches, 1)
     # staged ids are int16 when every vocabulary id is in 0..32767 (dpt_api.cpp ids16), else int32
     id_bytes = 2 if 0 <= min(t2i.values()) and max(t2i.values()) <= 32767 else 4
-    alg_bytes = n_bytes + 8 * (M + 1) + id_bytes * n_tok_rank + 8 * M + 4 * M
+    alg_bytes = algorithmic_bytes(n_bytes, M, n_tok_rank)
+    alg_staged = algorithmic_bytes(n_bytes, M, n_tok_rank, id_bytes)
     achieved = alg_bytes / (k_ms * 1e-3) / 1e9
 
-    # exact match vs the CPU DP (C oracle) and the CPU baseline -- rank 0 only
-    exact = None
-    if rank == 0:
-        from oracle import oracle
-        S = M if args.exact_sample is None else min(args.exact_sample, M)
-        ids_h = d_ids.cpu().numpy()
-        off_h = d_idoff.cpu().numpy().view(np.uint64)
-        st_h = d_status.cpu().numpy()
-        ov = oracle.OracleVocab(t2i)
-        sub_off = offs[: S + 1]
-        rids, roff, rst, _ = ov.encode_csr(text, sub_off, nthreads=cores)
-        same = exact_matches(ids_h, off_h, st_h, rids, roff, rst, S)
-        exact = {"rate": same / S, "sample": S, "checker": "oracle/dp_oracle.c"}
-        if cpu is not None:
-            t0c = time.perf_counter()
-            S2 = min(65536, M)
-            ov.encode_csr(text, offs[: S2 + 1], nthreads=cores)
-            cpu["c_restatement_bytes_per_s"] = int(offs[S2]) / (time.perf_counter() - t0c)
+    # exact match vs the CPU DP (C oracle): every rank checks its own shard, counts are summed
+    from oracle import oracle
+    per_rank_threads = max(1, cores // max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1"))))
+    S = M if args.exact_sample is None else min(args.exact_sample, M)
+    ids_h = d_ids.cpu().numpy()
+    off_h = d_idoff.cpu().numpy().view(np.uint64)
+    st_h = d_status.cpu().numpy()
+    ov = oracle.OracleVocab(t2i)
+    rids, roff, rst, _ = ov.encode_csr(text, offs[: S + 1], nthreads=per_rank_threads)
+    same = exact_matches(ids_h, off_h, st_h, rids, roff, rst, S)
+    same_all, checked_all = all_sum(float(same)), all_sum(float(S))
+    exact = {"rate": same_all / max(checked_all, 1.0), "sample": int(checked_all), "checker": "oracle/dp_oracle.c",
+             "per_rank": "each rank checks %s of its own shard" % ("all" if args.exact_sample is None else "a prefix")}
+    if rank == 0 and cpu is not None:
+        t0c = time.perf_counter()
+        S2 = min(65536, M)
+        ov.encode_csr(text, offs[: S2 + 1], nthreads=cores)
+        cpu["c_restatement_bytes_per_s"] = int(offs[S2]) / (time.perf_counter() - t0c)
+        cpu["c_restatement_threads"] = cores
 
     if rank == 0:
-        value = world * n_bytes * args.steps / dt
+        value = bytes_all * args.steps / dt
         line = {
             "metric": "input bytes/sec/GPU + exact-match rate vs CPU DP, 256-byte strings"
                       if args.workload == "cfg2" else "input bytes/sec/GPU + exact-match rate vs CPU DP (%s)" % args.workload,
@@ -268,23 +322,27 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": dt / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "u8",
             "data": data,
-            "config": {"workload": wl,
+            "config": {"workload": wl, "strings_total": strings_all,
                        "strings_per_gpu": M, "bytes_per_string": Lb, "vocab": "synthetic llama-shaped 32000",
-                       "parallelism": f"dp{world} (corpus shards, 1 RCCL all-reduce of the histogram per step)"},
+                       "parallelism": f"dp{world} ({scaling} scaling: corpus shards, 1 all-reduce of the histogram per step)"},
             "per_gpu_bytes_per_s": value / world,
-            "tokens_per_byte": n_tok_all / (world * n_bytes),
+            "tokens_per_byte": n_tok_all / max(bytes_all, 1.0),
             "ok_strings": ok_strings,
             "exact_match": exact,
             "stage_ms_per_step": {"tokenize": ms_stage[0] / max(launches, 1), "scan": ms_stage[1] / max(launches, 1),
                                   "compact": ms_stage[2] / max(launches, 1)},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic_for(M, Lb) if args.workload == "cfg2" else None,
-                         "kernel": "tokenize_kernel<256,16,false,false,1>" if id_bytes == 2 else "tokenize_kernel<256,16,false,false,2>", "alg_bytes_per_launch": alg_bytes,
-                         "staged_id_bytes": id_bytes},
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": traffic_for(M, Lb) if (args.workload == "cfg2" and world == 1) else None,
+                         "kernel": "tokenize_kernel<256,16,false,false,%d>" % (1 if id_bytes == 2 else 2),
+                         "alg_bytes_per_launch": alg_bytes,
+                         "alg_bytes_formula": "N_in + 4*N_tok + 8(N+1) + 8(N+1) + 4N (SURVEY.md 8d)",
+                         "alg_bytes_staged_width": alg_staged, "staged_id_bytes": id_bytes,
+                         "frac_staged_width": alg_staged / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -376,11 +376,18 @@ static int encode_host_impl(dpt_ctx *c, const dpt_vocab *v, int mode, const uint
                             const uint64_t *str_off, const uint8_t *cut_mask, uint64_t n_str, int32_t *ids,
                             uint64_t ids_cap, uint64_t *id_off, int32_t *status, int32_t *capped_len,
                             uint64_t *edges) {
-    if (!c || !v) return fail(DPT_E_ARG, "null ctx or vocab");
+    // host arguments first (checkable without a device)
     if (!str_off || !id_off || (n_str && !status)) return fail(DPT_E_ARG, "null output/offsets");
     if (n_bytes && (!text || !ids)) return fail(DPT_E_ARG, "null text/ids");
     if (ids_cap < n_bytes) return fail(DPT_E_CAP, "ids_cap must be >= n_bytes");
     if (str_off[n_str] - str_off[0] != n_bytes) return fail(DPT_E_ARG, "n_bytes != str_off[n_str]-str_off[0]");
+    // the kernels take string lengths as 32-bit values (dpt.h): offsets must be monotone and every
+    // string shorter than 4 GiB, or a wrapped length would read past the text
+    for (uint64_t i = 0; i < n_str; i++) {
+        if (str_off[i + 1] < str_off[i]) return fail(DPT_E_ARG, "str_off not monotone");
+        if (str_off[i + 1] - str_off[i] >= (1ull << 32)) return fail(DPT_E_ARG, "a string of 4 GiB or more");
+    }
+    if (!c || !v) return fail(DPT_E_ARG, "null ctx or vocab");
     DeviceGuard g(c->device);
     hipError_t e;
     uint64_t cb = c->h_cap_bytes, cs = c->h_cap_str;

@@ -109,6 +109,9 @@ int dpt_ctx_reserve(dpt_ctx *c, uint64_t n_bytes, uint64_t n_str);
  * ids_cap must be >= n_bytes (a string never yields more ids than bytes).
  * cut_mask (n_bytes bytes, PRESPLIT and ATOMS only): PRESPLIT: != 0 where a word starts (byte 0 of
  * every string always starts one); ATOMS: bit 1 where an atom starts, bit 0 where a word starts.
+ * str_off must be monotone (str_off[s] <= str_off[s+1]) and every string < 4 GiB: the device path
+ * cannot check device-resident offsets (an offset that goes backwards reads past the text);
+ * dpt_encode_host / dpt_dp_host check both and fail with DPT_E_ARG.
  * Limits: every string < 4 GiB, n_str < 2^31; RAW / PRESPLIT text is UTF-8 (code points are the
  * atoms).  No limit on word, atom or token length: words over 256 bytes take a 2048-byte window
  * pass, longer words (and atoms over 8 bytes, or words over 64 atoms when the vocabulary has

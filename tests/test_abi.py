@@ -53,3 +53,24 @@ def test_product_path_has_no_cpu_fallback():
             if f.endswith(".py"):
                 src = open(os.path.join(dp, f), encoding="utf-8").read()
                 assert "oracle" not in src.replace("no CPU fallback", ""), os.path.join(dp, f)
+
+
+def test_host_path_rejects_bad_offsets():
+    """dpt_encode_host validates offsets before touching a device (a backwards offset
+    would wrap the kernel's 32-bit string length and read past the text)."""
+    from dptok import _lib
+    L = _lib.lib()
+    text = ctypes.create_string_buffer(b"abcdef")
+    ids = (ctypes.c_int32 * 8)()
+    id_off = (ctypes.c_uint64 * 4)()
+    status = (ctypes.c_int32 * 3)()
+    # 0 -> 4 -> 2 -> 6: sums to n_bytes = 6 but goes backwards
+    off = (ctypes.c_uint64 * 4)(0, 4, 2, 6)
+    rc = L.dpt_encode_host(None, None, 0, text, 6, off, None, 3, ids, 8, id_off, status, None)
+    assert rc == -1 and b"monotone" in L.dpt_last_error()
+    big = (ctypes.c_uint64 * 3)(0, 1 << 32, (1 << 32) + 6)
+    rc = L.dpt_encode_host(None, None, 0, text, (1 << 32) + 6, big, None, 2, ids, (1 << 32) + 6, id_off, status, None)
+    assert rc == -1 and b"4 GiB" in L.dpt_last_error()
+    ok = (ctypes.c_uint64 * 4)(0, 2, 4, 6)
+    rc = L.dpt_encode_host(None, None, 0, text, 6, ok, None, 3, ids, 8, id_off, status, None)
+    assert rc == -1 and b"null ctx" in L.dpt_last_error()

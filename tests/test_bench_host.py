@@ -47,3 +47,35 @@ def test_exact_matches_vectorised_and_fallback():
     assert bench.exact_matches(*got3, *ref, 500) == 499 == _loop(got3, ref, 500)
     # a prefix sample
     assert bench.exact_matches(*got, *ref, 100) == _loop(got, ref, 100)
+
+
+def test_strong_shards_tile_the_corpus():
+    """cfg3 (BASELINE configs[2]): rank r of W takes [r*N/W, (r+1)*N/W) of ONE corpus."""
+    for n in (1, 7, 125_000, 1_000_000, 1_000_003):
+        for w in (1, 2, 4, 8):
+            r = [bench.rank_strings(n, k, w, "strong") for k in range(w)]
+            assert r[0][0] == 0 and r[-1][1] == n
+            assert all(r[k][1] == r[k + 1][0] for k in range(w - 1))
+            assert sum(b - a for a, b in r) == n
+    # weak: every rank owns its own n strings of the global index space, disjoint
+    r = [bench.rank_strings(1000, k, 4, "weak") for k in range(4)]
+    assert r == [(0, 1000), (1000, 2000), (2000, 3000), (3000, 4000)]
+
+
+def test_algorithmic_bytes_follow_survey_8d():
+    # cfg2: 1M x 256 B, tau = 0.816 ids/byte -> ~1.11 GB per launch with ids at 4 bytes
+    n_str, n_bytes = 1_000_000, 256_000_000
+    n_tok = int(0.816 * n_bytes)
+    b = bench.algorithmic_bytes(n_bytes, n_str, n_tok)
+    assert b == n_bytes + 4 * n_tok + 8 * (n_str + 1) * 2 + 4 * n_str
+    assert 1.10e9 < b < 1.12e9
+    assert bench.algorithmic_bytes(n_bytes, n_str, n_tok, 2) == b - 2 * n_tok
+
+
+def test_cpu_share_reports_threads_used(monkeypatch):
+    monkeypatch.setenv("OMP_NUM_THREADS", "3")
+    used, vis = bench.cpu_share()
+    assert used == min(3, vis) and vis >= 1
+    monkeypatch.delenv("OMP_NUM_THREADS")
+    used, vis = bench.cpu_share()
+    assert used == vis
