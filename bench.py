@@ -55,6 +55,9 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=2048, help="strings for the reference-port CPU baseline")
     ap.add_argument("--cpu-budget", type=float, default=25.0, help="seconds of CPU-baseline wall time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--host-path", action="store_true",
+                    help="instead of the headline line: the drop-in surface the reference's callers use "
+                         "(dp_tokenize(str) per call and dp_tokenize.batch, raw and llama mode, cfg2 and cfg4)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (RCCL, the real path) or gloo -- gloo lets a rehearsal put several ranks "
                          "on one GPU (device = local_rank mod visible GPUs)")
@@ -170,8 +173,51 @@ def algorithmic_bytes(n_bytes: int, n_str: int, n_tok: int, id_bytes: int = 4) -
     return n_bytes + id_bytes * n_tok + 8 * (n_str + 1) + 8 * (n_str + 1) + 4 * n_str
 
 
+def host_path(args):
+    """Secondary line: the unchanged callers' shape (main_analyze_s2orc.py:74-78 one dp_tokenize call
+    per row, :269-271 a serial loop) and the batched form, from Python str to List[List[int]], host
+    buffers through dpt_encode_host (pinned staging, PCIe both ways).  llama mode runs the real
+    SentencePiece model of tests/golden (sp_llama32k.model) through transformers.LlamaTokenizer: its
+    encode is third-party host work and is timed with the rest."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from dptok import synth
+    from packages.tokenizer_utils import dp_tokenize_llama
+    from sp_llama import hf_llama
+    from fake_llama import FakeLlamaTokenizer
+    t2i = synth.llama_shaped_vocab()
+    cfg2 = synth.unpack(*synth.random_ascii_corpus(4096, 256, seed=args.seed))
+    cfg4 = synth.unpack(*synth.s2orc_like_corpus(512, seed=4))
+    out = {"metric": "drop-in host path: us per dp_tokenize(str) call, strings/s and bytes/s per dp_tokenize.batch",
+           "unit": "mixed", "n_gpus": 1, "data": "synthetic", "rows": []}
+    tokz = {"raw": FakeLlamaTokenizer(t2i), "llama": hf_llama()}
+    for mode in ("raw", "llama"):
+        dp_tokenize, _ = dp_tokenize_llama(tokz[mode], mode)
+        for wl, texts in (("cfg2", cfg2), ("cfg4", cfg4)):
+            nbytes = sum(len(t.encode()) for t in texts)
+            for t in texts[:8]:
+                dp_tokenize(t)                       # warm-up (workspace growth, code paths)
+            dp_tokenize.batch(texts)
+            k = 200 if wl == "cfg2" else 100
+            t0 = time.perf_counter()
+            for t in texts[:k]:
+                dp_tokenize(t)
+            per_call = (time.perf_counter() - t0) / k
+            reps = 3
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                dp_tokenize.batch(texts)
+            bt = (time.perf_counter() - t0) / reps
+            out["rows"].append({"mode": mode, "workload": wl, "us_per_call": per_call * 1e6,
+                                "batch_strings": len(texts), "batch_strings_per_s": len(texts) / bt,
+                                "batch_bytes_per_s": nbytes / bt,
+                                "vocab": "synthetic llama-shaped 32000" if mode == "raw" else "SentencePiece BPE 32000 (tests/golden)"})
+    print(json.dumps(out), flush=True)
+
+
 def main():
     args = parse()
+    if args.host_path:
+        return host_path(args)
     import torch
     import torch.distributed as dist
 

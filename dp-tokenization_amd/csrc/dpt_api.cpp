@@ -26,29 +26,25 @@ struct dpt_vocab {
 
 struct dpt_ctx {
     int device = 0;
-    // workspace
-    int32_t *staging = nullptr;
-    int16_t *staging16 = nullptr;     // int16 staging for vocabularies with ids16
-    uint4 *rec = nullptr;             // lane kernel backtrace records (cap_bytes entries)
-    uint64_t cap_bytes = 0;
+    // workspace of the device path (ensure_workspace)
+    int32_t *staging32 = nullptr;     // ids staged as int32 (vocabularies with an id outside 0..32767)
+    uint64_t cap32 = 0;
+    int16_t *staging16 = nullptr;     // ids staged as int16 (vocabularies with ids16)
+    uint64_t cap16 = 0;
+    uint8_t *arena = nullptr;         // the unbounded pass's scratch, 20 bytes per input byte it holds
+    uint64_t arena_cap = 0;           // input bytes
     uint64_t *counts = nullptr;
     uint32_t *retry_list = nullptr;
     uint64_t cap_str = 0;
-    uint32_t *retry_count = nullptr;
+    uint32_t *retry_count = nullptr;  // 64 bytes: 8 uint32 counters, the uint64 arena counter at byte 32
     uint8_t *wsl_scratch = nullptr;   // word lists of the 256-byte pass (dpt::wsl_scratch_bytes)
     void *scan_temp = nullptr;
     size_t scan_bytes = 0;
     unsigned max_blocks = 0;
-    // host-path device buffers
-    uint8_t *h_text = nullptr;
-    uint64_t h_cap_bytes = 0;
-    uint8_t *h_cut = nullptr;
-    int32_t *h_ids = nullptr;
-    uint64_t *h_off = nullptr, *h_idoff = nullptr;
-    int32_t *h_status = nullptr, *h_capped = nullptr;
-    uint64_t h_cap_str = 0;
-    uint64_t *h_edges = nullptr;
-    uint64_t h_cap_edges = 0;
+    // host path: one device buffer in (text | offsets | cut) and one out (id_off | status | capped |
+    // counters | ids | edges), each mirrored by a pinned host buffer so every copy is one async DMA
+    uint8_t *d_in = nullptr, *p_in = nullptr, *d_out = nullptr, *p_out = nullptr;
+    uint64_t cap_in = 0, cap_pin_in = 0, cap_out = 0, cap_pin_out = 0;
     // profiling
     bool profile = false;
     std::vector<hipEvent_t> events;   // groups of 4 per call
@@ -80,10 +76,12 @@ struct DeviceGuard {
     }
 };
 
+// Device buffer of at least `need` elements: exact on first allocation, +25 % when it grows.
 template <typename T>
 hipError_t grow(T **p, uint64_t *cap, uint64_t need) {
     if (need <= *cap && *p) return hipSuccess;
-    uint64_t n = need < 1024 ? 1024 : need + need / 4;
+    uint64_t n = need < 64 ? 64 : need;
+    if (*cap) n += n / 4;
     if (*p) (void)hipFree(*p);
     *p = nullptr;
     *cap = 0;
@@ -92,27 +90,49 @@ hipError_t grow(T **p, uint64_t *cap, uint64_t need) {
     return e;
 }
 
-int ensure_workspace(dpt_ctx *c, uint64_t n_bytes, uint64_t n_str) {
+hipError_t grow_pinned(uint8_t **p, uint64_t *cap, uint64_t need) {
+    if (need <= *cap && *p) return hipSuccess;
+    uint64_t n = need < 4096 ? 4096 : need + (*cap ? need / 4 : 0);
+    if (*p) (void)hipHostFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    hipError_t e = hipHostMalloc((void **)p, n, hipHostMallocDefault);
+    if (e == hipSuccess) *cap = n;
+    return e;
+}
+
+// Input bytes the unbounded pass can hold per call when the caller does not say: every string for
+// small batches, 1/32 of the batch for large ones (20 bytes of arena per held byte: 5/8 of the
+// batch's size); the host path grows it on overflow, dpt_ctx_reserve_vocab sets it.
+uint64_t default_long_bytes(uint64_t n_bytes) {
+    const uint64_t floor = 4ull << 20;
+    uint64_t lb = n_bytes / 32;
+    if (lb < floor) lb = floor;
+    return lb < n_bytes ? lb : n_bytes;
+}
+
+constexpr uint64_t ARENA_PER_BYTE = 20;   // uint4 rec + int32 stg (dpt_long.hip)
+constexpr size_t COUNTER_BYTES = 64;
+
+// v == nullptr: both staging widths (the vocabulary is not known yet)
+int ensure_workspace(dpt_ctx *c, const dpt_vocab *v, uint64_t n_bytes, uint64_t n_str, uint64_t long_bytes) {
     hipError_t e;
-    if (n_bytes > c->cap_bytes || !c->staging) {
-        uint64_t cap1 = c->cap_bytes, cap2 = c->cap_bytes;
-        e = grow(&c->staging, &cap1, n_bytes);
-        if (e != hipSuccess) return hip_fail(e, "hipMalloc(staging)");
-        e = grow(&c->rec, &cap2, n_bytes);
-        if (e != hipSuccess) return hip_fail(e, "hipMalloc(rec)");
-        uint64_t cap3 = c->cap_bytes;
-        e = grow(&c->staging16, &cap3, n_bytes);
-        if (e != hipSuccess) return hip_fail(e, "hipMalloc(staging16)");
-        c->cap_bytes = cap1 < cap2 ? cap1 : cap2;
-        c->cap_bytes = c->cap_bytes < cap3 ? c->cap_bytes : cap3;
+    const bool need16 = !v || v->ids16, need32 = !v || !v->ids16;
+    if (need16 && (e = grow(&c->staging16, &c->cap16, n_bytes)) != hipSuccess) return hip_fail(e, "hipMalloc(staging16)");
+    if (need32 && (e = grow(&c->staging32, &c->cap32, n_bytes)) != hipSuccess) return hip_fail(e, "hipMalloc(staging32)");
+    const uint64_t lb = long_bytes ? long_bytes : default_long_bytes(n_bytes);
+    if (lb > c->arena_cap || !c->arena) {
+        uint64_t cap = c->arena_cap ? c->arena_cap * ARENA_PER_BYTE : 0;
+        if ((e = grow(&c->arena, &cap, lb * ARENA_PER_BYTE)) != hipSuccess) return hip_fail(e, "hipMalloc(arena)");
+        c->arena_cap = cap / ARENA_PER_BYTE;
     }
     if (n_str > c->cap_str || !c->counts) {
-        uint64_t cap = c->cap_str, cap2 = c->cap_str;
+        uint64_t cap = c->cap_str, cap2 = 2 * c->cap_str;
         e = grow(&c->counts, &cap, n_str);
         if (e != hipSuccess) return hip_fail(e, "hipMalloc(counts)");
         e = grow(&c->retry_list, &cap2, 2 * n_str);   // the 2048-byte pass's list, then the unbounded pass's
-        cap2 /= 2;
         if (e != hipSuccess) return hip_fail(e, "hipMalloc(retry_list)");
+        cap2 /= 2;
         c->cap_str = cap < cap2 ? cap : cap2;
         size_t tb = dpt::scan_temp_bytes(c->cap_str);
         if (tb > c->scan_bytes) {
@@ -128,24 +148,18 @@ int ensure_workspace(dpt_ctx *c, uint64_t n_bytes, uint64_t n_str) {
         if (e != hipSuccess) return hip_fail(e, "hipMalloc(wsl_scratch)");
     }
     if (!c->retry_count) {
-        e = hipMalloc((void **)&c->retry_count, 32);
+        e = hipMalloc((void **)&c->retry_count, COUNTER_BYTES);
         if (e != hipSuccess) return hip_fail(e, "hipMalloc(retry_count)");
     }
     return DPT_OK;
 }
 
-// First-pass kernel: 16-lane rows (4 strings per wave) when every token has <= 16 code
-// points, else 64-lane rows.  DPT_KERNEL=lane|rows16|rows64 overrides (A/B measurements; the
-// lane kernel measured slower on cfg2: 2x the VALU count and ~30 GB of scratch traffic per
-// 1M strings, profiles/r01_pmc_*).
+// First-pass kernel: 16-lane rows (4 strings per wave) when every token has <= 16 code points,
+// else 64-lane rows.  DPT_KERNEL=rows64 forces the 64-lane kernel (tests run it on the 32k vocab).
 int kernel_variant(uint32_t max_cp) {
     int v = max_cp <= 16 ? dpt::KERNEL_ROWS16 : dpt::KERNEL_ROWS64;
-    if (const char *e = getenv("DPT_KERNEL")) {
-        if (!strcmp(e, "rows16")) v = dpt::KERNEL_ROWS16;
-        else if (!strcmp(e, "rows64")) v = dpt::KERNEL_ROWS64;
-        else if (!strcmp(e, "lane")) v = dpt::KERNEL_LANE;
-    }
-    if (max_cp > 16) v = dpt::KERNEL_ROWS64;
+    if (const char *e = getenv("DPT_KERNEL"))
+        if (!strcmp(e, "rows64")) v = dpt::KERNEL_ROWS64;
     return v;
 }
 
@@ -281,19 +295,47 @@ int dpt_ctx_create(int device, dpt_ctx **out) {
 int dpt_ctx_destroy(dpt_ctx *c) {
     if (!c) return DPT_OK;
     DeviceGuard g(c->device);
-    void *ps[] = {c->staging, c->staging16, c->rec, c->counts, c->retry_list, c->retry_count, c->wsl_scratch, c->scan_temp, c->h_text, c->h_cut,
-                  c->h_ids, c->h_off, c->h_idoff, c->h_status, c->h_capped, c->h_edges};
+    void *ps[] = {c->staging32, c->staging16, c->arena, c->counts, c->retry_list, c->retry_count, c->wsl_scratch,
+                  c->scan_temp, c->d_in, c->d_out};
     for (void *p : ps)
         if (p) (void)hipFree(p);
+    if (c->p_in) (void)hipHostFree(c->p_in);
+    if (c->p_out) (void)hipHostFree(c->p_out);
     for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
     delete c;
     return DPT_OK;
 }
 
 int dpt_ctx_reserve(dpt_ctx *c, uint64_t n_bytes, uint64_t n_str) {
+    return dpt_ctx_reserve_vocab(c, nullptr, n_bytes, n_str, 0);
+}
+
+int dpt_ctx_reserve_vocab(dpt_ctx *c, const dpt_vocab *v, uint64_t n_bytes, uint64_t n_str, uint64_t long_bytes) {
     if (!c) return fail(DPT_E_ARG, "null ctx");
+    if (v && v->device != c->device) return fail(DPT_E_ARG, "ctx and vocab on different devices");
     DeviceGuard g(c->device);
-    return ensure_workspace(c, n_bytes, n_str);
+    return ensure_workspace(c, v, n_bytes, n_str, long_bytes);
+}
+
+int dpt_ctx_workspace_bytes(const dpt_ctx *c, uint64_t *device_path, uint64_t *host_path) {
+    if (!c) return fail(DPT_E_ARG, "null ctx");
+    if (device_path)
+        *device_path = c->cap16 * 2 + c->cap32 * 4 + c->arena_cap * ARENA_PER_BYTE + c->cap_str * (8 + 2 * 4) +
+                       c->scan_bytes + (c->wsl_scratch ? dpt::wsl_scratch_bytes(c->max_blocks) : 0) +
+                       (c->retry_count ? COUNTER_BYTES : 0);
+    if (host_path) *host_path = c->cap_in + c->cap_out;
+    return DPT_OK;
+}
+
+int dpt_ctx_long_need(dpt_ctx *c, uint64_t *need, uint64_t *cap) {
+    if (!c || !need) return fail(DPT_E_ARG, "null argument");
+    *need = 0;
+    if (cap) *cap = c->arena_cap;
+    if (!c->retry_count) return DPT_OK;
+    DeviceGuard g(c->device);
+    hipError_t e = hipMemcpy(need, reinterpret_cast<uint8_t *>(c->retry_count) + 32, sizeof(uint64_t), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return hip_fail(e, "D2H arena counter");
+    return DPT_OK;
 }
 
 static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uint8_t *text, uint64_t n_bytes,
@@ -310,13 +352,11 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
     if (n_str > 0x7FFFFFFFull) return fail(DPT_E_ARG, "too many strings for one call (max 2^31-1)");
     if (c->device != v->device) return fail(DPT_E_ARG, "ctx and vocab on different devices");
     DeviceGuard g(c->device);
-    int rc = ensure_workspace(c, n_bytes, n_str);
+    int rc = ensure_workspace(c, v, n_bytes, n_str, 0);
     if (rc) return rc;
     hipStream_t st = (hipStream_t)hip_stream;
     dpt::EncodeLaunch p;
     p.mode = mode_flags;
-    if (const char *e = getenv("DPT_B"))   // A/B diagnostic only
-        if (e[0] == 'r') p.mode |= dpt::DPT_FLAG_OLD_B;
     p.edges = edges;
     p.text = text;
     p.str_off = str_off;
@@ -326,7 +366,7 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
     p.id_off = id_off;
     p.status = status;
     p.capped = capped_len;
-    p.staging = c->staging;
+    p.staging = c->staging32;
     p.counts = c->counts;
     p.retry_list = c->retry_list;
     p.retry_count = c->retry_count;
@@ -336,13 +376,11 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
     p.scan_temp = c->scan_temp;
     p.scan_temp_bytes = c->scan_bytes;
     p.max_blocks = c->max_blocks;
-    p.rec = c->rec;
+    p.arena = c->arena;
+    p.arena_cap = c->arena_cap;
     p.variant = kernel_variant(v->stats.max_cp);
-    // the lane kernel implements the plain raw / pre-split encode only
-    if (p.variant == dpt::KERNEL_LANE && ((mode_flags != DPT_MODE_RAW && mode_flags != DPT_MODE_PRESPLIT) || edges))
-        p.variant = v->stats.max_cp <= 16 ? dpt::KERNEL_ROWS16 : dpt::KERNEL_ROWS64;
-    // int16 staging when every id fits (the lane kernel stages int32 only); DPT_WIDE_STAGING=1: A/B only
-    p.staging16 = (v->ids16 && p.variant != dpt::KERNEL_LANE && !getenv("DPT_WIDE_STAGING")) ? c->staging16 : nullptr;
+    // int16 staging when every id fits in 0..32767 (half the staging traffic)
+    p.staging16 = v->ids16 ? c->staging16 : nullptr;
     p.slots = v->d_slots;
     p.slot_ids = v->d_ids;
     p.n_slots = v->stats.n_slots;
@@ -390,60 +428,66 @@ static int encode_host_impl(dpt_ctx *c, const dpt_vocab *v, int mode, const uint
     if (!c || !v) return fail(DPT_E_ARG, "null ctx or vocab");
     DeviceGuard g(c->device);
     hipError_t e;
-    uint64_t cb = c->h_cap_bytes, cs = c->h_cap_str;
-    if (n_bytes + 1 > c->h_cap_bytes || !c->h_text) {
-        uint64_t c1 = cb, c2 = cb, c3 = cb;
-        if ((e = grow(&c->h_text, &c1, n_bytes + 1)) != hipSuccess) return hip_fail(e, "hipMalloc");
-        if ((e = grow(&c->h_cut, &c2, n_bytes + 1)) != hipSuccess) return hip_fail(e, "hipMalloc");
-        if ((e = grow(&c->h_ids, &c3, n_bytes + 1)) != hipSuccess) return hip_fail(e, "hipMalloc");
-        c->h_cap_bytes = c1 < c2 ? (c1 < c3 ? c1 : c3) : (c2 < c3 ? c2 : c3);
-    }
-    if (n_str + 2 > c->h_cap_str || !c->h_off) {
-        uint64_t c1 = cs, c2 = cs, c3 = cs, c4 = cs;
-        if ((e = grow(&c->h_off, &c1, n_str + 2)) != hipSuccess) return hip_fail(e, "hipMalloc");
-        if ((e = grow(&c->h_idoff, &c2, n_str + 2)) != hipSuccess) return hip_fail(e, "hipMalloc");
-        if ((e = grow(&c->h_status, &c3, n_str + 2)) != hipSuccess) return hip_fail(e, "hipMalloc");
-        if ((e = grow(&c->h_capped, &c4, n_str + 2)) != hipSuccess) return hip_fail(e, "hipMalloc");
-        uint64_t m = c1 < c2 ? c1 : c2;
-        m = m < c3 ? m : c3;
-        c->h_cap_str = m < c4 ? m : c4;
-    }
-    hipStream_t st = 0;
-    if (n_bytes && (e = hipMemcpyAsync(c->h_text, text, n_bytes, hipMemcpyHostToDevice, st)) != hipSuccess)
-        return hip_fail(e, "H2D text");
-    if ((mode & DPT_MODE_MASK) != DPT_MODE_RAW && n_bytes &&
-        (e = hipMemcpyAsync(c->h_cut, cut_mask, n_bytes, hipMemcpyHostToDevice, st)) != hipSuccess)
-        return hip_fail(e, "H2D cut");
-    // offsets rebased to 0 so that the device view is self-contained
-    std::vector<uint64_t> off(n_str + 1);
+    const bool cut = (mode & DPT_MODE_MASK) != DPT_MODE_RAW && n_bytes;
+    if (cut && !cut_mask) return fail(DPT_E_ARG, "PRESPLIT/ATOMS need cut_mask");
+    auto al8 = [](uint64_t x) { return (x + 7) & ~7ull; };
+    // in:  text | offsets rebased to 0 (the device view is self-contained) | cut mask
+    const uint64_t o_off = al8(n_bytes + 1), o_cut = o_off + 8 * (n_str + 1), in_bytes = o_cut + al8(n_bytes + 1);
+    // out: id_off | status | capped | counters | ids | edges
+    const uint64_t o_st = 8 * (n_str + 1), o_cap = o_st + al8(4 * n_str + 4), o_ctr = o_cap + al8(4 * n_str + 4);
+    const uint64_t o_ids = o_ctr + COUNTER_BYTES, o_edges = o_ids + al8(4 * (n_bytes + 1));
+    const uint64_t out_bytes = o_edges + (edges ? 8 * (n_bytes + 1) : 0);
+    if ((e = grow(&c->d_in, &c->cap_in, in_bytes)) != hipSuccess) return hip_fail(e, "hipMalloc(host-path in)");
+    if ((e = grow(&c->d_out, &c->cap_out, out_bytes)) != hipSuccess) return hip_fail(e, "hipMalloc(host-path out)");
+    if ((e = grow_pinned(&c->p_in, &c->cap_pin_in, in_bytes)) != hipSuccess) return hip_fail(e, "hipHostMalloc(in)");
+    if ((e = grow_pinned(&c->p_out, &c->cap_pin_out, out_bytes)) != hipSuccess) return hip_fail(e, "hipHostMalloc(out)");
+    if (n_bytes) memcpy(c->p_in, text, n_bytes);
+    uint64_t *off = reinterpret_cast<uint64_t *>(c->p_in + o_off);
     for (uint64_t i = 0; i <= n_str; i++) off[i] = str_off[i] - str_off[0];
-    if ((e = hipMemcpyAsync(c->h_off, off.data(), (n_str + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st)) != hipSuccess)
-        return hip_fail(e, "H2D offsets");
-    uint64_t *d_edges = nullptr;
-    if (edges) {
-        uint64_t cap = c->h_cap_edges;
-        if ((e = grow(&c->h_edges, &cap, n_bytes + 1)) != hipSuccess) return hip_fail(e, "hipMalloc(edges)");
-        c->h_cap_edges = cap;
-        d_edges = c->h_edges;
+    if (cut) memcpy(c->p_in + o_cut, cut_mask, n_bytes);
+    hipStream_t st = 0;
+    if ((e = hipMemcpyAsync(c->d_in, c->p_in, in_bytes, hipMemcpyHostToDevice, st)) != hipSuccess) return hip_fail(e, "H2D");
+    uint64_t *d_idoff = reinterpret_cast<uint64_t *>(c->d_out);
+    int32_t *d_status = reinterpret_cast<int32_t *>(c->d_out + o_st);
+    int32_t *d_capped = reinterpret_cast<int32_t *>(c->d_out + o_cap);
+    int32_t *d_ids = reinterpret_cast<int32_t *>(c->d_out + o_ids);
+    uint64_t *d_edges = edges ? reinterpret_cast<uint64_t *>(c->d_out + o_edges) : nullptr;
+    const uint64_t *p_idoff = reinterpret_cast<const uint64_t *>(c->p_out);
+    // small batches: everything in one copy (ids up to the n_bytes bound); large: the head, then the ids
+    const bool one_copy = 4 * n_bytes <= (4ull << 20);
+    for (int attempt = 0;; attempt++) {
+        int rc = encode_impl(c, v, mode, c->d_in, n_bytes, reinterpret_cast<const uint64_t *>(c->d_in + o_off),
+                             cut ? c->d_in + o_cut : nullptr, n_str, d_ids, n_bytes ? n_bytes : 1, d_idoff, d_status,
+                             d_capped, d_edges, st);
+        if (rc) return rc;
+        if ((e = hipMemcpyAsync(c->p_out + o_ctr, c->retry_count, COUNTER_BYTES, hipMemcpyDeviceToHost, st)) != hipSuccess)
+            return hip_fail(e, "D2H counters");
+        if ((e = hipMemcpyAsync(c->p_out, c->d_out, one_copy ? out_bytes : o_ctr, hipMemcpyDeviceToHost, st)) != hipSuccess)
+            return hip_fail(e, "D2H");
+        if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(e, "sync");
+        uint64_t used = 0;
+        memcpy(&used, c->p_out + o_ctr + 32, sizeof(used));
+        if (used <= c->arena_cap) break;
+        // the unbounded pass's arena was too small for the strings routed to it (those strings got
+        // status 3): grow it to what the pass claimed and run the call again
+        if (attempt > 0) return fail(DPT_E_ARG, "unbounded pass arena overflow after growth");
+        if ((rc = ensure_workspace(c, v, n_bytes, n_str, used))) return rc;
     }
-    int rc = encode_impl(c, v, mode, c->h_text, n_bytes, c->h_off, c->h_cut, n_str, c->h_ids, c->h_cap_bytes, c->h_idoff,
-                         c->h_status, c->h_capped, d_edges, st);
-    if (rc) return rc;
-    if (edges && n_bytes &&
-        (e = hipMemcpyAsync(edges, d_edges, n_bytes * sizeof(uint64_t), hipMemcpyDeviceToHost, st)) != hipSuccess)
-        return hip_fail(e, "D2H edges");
-    if ((e = hipMemcpyAsync(id_off, c->h_idoff, (n_str + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, st)) != hipSuccess)
-        return hip_fail(e, "D2H id_off");
-    if (n_str && (e = hipMemcpyAsync(status, c->h_status, n_str * sizeof(int32_t), hipMemcpyDeviceToHost, st)) != hipSuccess)
-        return hip_fail(e, "D2H status");
-    if (capped_len && n_str &&
-        (e = hipMemcpyAsync(capped_len, c->h_capped, n_str * sizeof(int32_t), hipMemcpyDeviceToHost, st)) != hipSuccess)
-        return hip_fail(e, "D2H capped");
-    if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(e, "sync");
-    const uint64_t total = id_off[n_str];
+    const uint64_t total = p_idoff[n_str];
     if (total > ids_cap) return fail(DPT_E_CAP, "ids overflow");
-    if (total && (e = hipMemcpy(ids, c->h_ids, total * sizeof(int32_t), hipMemcpyDeviceToHost)) != hipSuccess)
-        return hip_fail(e, "D2H ids");
+    if (!one_copy) {
+        if (total && (e = hipMemcpyAsync(c->p_out + o_ids, d_ids, 4 * total, hipMemcpyDeviceToHost, st)) != hipSuccess)
+            return hip_fail(e, "D2H ids");
+        if (edges && n_bytes &&
+            (e = hipMemcpyAsync(c->p_out + o_edges, d_edges, 8 * n_bytes, hipMemcpyDeviceToHost, st)) != hipSuccess)
+            return hip_fail(e, "D2H edges");
+        if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(e, "sync");
+    }
+    memcpy(id_off, c->p_out, 8 * (n_str + 1));
+    if (n_str) memcpy(status, c->p_out + o_st, 4 * n_str);
+    if (capped_len && n_str) memcpy(capped_len, c->p_out + o_cap, 4 * n_str);
+    if (total) memcpy(ids, c->p_out + o_ids, 4 * total);
+    if (edges && n_bytes) memcpy(edges, c->p_out + o_edges, 8 * n_bytes);
     return DPT_OK;
 }
 

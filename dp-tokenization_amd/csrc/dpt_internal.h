@@ -24,7 +24,8 @@ struct EncodeLaunch {
     int16_t *staging16;      // non-null: ids staged as int16 here instead (every vocabulary id in 0..32767)
     uint64_t *counts;
     uint32_t *retry_list;    // 2 x n_str: the 2048-byte pass's list, then (at + n_str) the unbounded pass's list
-    uint32_t *retry_count;   // 8 counters: retry count, pass-1 / pass-2 work, long count, long work
+    uint32_t *retry_count;   // 8 counters: retry count, pass-1 / pass-2 work, long count, long work; then
+                             // (as uint64 at byte 32) the unbounded pass's arena use in input bytes
     uint8_t *wsl_scratch;    // max_blocks x wsl_scratch_bytes(1) bytes
     int long_span;           // vocabulary tokens longer than 64 code points: words over 64 atoms -> unbounded pass
     uint32_t max_tok_bytes;  // longest vocabulary token, bytes
@@ -32,11 +33,12 @@ struct EncodeLaunch {
     size_t scan_temp_bytes;
     unsigned max_blocks;
     int variant;             // KERNEL_* below
-    uint4 *rec;              // lane kernel: per-atom backtrace records (n_bytes entries)
+    uint8_t *arena;          // the unbounded pass's scratch: 20 bytes per input byte of the strings it takes
+    uint64_t arena_cap;      // input bytes the arena holds
     // vocabulary
     const int2 *slots;
     const int32_t *slot_ids;
-    const int4 *slots4;      // lane kernel: {base | TERM<<31, check, id, 0}
+    const int4 *slots4;      // {base | TERM<<31 | LEAF<<30, check, id, child filter}
     uint32_t n_slots;
     int32_t root_base;
 };
@@ -45,12 +47,7 @@ struct EncodeLaunch {
 // low five bits inside each 32-byte block, so the 26 lowercase letters get distinct bits
 __host__ __device__ inline unsigned child_bit(unsigned b) { return (b ^ (b >> 5)) & 31u; }
 
-// internal mode bit (never in the public API): A/B diagnostic, DPT_B=rows selects the 16-lane
-// row recurrence for capless windows instead of the lane-chunk one (dpt_api.cpp)
-constexpr int DPT_FLAG_OLD_B = 0x40000000;
-
 // kernel variants for the first pass (the 2048-byte window pass always follows for retries)
-constexpr int KERNEL_LANE = 0;    // lane per string, register ring of 16 walks (vocab max_cp <= 16)
 constexpr int KERNEL_ROWS16 = 1;  // 4 strings per wave in 16-lane DPP rows, LDS windows (max_cp <= 16)
 constexpr int KERNEL_ROWS64 = 2;  // 1 string per wave, 64-lane DPP (max_cp <= 64)
 
@@ -60,9 +57,11 @@ struct LongLaunch {
     const uint8_t *text;
     const uint64_t *str_off;
     const uint8_t *cut_mask;
-    int32_t *staging;
-    int16_t *staging16;      // as EncodeLaunch: the final ids go here when non-null
-    uint4 *rec;              // 16 bytes of scratch per input byte
+    int32_t *staging;        // the final ids (int32 vocabularies) at the string's byte offset + k
+    int16_t *staging16;      // as EncodeLaunch: the final ids go here instead when non-null
+    uint8_t *arena;          // scratch: uint4 rec[arena_cap] then int32 stg[arena_cap], per string at its
+    uint64_t arena_cap;      //   claimed offset (input bytes; 20 bytes of scratch per input byte)
+    unsigned long long *arena_used;   // claimed input bytes (all long strings; > arena_cap: overflow)
     uint64_t *counts;
     int32_t *status;
     int32_t *capped;
@@ -81,7 +80,6 @@ struct LongLaunch {
 void launch_long(const LongLaunch &p, hipStream_t stream);
 
 hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t ev[6]);
-void launch_lane(const EncodeLaunch &p, unsigned blocks, hipStream_t stream);
 size_t scan_temp_bytes(uint64_t n_str);
 size_t wsl_scratch_bytes(unsigned max_blocks);
 hipError_t launch_histogram(const uint64_t *id_off, const int32_t *status, uint64_t n_str, int64_t *hist,

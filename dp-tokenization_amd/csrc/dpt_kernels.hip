@@ -1290,8 +1290,8 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
             } else {
                 if (!capb) {
                     if constexpr (G == 16) {
-                        if (a.mode & dpt::DPT_FLAG_OLD_B) forward(F_{}, C2_{});
-                        else { forward_lanes(); lane_mode = true; }
+                        forward_lanes();
+                        lane_mode = true;
 #ifdef DPT_LANEDBG
                         if (lane == 0) atomicAdd(&g_lanedbg[16 * 16 + 1], 1u);
 #endif
@@ -1579,45 +1579,6 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
 
 // ------------------------------------------------------------------ compaction
 
-// One wave per 64 consecutive strings: their offsets arrive in one coalesced load per lane,
-// then the wave copies string after string with up to 256 ids (4 loads per lane) in flight.
-template <typename ST>   // int32_t, or int16_t when every id fits (sign-extended: -1 stays -1)
-__global__ void __launch_bounds__(256) compact_kernel(const ST *__restrict__ staging, const uint64_t *__restrict__ str_off,
-                                                      const uint64_t *__restrict__ id_off, uint64_t n_str,
-                                                      int32_t *__restrict__ ids) {
-    const uint64_t base_off = str_off[0];
-    const unsigned lane = threadIdx.x & 63;
-    const uint64_t n_batches = (n_str + 63) / 64;
-    for (uint64_t bt = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); bt < n_batches; bt += (uint64_t)gridDim.x * 4) {
-        const uint64_t s = bt * 64 + lane;
-        uint64_t src = 0, dst = 0, n = 0;
-        if (s < n_str) {
-            src = str_off[s] - base_off;
-            dst = id_off[s];
-            n = id_off[s + 1] - dst;
-        }
-        const unsigned cnt = (unsigned)min((uint64_t)64, n_str - bt * 64);
-        for (unsigned t = 0; t < cnt; t++) {
-            const uint64_t so = uni64(__builtin_amdgcn_readlane((unsigned)src, t) | ((uint64_t)__builtin_amdgcn_readlane((unsigned)(src >> 32), t) << 32));
-            const uint64_t dO = ((uint64_t)__builtin_amdgcn_readlane((unsigned)(dst >> 32), t) << 32) | __builtin_amdgcn_readlane((unsigned)dst, t);
-            const unsigned nn = __builtin_amdgcn_readlane((unsigned)n, t);
-            for (unsigned k0 = 0; k0 < nn; k0 += 256) {
-                int32_t v[4];
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    const unsigned k = k0 + q * 64 + lane;
-                    v[q] = k < nn ? (int32_t)staging[so + k] : 0;
-                }
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    const unsigned k = k0 + q * 64 + lane;
-                    if (k < nn) ids[dO + k] = v[q];
-                }
-            }
-        }
-    }
-}
-
 // Flat compaction: one wave (block) per 64 consecutive strings, lanes over the batch's OUTPUT
 // ids (contiguous in ids[]: every store is a coalesced row), each lane tracking the string its
 // id falls in (offsets in LDS; strings usually hold more than 64 ids, so the string index
@@ -1669,7 +1630,8 @@ __global__ void __launch_bounds__(64) compact_flat_kernel(const ST *__restrict__
 }
 
 __global__ void zero_first(uint64_t *p, uint32_t *rc) {
-    if (threadIdx.x < 8) rc[threadIdx.x] = 0;   // retry count, pass-1 / pass-2 work, long count, long work
+    // retry count, pass-1 / pass-2 work, long count, long work; the uint64 arena counter at byte 32
+    if (threadIdx.x < 10) rc[threadIdx.x] = 0;
     if (threadIdx.x == 0) p[0] = 0;
 }
 
@@ -1773,11 +1735,7 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
         if (er != hipSuccess) return er;
     }
     if (p.n_str > 0) {
-        if (p.variant == KERNEL_LANE) {
-            uint64_t blocks = (p.n_str + 63) / 64;
-            if (blocks > (uint64_t)p.max_blocks) blocks = p.max_blocks;
-            launch_lane(p, (unsigned)blocks, stream);
-        } else {
+        {
             const unsigned n_cu = p.max_blocks / 64;
             if (p.variant == KERNEL_ROWS16) {
                 // the hot kernel gets the staged id width as a template constant
@@ -1804,7 +1762,9 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
         // its waves read a zero count and exit)
         LongLaunch l;
         l.mode = p.mode; l.text = p.text; l.str_off = p.str_off; l.cut_mask = p.cut_mask;
-        l.staging = p.staging; l.staging16 = p.staging16; l.rec = p.rec; l.counts = p.counts; l.status = p.status; l.capped = p.capped;
+        l.staging = p.staging; l.staging16 = p.staging16; l.counts = p.counts; l.status = p.status; l.capped = p.capped;
+        l.arena = p.arena; l.arena_cap = p.arena_cap;
+        l.arena_used = reinterpret_cast<unsigned long long *>(p.retry_count + 8);
         l.edges = p.edges; l.list = a.long_list; l.list_count = a.long_count; l.work_next = p.retry_count + 4;
         l.slots = p.slots; l.slots4 = p.slots4; l.n_slots = p.n_slots; l.root_base = p.root_base;
         l.max_tok_bytes = p.max_tok_bytes; l.long_span = p.long_span;
@@ -1826,20 +1786,12 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
         if (er != hipSuccess) return er;
     }
     if (p.n_str > 0) {
-        uint64_t blocks = (p.n_str + 255) / 256;   // 4 waves x 64 strings
-        if (blocks > 4096) blocks = 4096;
-        static const bool flat = !getenv("DPT_COMPACT_OLD");   // A/B only
-        if (flat) {
-            uint64_t fb = (p.n_str + 63) / 64;
-            if (fb > (uint64_t)p.max_blocks / 2) fb = p.max_blocks / 2;   // 32 waves per CU
-            if (p.staging16)
-                hipLaunchKernelGGL(compact_flat_kernel<int16_t>, dim3((unsigned)fb), dim3(64), 0, stream, p.staging16, p.str_off, p.id_off, p.n_str, p.ids);
-            else
-                hipLaunchKernelGGL(compact_flat_kernel<int32_t>, dim3((unsigned)fb), dim3(64), 0, stream, p.staging, p.str_off, p.id_off, p.n_str, p.ids);
-        } else if (p.staging16)
-            hipLaunchKernelGGL(compact_kernel<int16_t>, dim3((unsigned)blocks), dim3(256), 0, stream, p.staging16, p.str_off, p.id_off, p.n_str, p.ids);
+        uint64_t fb = (p.n_str + 63) / 64;
+        if (fb > (uint64_t)p.max_blocks / 2) fb = p.max_blocks / 2;   // 32 waves per CU
+        if (p.staging16)
+            hipLaunchKernelGGL(compact_flat_kernel<int16_t>, dim3((unsigned)fb), dim3(64), 0, stream, p.staging16, p.str_off, p.id_off, p.n_str, p.ids);
         else
-            hipLaunchKernelGGL(compact_kernel<int32_t>, dim3((unsigned)blocks), dim3(256), 0, stream, p.staging, p.str_off, p.id_off, p.n_str, p.ids);
+            hipLaunchKernelGGL(compact_flat_kernel<int32_t>, dim3((unsigned)fb), dim3(64), 0, stream, p.staging, p.str_off, p.id_off, p.n_str, p.ids);
     }
     if (ev) {
         const hipError_t er = hipEventRecord(ev[3], stream);

@@ -27,10 +27,14 @@
 //            in DFS order, dp_tokenize.py:58, :84), C2 ids by re-walking every selected span
 //            (t2i[token], tokenizer_utils.py:76-79), 64 tokens at a time.
 //
-// Scratch per string s (byte range [sb, sb+slen) of the batch, atoms n <= slen):
-//   rec[sb+a]      uint4 {off, cpb | WS | LONG_END, mask lo -> dg | de << 16 of end a+1,
+// Scratch per string s (atoms n <= slen): a range [ao, ao+slen) of the ctx's arena, claimed in list
+// order (ao = an atomic add of slen to the arena counter); a string whose range does not fit gets
+// status 3 and the host path reruns the call with an arena as large as the counter says
+// (dpt_api.cpp), so the arena need not hold 20 bytes per input byte of the whole batch:
+//   rec[ao+a]      uint4 {off, cpb | WS | LONG_END, mask lo -> dg | de << 16 of end a+1,
 //                         mask hi -> state of a (long candidates) / final key of the word ending at a+1}
-//   staging[sb+a]  state of a (cost part) / word-final cost -> token starts (C1) -> ids (C2)
+//   stg[ao+a]      state of a (cost part) / word-final cost -> token starts (C1)
+// The ids (C2) go to the staging row of the string, staging16 / staging at its byte offset sb + k.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -101,9 +105,12 @@ struct Args {
     const uint8_t *text;
     const uint64_t *str_off;
     const uint8_t *cut_mask;
-    int32_t *staging;
-    int16_t *staging16;   // non-null: the final ids go here as int16 (staging stays the scratch)
-    uint4 *rec;
+    int32_t *staging;     // the final ids at sb + k (int32 vocabularies)
+    int16_t *staging16;   // non-null: the final ids go here as int16 instead
+    uint4 *rec;           // arena: rec[arena_cap], then stg[arena_cap]
+    int32_t *stg;
+    uint64_t arena_cap;
+    unsigned long long *arena_used;
     uint64_t *counts;
     int32_t *status;
     int32_t *capped;
@@ -203,10 +210,23 @@ __global__ void __launch_bounds__(64) long_kernel(Args a) {
         const uint64_t s = a.list[idx];
         const uint64_t o0 = a.str_off[s], o1 = a.str_off[s + 1];
         const uint64_t sb = o0 - base_off;
+        // the string's scratch range in the arena
+        unsigned long long ao = 0;
+        if (lane == 0) ao = atomicAdd(a.arena_used, (unsigned long long)(o1 - o0));
+        ao = ((unsigned long long)__builtin_amdgcn_readlane((unsigned)(ao >> 32), 0) << 32) | __builtin_amdgcn_readlane((unsigned)ao, 0);
+        if (ao + (o1 - o0) > a.arena_cap) {
+            // does not fit: status 3 (dpt_encode_host / dpt_dp_host grow the arena and rerun)
+            if (lane == 0) {
+                a.status[s] = DPT_STATUS_TOO_LONG;
+                a.counts[s] = 0;
+                if (a.capped) a.capped[s] = -1;
+            }
+            continue;
+        }
         Str S;
         S.t = a.text + sb;
-        S.rec = a.rec + sb;
-        S.stg = a.staging + sb;
+        S.rec = a.rec + ao;
+        S.stg = a.stg + ao;
         S.slen = (unsigned)(o1 - o0);
         S.raw = raw;
         const uint8_t *cut = raw ? nullptr : a.cut_mask + sb;
@@ -482,7 +502,7 @@ __global__ void __launch_bounds__(64) long_kernel(Args a) {
                 phase_sync();
                 if (in) {
                     if (a.staging16) a.staging16[sb + k] = (int16_t)(ok ? id : -1);
-                    else S.stg[k] = ok ? id : -1;
+                    else a.staging[sb + k] = ok ? id : -1;
                 }
             }
         }
@@ -500,7 +520,11 @@ __global__ void __launch_bounds__(64) long_kernel(Args a) {
 void launch_long(const LongLaunch &p, hipStream_t stream) {
     lng::Args a;
     a.text = p.text; a.str_off = p.str_off; a.cut_mask = p.cut_mask;
-    a.staging = p.staging; a.staging16 = p.staging16; a.rec = p.rec; a.counts = p.counts; a.status = p.status; a.capped = p.capped;
+    a.staging = p.staging; a.staging16 = p.staging16; a.counts = p.counts; a.status = p.status; a.capped = p.capped;
+    a.rec = reinterpret_cast<uint4 *>(p.arena);
+    a.stg = reinterpret_cast<int32_t *>(p.arena + 16 * p.arena_cap);
+    a.arena_cap = p.arena_cap;
+    a.arena_used = p.arena_used;
     a.edges = p.edges; a.list = p.list; a.list_count = p.list_count; a.work_next = p.work_next;
     a.slots = p.slots; a.slots4 = p.slots4; a.n_slots = p.n_slots; a.root_base = p.root_base;
     a.max_tok_bytes = p.max_tok_bytes; a.long_span = p.long_span; a.mode = p.mode;

@@ -146,22 +146,46 @@ class Encoder:
         ids, id_off, st, _ = self.encode_csr(text, offs)
         return [(ids[int(id_off[i]):int(id_off[i + 1])].tolist(), int(st[i])) for i in range(len(texts))]
 
+    def encode_presplit(self, strings: Sequence[Sequence[str]]) -> List[Tuple[List[int], int]]:
+        """Many strings, each pre-split into words (llama mode, DPT_MODE_PRESPLIT), in ONE launch:
+        per string (ids, status).  Words are processed in order like the reference's loop
+        (tokenizer_utils.py:70-75): an empty word raises IndexError there (dp_tokenize.py:49)
+        unless an earlier word already failed (no tokenization -> ValueError), so a string is cut
+        at its first empty word and that word's status is decided by the prefix before it."""
+        enc_words, n_words, cut_at = [], [], []
+        for words in strings:
+            k = next((i for i, w in enumerate(words) if not w), -1)
+            ws = words if k < 0 else words[:k]
+            enc_words.extend(encode_utf8(w) for w in ws)
+            n_words.append(len(ws))
+            cut_at.append(k)
+        wl = np.fromiter((len(e) for e in enc_words), dtype=np.uint64, count=len(enc_words))
+        wend = np.concatenate([np.zeros(1, np.uint64), np.cumsum(wl, dtype=np.uint64)])   # bytes of the first k words
+        n_str = len(strings)
+        offs = np.concatenate([np.zeros(1, np.uint64), wend[np.cumsum(np.asarray(n_words, dtype=np.int64))]]) \
+            if n_str else np.zeros(1, np.uint64)
+        raw = b"".join(enc_words)
+        cut = np.zeros(len(raw) + 1, dtype=np.uint8)
+        if len(wl):
+            cut[wend[:-1].astype(np.int64)] = 1   # every word's first byte
+        text = np.frombuffer(raw + b"\0", dtype=np.uint8)
+        ids, id_off, st, _ = self.encode_csr(text, offs, mode="presplit", cut_mask=cut)
+        flat = ids.tolist()
+        o = id_off.tolist()
+        out = []
+        for i in range(n_str):
+            s = int(st[i])
+            if cut_at[i] < 0 and n_words[i] == 0:
+                out.append(([], _lib.STATUS_OK))           # no words: the reference's loop emits nothing
+            elif cut_at[i] >= 0 and s in (_lib.STATUS_OK, _lib.STATUS_EMPTY_WORD):
+                out.append(([], _lib.STATUS_EMPTY_WORD))   # the prefix tokenized (or was empty): IndexError
+            else:
+                out.append((flat[o[i]:o[i + 1]] if s == _lib.STATUS_OK else [], s))
+        return out
+
     def encode_words(self, words: Sequence[str]) -> Tuple[List[int], int]:
         """One string pre-split into words (llama mode, DPT_MODE_PRESPLIT): ids and status."""
-        enc = [encode_utf8(w) for w in words]
-        raw = b"".join(enc)
-        cut = np.zeros(len(raw) + 1, dtype=np.uint8)
-        o = 0
-        for e in enc:
-            if o < len(raw):
-                cut[o] = 1
-            o += len(e)
-        if any(len(e) == 0 for e in enc):
-            return [], _lib.STATUS_EMPTY_WORD
-        text = np.frombuffer(raw + b"\0", dtype=np.uint8)
-        offs = np.array([0, len(raw)], dtype=np.uint64)
-        ids, id_off, st, _ = self.encode_csr(text, offs, mode="presplit", cut_mask=cut)
-        return ids.tolist(), int(st[0])
+        return self.encode_presplit([words])[0]
 
     def encode_word_atoms(self, strings: Sequence[Sequence[Sequence[str]]]) -> List[Tuple[List[int], int]]:
         """Strings given as words of atoms (DPT_MODE_ATOMS), one launch for the batch: per string
@@ -227,8 +251,24 @@ class Encoder:
                                     ctypes.c_void_p(status_ptr), ctypes.c_void_p(capped_ptr or None),
                                     ctypes.c_void_p(stream or None)), "dpt_encode")
 
-    def reserve(self, n_bytes: int, n_str: int) -> None:
-        check(_lib.lib().dpt_ctx_reserve(self.handle, n_bytes, n_str), "dpt_ctx_reserve")
+    def reserve(self, n_bytes: int, n_str: int, long_bytes: int = 0) -> None:
+        """Pre-size the workspace for this vocabulary's staging width (a later call of that size is
+        capture-safe); ``long_bytes``: input bytes the unbounded pass holds per call (0: default)."""
+        check(_lib.lib().dpt_ctx_reserve_vocab(self.handle, self.vocab.handle, n_bytes, n_str, long_bytes),
+              "dpt_ctx_reserve_vocab")
+
+    def workspace_bytes(self) -> Tuple[int, int]:
+        """(device-path workspace, host-path staging) bytes held on the device."""
+        a, b = ctypes.c_uint64(), ctypes.c_uint64()
+        check(_lib.lib().dpt_ctx_workspace_bytes(self.handle, ctypes.byref(a), ctypes.byref(b)), "dpt_ctx_workspace_bytes")
+        return a.value, b.value
+
+    def long_need(self) -> Tuple[int, int]:
+        """(input bytes the last call's unbounded pass took, its arena capacity); call after the
+        encode's stream has completed."""
+        a, b = ctypes.c_uint64(), ctypes.c_uint64()
+        check(_lib.lib().dpt_ctx_long_need(self.handle, ctypes.byref(a), ctypes.byref(b)), "dpt_ctx_long_need")
+        return a.value, b.value
 
     def histogram_device(self, idoff_ptr: int, status_ptr: int, n_str: int, hist_ptr: int, n_bins: int,
                          stream: int = 0) -> None:

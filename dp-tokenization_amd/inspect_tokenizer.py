@@ -53,10 +53,9 @@ def _uncapped_min(atoms, vocabulary) -> float:
     atoms = list(atoms)
     if not atoms:
         return 0
-    vocab = {t for t in vocabulary if isinstance(t, str) and t}
-    if not vocab:
+    if not any(isinstance(t, str) and t for t in vocabulary):
         return float("inf")
-    status, length, _ = _dp_edges(atoms, vocab, uncapped=True, edges=False)
+    status, length, _ = _dp_edges(atoms, vocabulary, uncapped=True, edges=False)
     if status not in (0, 1) or length >= _INF_WORD:
         return float("inf")
     return length

@@ -31,11 +31,21 @@ if _HERE not in sys.path:
 from dptok import DptError, Encoder, Vocab  # noqa: E402
 from dptok.engine import atoms_to_csr  # noqa: E402
 
-_CACHE: "OrderedDict[frozenset, Encoder]" = OrderedDict()
+_CACHE: "OrderedDict[frozenset, Encoder]" = OrderedDict()   # by content: token set -> engine
+_BY_ID: "OrderedDict[tuple, tuple]" = OrderedDict()          # by identity: (id, len) -> (object, engine)
 
 
 def _engine_for(vocabulary) -> Encoder:
-    key = frozenset(vocabulary)
+    """The engine of a vocabulary (set, dict or list of token strings; non-strings and '' are not
+    tokens).  Looked up by object identity + size first (O(1) for the callers that pass the same
+    vocabulary every call), then by content (O(|V|), e.g. a set rebuilt per call), and built and
+    uploaded only for a vocabulary not seen before."""
+    key_id = (id(vocabulary), len(vocabulary))
+    hit = _BY_ID.get(key_id)
+    if hit is not None and hit[0] is vocabulary:
+        _BY_ID.move_to_end(key_id)
+        return hit[1]
+    key = frozenset(t for t in vocabulary if isinstance(t, str) and t)
     enc = _CACHE.get(key)
     if enc is None:
         t2i = {tok: i for i, tok in enumerate(sorted(key))}
@@ -45,6 +55,9 @@ def _engine_for(vocabulary) -> Encoder:
             _CACHE.popitem(last=False)
     else:
         _CACHE.move_to_end(key)
+    _BY_ID[key_id] = (vocabulary, enc)
+    if len(_BY_ID) > 8:
+        _BY_ID.popitem(last=False)
     return enc
 
 
@@ -66,8 +79,7 @@ def compute_shortest_tokenizations(base_representation_s, vocabulary, disregard_
     n = len(atoms)
     if n == 0:
         raise IndexError("list index out of range")
-    vocab = {t for t in vocabulary if t}
-    status, length, edges = _dp_edges(atoms, vocab)
+    status, length, edges = _dp_edges(atoms, vocabulary)
     if status == 3:
         # an optimal predecessor more than 64 atoms back (a token of > 64 code points): the
         # 64-bit per-end edge masks of dpt_dp_host cannot list it

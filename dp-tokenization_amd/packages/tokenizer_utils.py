@@ -13,7 +13,8 @@ MI355X engine.  Same names, argument meaning and error behaviour:
   (reference: ipdb.set_trace then max([]) at dp_tokenize.py:84), an empty word -> IndexError
   (dp_tokenize.py:49).  An unknown ``pretokenize_option`` fails at call time with NameError,
   like the reference's unbound ``pretokenize_func``.
-* ``dp_tokenize.batch(List[str]) -> List[List[int]]``: the batched form (one GPU launch).
+* ``dp_tokenize.batch(List[str]) -> List[List[int]]``: the batched form (one GPU launch, in both
+  modes).
 * ``merge_tokens``, ``pretokenize_with_llama``, ``pretokenize_raw``: the reference's host-side
   string utilities with identical behaviour (pre-tokenization, not the DP).
 """
@@ -114,9 +115,11 @@ def dp_tokenize_llama(llama_tokenizer, pretokenize_option="llama"):
         pretokenize = pretokenize_with_llama(llama_tokenizer, vocab_bidict)
 
         def encode_many(texts: Sequence[str]) -> List[List[int]]:
+            # SentencePiece runs on the host (third-party); the DP of every word of every text is
+            # ONE pre-split launch
+            texts = list(texts)
             out = []
-            for t in texts:
-                ids, st = engine.encode_words(pretokenize(t))
+            for t, (ids, st) in zip(texts, engine.encode_presplit([pretokenize(t) for t in texts])):
                 raise_for_status(st, t)
                 out.append(ids)
             return out

@@ -60,10 +60,11 @@ extern "C" {
 #define DPT_STATUS_OK 0
 #define DPT_STATUS_NO_TOKENIZATION 1 /* reference: ipdb.set_trace / ValueError (dp_tokenize.py:84) */
 #define DPT_STATUS_EMPTY_WORD 2      /* reference: IndexError (dp_tokenize.py:49) */
-#define DPT_STATUS_TOO_LONG 3        /* outside the engine's limits: dpt_encode never returns it (words, atoms
-                                        and tokens of any length are exact -- the windowed kernels hand what
-                                        they cannot hold to the unbounded pass); dpt_dp_host with edges returns
-                                        it when an optimal predecessor lies more than 64 atoms back */
+#define DPT_STATUS_TOO_LONG 3        /* words, atoms and tokens of any length are exact (the windowed kernels
+                                        hand what they cannot hold to the unbounded pass); dpt_encode returns
+                                        3 only for a string the unbounded pass's arena could not hold in that
+                                        call (dpt_ctx_long_need / dpt_ctx_reserve_vocab); dpt_encode_host and
+                                        dpt_dp_host grow the arena and rerun, so they never do */
 #define DPT_STATUS_INTERNAL 4        /* engine invariant violated (never expected) */
 
 typedef struct dpt_vocab dpt_vocab;
@@ -93,10 +94,22 @@ int dpt_vocab_create(const uint8_t *utf8_blob, const uint64_t *tok_off, const in
 int dpt_vocab_destroy(dpt_vocab *v);
 int dpt_vocab_stats_get(const dpt_vocab *v, dpt_vocab_stats *out);
 
-/* Workspace on `device` (grows on demand; dpt_ctx_reserve makes a later call capture-safe). */
+/* Workspace on `device` (grows on demand; dpt_ctx_reserve makes a later call capture-safe).
+ * Device-path workspace per call of n_bytes / n_str: the staged ids (2 bytes per input byte when
+ * every vocabulary id is in 0..32767, else 4), 16 bytes per string, and the unbounded pass's arena
+ * (20 bytes per input byte it holds; by default max(4 MiB, n_bytes/32) input bytes, at most n_bytes). */
 int dpt_ctx_create(int device, dpt_ctx **out);
 int dpt_ctx_destroy(dpt_ctx *c);
-int dpt_ctx_reserve(dpt_ctx *c, uint64_t n_bytes, uint64_t n_str);
+int dpt_ctx_reserve(dpt_ctx *c, uint64_t n_bytes, uint64_t n_str);   /* both staging widths */
+/* Reserve for vocabulary v's staging width (v may be NULL: both) and an unbounded-pass arena holding
+ * long_bytes input bytes of long-word strings per call (0: the default above; n_bytes: every string). */
+int dpt_ctx_reserve_vocab(dpt_ctx *c, const dpt_vocab *v, uint64_t n_bytes, uint64_t n_str, uint64_t long_bytes);
+/* Device bytes held: the device-path workspace and the host path's staging buffers. */
+int dpt_ctx_workspace_bytes(const dpt_ctx *c, uint64_t *device_path, uint64_t *host_path);
+/* After the ctx's last dpt_encode has completed (synchronise its stream first): the input bytes of the
+ * strings its unbounded pass took (*need) and the arena's capacity (*cap).  need > cap: the strings that
+ * did not fit have status DPT_STATUS_TOO_LONG -- reserve long_bytes >= need and call again. */
+int dpt_ctx_long_need(dpt_ctx *c, uint64_t *need, uint64_t *cap);
 
 /*
  * Tokenize n_str strings, CSR-packed: string s is text[str_off[s]-str_off[0] .. str_off[s+1]-str_off[0]),

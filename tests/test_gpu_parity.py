@@ -172,7 +172,7 @@ def test_device_path_and_histogram(engines, oracles):
     assert np.array_equal(h[:257], np.bincount(np.minimum(counts, 257), minlength=258)[:257])
 
 
-@pytest.mark.parametrize("variant", ["lane", "rows16", "rows64"])
+@pytest.mark.parametrize("variant", ["rows16", "rows64"])
 def test_kernel_variants_vs_oracle(variant, engines, oracles, monkeypatch):
     """Every first-pass kernel (DPT_KERNEL override) is bit-exact on cfg2 / Arabic / S2ORC samples."""
     from dptok import synth
