@@ -460,10 +460,11 @@ static int encode_host_impl(dpt_ctx *c, const dpt_vocab *v, int mode, const uint
                              cut ? c->d_in + o_cut : nullptr, n_str, d_ids, n_bytes ? n_bytes : 1, d_idoff, d_status,
                              d_capped, d_edges, st);
         if (rc) return rc;
-        if ((e = hipMemcpyAsync(c->p_out + o_ctr, c->retry_count, COUNTER_BYTES, hipMemcpyDeviceToHost, st)) != hipSuccess)
-            return hip_fail(e, "D2H counters");
         if ((e = hipMemcpyAsync(c->p_out, c->d_out, one_copy ? out_bytes : o_ctr, hipMemcpyDeviceToHost, st)) != hipSuccess)
             return hip_fail(e, "D2H");
+        // after the block copy, which spans the (unused) counter slot of d_out
+        if ((e = hipMemcpyAsync(c->p_out + o_ctr, c->retry_count, COUNTER_BYTES, hipMemcpyDeviceToHost, st)) != hipSuccess)
+            return hip_fail(e, "D2H counters");
         if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(e, "sync");
         uint64_t used = 0;
         memcpy(&used, c->p_out + o_ctr + 32, sizeof(used));
