@@ -379,8 +379,7 @@ def main():
             "tokens_per_byte": n_tok_all / max(bytes_all, 1.0),
             "ok_strings": ok_strings,
             "exact_match": exact,
-            "stage_ms_per_step": {"tokenize": ms_stage[0] / max(launches, 1), "scan": ms_stage[1] / max(launches, 1),
-                                  "compact": ms_stage[2] / max(launches, 1)},
+            "stage_ms_per_step": {"tokenize": ms_stage[0] / max(launches, 1)},   # finish (offsets + CSR ids): rocprof
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic_for(M, Lb) if (args.workload == "cfg2" and world == 1) else None,

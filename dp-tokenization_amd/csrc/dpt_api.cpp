@@ -38,8 +38,9 @@ struct dpt_ctx {
     uint64_t cap_str = 0;
     uint32_t *retry_count = nullptr;  // 64 bytes: 8 uint32 counters, the uint64 arena counter at byte 32
     uint8_t *wsl_scratch = nullptr;   // word lists of the 256-byte pass (dpt::wsl_scratch_bytes)
-    void *scan_temp = nullptr;
-    size_t scan_bytes = 0;
+    unsigned long long *flags = nullptr;   // finish kernel's look-back flags (one per 64 strings)
+    uint64_t cap_flags = 0;
+    unsigned epoch = 0;               // call counter for the flags (1..65535; the array is cleared on wrap)
     unsigned max_blocks = 0;
     // host path: one device buffer in (text | offsets | cut) and one out (id_off | status | capped |
     // counters | ids | edges), each mirrored by a pinned host buffer so every copy is one async DMA
@@ -134,21 +135,20 @@ int ensure_workspace(dpt_ctx *c, const dpt_vocab *v, uint64_t n_bytes, uint64_t 
         if (e != hipSuccess) return hip_fail(e, "hipMalloc(retry_list)");
         cap2 /= 2;
         c->cap_str = cap < cap2 ? cap : cap2;
-        size_t tb = dpt::scan_temp_bytes(c->cap_str);
-        if (tb > c->scan_bytes) {
-            if (c->scan_temp) (void)hipFree(c->scan_temp);
-            c->scan_temp = nullptr;
-            e = hipMalloc(&c->scan_temp, tb);
-            if (e != hipSuccess) return hip_fail(e, "hipMalloc(scan)");
-            c->scan_bytes = tb;
-        }
+    }
+    if ((n_str + 63) / 64 > c->cap_flags || !c->flags) {
+        if ((e = grow(&c->flags, &c->cap_flags, (n_str + 63) / 64)) != hipSuccess) return hip_fail(e, "hipMalloc(flags)");
+        if ((e = hipMemset(c->flags, 0, c->cap_flags * sizeof(unsigned long long))) != hipSuccess) return hip_fail(e, "hipMemset(flags)");
+        c->epoch = 0;
     }
     if (!c->wsl_scratch) {
         e = hipMalloc((void **)&c->wsl_scratch, dpt::wsl_scratch_bytes(c->max_blocks));
         if (e != hipSuccess) return hip_fail(e, "hipMalloc(wsl_scratch)");
     }
     if (!c->retry_count) {
+        // zeroed once here; every call's finish kernel resets it for the next call
         e = hipMalloc((void **)&c->retry_count, COUNTER_BYTES);
+        if (e == hipSuccess) e = hipMemset(c->retry_count, 0, COUNTER_BYTES);
         if (e != hipSuccess) return hip_fail(e, "hipMalloc(retry_count)");
     }
     return DPT_OK;
@@ -296,7 +296,7 @@ int dpt_ctx_destroy(dpt_ctx *c) {
     if (!c) return DPT_OK;
     DeviceGuard g(c->device);
     void *ps[] = {c->staging32, c->staging16, c->arena, c->counts, c->retry_list, c->retry_count, c->wsl_scratch,
-                  c->scan_temp, c->d_in, c->d_out};
+                  c->flags, c->d_in, c->d_out};
     for (void *p : ps)
         if (p) (void)hipFree(p);
     if (c->p_in) (void)hipHostFree(c->p_in);
@@ -321,7 +321,7 @@ int dpt_ctx_workspace_bytes(const dpt_ctx *c, uint64_t *device_path, uint64_t *h
     if (!c) return fail(DPT_E_ARG, "null ctx");
     if (device_path)
         *device_path = c->cap16 * 2 + c->cap32 * 4 + c->arena_cap * ARENA_PER_BYTE + c->cap_str * (8 + 2 * 4) +
-                       c->scan_bytes + (c->wsl_scratch ? dpt::wsl_scratch_bytes(c->max_blocks) : 0) +
+                       c->cap_flags * 8 + (c->wsl_scratch ? dpt::wsl_scratch_bytes(c->max_blocks) : 0) +
                        (c->retry_count ? COUNTER_BYTES : 0);
     if (host_path) *host_path = c->cap_in + c->cap_out;
     return DPT_OK;
@@ -333,7 +333,7 @@ int dpt_ctx_long_need(dpt_ctx *c, uint64_t *need, uint64_t *cap) {
     if (cap) *cap = c->arena_cap;
     if (!c->retry_count) return DPT_OK;
     DeviceGuard g(c->device);
-    hipError_t e = hipMemcpy(need, reinterpret_cast<uint8_t *>(c->retry_count) + 32, sizeof(uint64_t), hipMemcpyDeviceToHost);
+    hipError_t e = hipMemcpy(need, reinterpret_cast<uint8_t *>(c->retry_count) + 40, sizeof(uint64_t), hipMemcpyDeviceToHost);
     if (e != hipSuccess) return hip_fail(e, "D2H arena counter");
     return DPT_OK;
 }
@@ -373,8 +373,13 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
     p.wsl_scratch = c->wsl_scratch;
     p.long_span = v->stats.max_cp > 64 ? 1 : 0;
     p.max_tok_bytes = v->stats.max_bytes;
-    p.scan_temp = c->scan_temp;
-    p.scan_temp_bytes = c->scan_bytes;
+    p.flags = c->flags;
+    if (++c->epoch > 0xFFFFu) {   // the flags' epoch wraps: clear them so no stale flag can match
+        hipError_t e0 = hipMemsetAsync(c->flags, 0, c->cap_flags * sizeof(unsigned long long), (hipStream_t)hip_stream);
+        if (e0 != hipSuccess) return hip_fail(e0, "hipMemsetAsync(flags)");
+        c->epoch = 1;
+    }
+    p.epoch = c->epoch;
     p.max_blocks = c->max_blocks;
     p.arena = c->arena;
     p.arena_cap = c->arena_cap;
@@ -386,10 +391,10 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
     p.n_slots = v->stats.n_slots;
     p.slots4 = v->d_slots4;
     p.root_base = v->root_base;
-    hipEvent_t ev[6];
+    hipEvent_t ev[2];
     hipEvent_t *evp = nullptr;
     if (c->profile) {
-        for (int k = 0; k < 4; k++) {
+        for (int k = 0; k < 2; k++) {
             hipError_t e = hipEventCreate(&ev[k]);
             if (e != hipSuccess) return hip_fail(e, "hipEventCreate");
             c->events.push_back(ev[k]);
@@ -398,7 +403,10 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
         c->launches++;
     }
     hipError_t e = dpt::launch_encode(p, st, evp);
-    if (e != hipSuccess) return hip_fail(e, "encode launch");
+    if (e != hipSuccess) {
+        (void)hipMemsetAsync(c->retry_count, 0, COUNTER_BYTES, st);   // the finish kernel did not reset them
+        return hip_fail(e, "encode launch");
+    }
     return DPT_OK;
 }
 
@@ -467,7 +475,7 @@ static int encode_host_impl(dpt_ctx *c, const dpt_vocab *v, int mode, const uint
             return hip_fail(e, "D2H counters");
         if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(e, "sync");
         uint64_t used = 0;
-        memcpy(&used, c->p_out + o_ctr + 32, sizeof(used));
+        memcpy(&used, c->p_out + o_ctr + 40, sizeof(used));   // the call's claimed bytes (finish_kernel)
         if (used > n_bytes) return fail(DPT_E_HIP, "unbounded pass counter out of range");   // never expected
         if (used <= c->arena_cap) break;
         // the unbounded pass's arena was too small for the strings routed to it (those strings got
@@ -530,16 +538,15 @@ int dpt_ctx_profile(dpt_ctx *c, int enable) {
 int dpt_ctx_profile_read(dpt_ctx *c, double *ms, uint64_t *launches) {
     if (!c || !ms) return fail(DPT_E_ARG, "null argument");
     DeviceGuard g(c->device);
-    ms[0] = ms[1] = ms[2] = 0.0;
-    for (size_t k = 0; k + 3 < c->events.size(); k += 4) {
-        hipError_t e = hipEventSynchronize(c->events[k + 3]);
+    ms[0] = 0.0;
+    ms[1] = ms[2] = -1.0;   // not timed: one event pair per call (every event record costs the stream ~6 us)
+    for (size_t k = 0; k + 1 < c->events.size(); k += 2) {
+        hipError_t e = hipEventSynchronize(c->events[k + 1]);
         if (e != hipSuccess) return hip_fail(e, "hipEventSynchronize");
-        for (int s = 0; s < 3; s++) {
-            float t = 0.f;
-            e = hipEventElapsedTime(&t, c->events[k + s], c->events[k + s + 1]);
-            if (e != hipSuccess) return hip_fail(e, "hipEventElapsedTime");
-            ms[s] += t;
-        }
+        float t = 0.f;
+        e = hipEventElapsedTime(&t, c->events[k], c->events[k + 1]);
+        if (e != hipSuccess) return hip_fail(e, "hipEventElapsedTime");
+        ms[0] += t;
     }
     for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
     c->events.clear();

@@ -24,13 +24,12 @@ struct EncodeLaunch {
     int16_t *staging16;      // non-null: ids staged as int16 here instead (every vocabulary id in 0..32767)
     uint64_t *counts;
     uint32_t *retry_list;    // 2 x n_str: the 2048-byte pass's list, then (at + n_str) the unbounded pass's list
-    uint32_t *retry_count;   // 8 counters: retry count, pass-1 / pass-2 work, long count, long work; then
-                             // (as uint64 at byte 32) the unbounded pass's arena use in input bytes
+    uint32_t *retry_count;   // the 64-byte counter block (dpt_kernels.hip, finish_kernel)
     uint8_t *wsl_scratch;    // max_blocks x wsl_scratch_bytes(1) bytes
     int long_span;           // vocabulary tokens longer than 64 code points: words over 64 atoms -> unbounded pass
     uint32_t max_tok_bytes;  // longest vocabulary token, bytes
-    void *scan_temp;
-    size_t scan_temp_bytes;
+    unsigned long long *flags;   // finish kernel's look-back flags, one per 64 strings
+    unsigned epoch;              // the ctx's call counter (1..65535)
     unsigned max_blocks;
     int variant;             // KERNEL_* below
     uint8_t *arena;          // the unbounded pass's scratch: 20 bytes per input byte of the strings it takes
@@ -79,8 +78,7 @@ struct LongLaunch {
 };
 void launch_long(const LongLaunch &p, hipStream_t stream);
 
-hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t ev[6]);
-size_t scan_temp_bytes(uint64_t n_str);
+hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t ev[2]);
 size_t wsl_scratch_bytes(unsigned max_blocks);
 hipError_t launch_histogram(const uint64_t *id_off, const int32_t *status, uint64_t n_str, int64_t *hist,
                             uint32_t n_bins, hipStream_t stream);

@@ -36,7 +36,6 @@
 // Strings whose single word exceeds CH bytes are re-run by the 2048-byte, one-string-per-wave
 // instantiation.  A scan + compaction turns the staging rows into CSR ids.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -1579,60 +1578,143 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
 
 // ------------------------------------------------------------------ compaction
 
-// Flat compaction: one wave (block) per 64 consecutive strings, lanes over the batch's OUTPUT
-// ids (contiguous in ids[]: every store is a coalesced row), each lane tracking the string its
-// id falls in (offsets in LDS; strings usually hold more than 64 ids, so the string index
-// advances at most once per step), COMPACT_U independent loads in flight per lane -- no
-// per-string round trip.
-#ifndef COMPACT_U
-#define COMPACT_U 8
-#endif
-template <typename ST>
-__global__ void __launch_bounds__(64) compact_flat_kernel(const ST *__restrict__ staging, const uint64_t *__restrict__ str_off,
-                                                          const uint64_t *__restrict__ id_off, uint64_t n_str,
-                                                          int32_t *__restrict__ ids) {
-    __shared__ uint64_t s_rel[65];   // id_off of the batch's strings - id_off of its first, + end
-    __shared__ uint64_t s_src[64];   // staging element of each string's first id
-    const uint64_t base_off = str_off[0];
-    const unsigned lane = threadIdx.x;
-    const uint64_t n_batches = (n_str + 63) / 64;
-    for (uint64_t bt = blockIdx.x; bt < n_batches; bt += gridDim.x) {
-        const uint64_t s0 = bt * 64;
-        const unsigned cnt = (unsigned)min((uint64_t)64, n_str - s0);
-        const uint64_t o0 = uni64(id_off[s0]);
-        if (lane < cnt) {
-            s_rel[lane] = id_off[s0 + lane] - o0;
-            s_src[lane] = str_off[s0 + lane] - base_off;
-        }
-        if (lane == 0) s_rel[cnt] = id_off[s0 + cnt] - o0;
-        wave_sync();
-        const uint64_t total = s_rel[cnt];
-        unsigned j = 0;   // the string of this lane's current id (monotone in t)
-        for (uint64_t t0 = 0; t0 < total; t0 += 64u * COMPACT_U) {
-            int32_t v[COMPACT_U];
-#pragma unroll
-            for (int u = 0; u < COMPACT_U; u++) {
-                const uint64_t t = t0 + (uint64_t)u * 64u + lane;
-                v[u] = 0;
-                if (t < total) {
-                    while (s_rel[j + 1] <= t) j++;
-                    v[u] = (int32_t)staging[s_src[j] + (t - s_rel[j])];
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < COMPACT_U; u++) {
-                const uint64_t t = t0 + (uint64_t)u * 64u + lane;
-                if (t < total) ids[o0 + t] = v[u];
-            }
-        }
-        wave_sync();   // s_rel / s_src are rewritten by the next batch
-    }
+// ------------------------------------------------------------------ finish: offsets + CSR ids in one pass
+
+// Counter block (EncodeLaunch::retry_count, 64 bytes; zeroed once at allocation, then reset for the
+// next call by the finish kernel's last block): uint32 [0] retry count, [1] first-pass work, [2]
+// 2048-byte pass work, [3] long count, [4] long work, [5] finish ticket; uint64 [4] (byte 32) the
+// unbounded pass's claimed bytes, [5] (byte 40) the last call's claimed bytes (dpt_ctx_long_need),
+// [6] (byte 48) far edges listed (dpt_dp_host_far).
+constexpr unsigned CTR_TICKET = 5;
+constexpr unsigned CTR_ARENA64 = 4, CTR_LASTNEED64 = 5;
+
+// Look-back flags, one uint64 per 64-string batch: epoch (16 bits, the ctx's call counter; 0 never
+// used, the host clears the array when it wraps) | state (2 bits: 1 = batch aggregate, 2 = inclusive
+// prefix) | value (46 bits of ids).
+__device__ __forceinline__ uint64_t flag_pack(unsigned epoch, unsigned st, uint64_t v) {
+    return ((uint64_t)epoch << 48) | ((uint64_t)st << 46) | v;
 }
 
-__global__ void zero_first(uint64_t *p, uint32_t *rc) {
-    // retry count, pass-1 / pass-2 work, long count, long work; the uint64 arena counter at byte 32
-    if (threadIdx.x < 10) rc[threadIdx.x] = 0;
-    if (threadIdx.x == 0) p[0] = 0;
+// 64-bit inclusive add-scan over the wave (ds_bpermute shifts)
+__device__ __forceinline__ uint64_t wave_incl_scan_add64(uint64_t v, unsigned lane) {
+#pragma unroll
+    for (unsigned k = 1; k < 64; k <<= 1) {
+        const int src = (int)((lane >= k ? lane - k : lane) << 2);
+        const unsigned lo = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)(unsigned)v);
+        const unsigned hi = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)(unsigned)(v >> 32));
+        v += lane >= k ? (((uint64_t)hi << 32) | lo) : 0ull;
+    }
+    return v;
+}
+
+struct FinishArgs {
+    const void *staging;          // int16_t or int32_t (ST)
+    const uint64_t *str_off;
+    const uint64_t *counts;
+    uint64_t n_str;
+    uint64_t *id_off;
+    int32_t *ids;
+    unsigned long long *flags;
+    uint32_t *ctr;
+    unsigned epoch;
+};
+
+// One block of 256 threads per 64 consecutive strings, in ticket order (a block waits only for
+// batches whose tickets were taken before its own, so by blocks already running): wave 0 scans the
+// batch's counts, publishes the aggregate, looks back over the earlier batches' flags for its
+// exclusive offset (decoupled look-back) and publishes the inclusive prefix; then the four waves
+// copy the batch's staged ids -- lanes over the batch's OUTPUT ids, so every store is a coalesced
+// row -- 8 independent loads in flight per lane.  Replaces the counter reset, the offset scan and
+// the compaction of round 1 (three launches and two more passes over the counts).
+template <typename ST>
+__global__ void __launch_bounds__(256) finish_kernel(FinishArgs f) {
+    __shared__ uint64_t s_rel[65];   // ids of the batch's strings before string k, + the batch total
+    __shared__ uint64_t s_src[64];   // staging element of each string's first id
+    __shared__ uint64_t s_base;      // the batch's first id
+    __shared__ unsigned s_ticket;
+    const unsigned tid = threadIdx.x, lane = tid & 63u;
+    const uint64_t n_batches = (f.n_str + 63) / 64;
+    if (tid == 0) {
+        const unsigned t = atomicAdd(&f.ctr[CTR_TICKET], 1u);
+        if ((uint64_t)t + 1 == n_batches) {
+            // the last ticket: every block has its batch, and every tokenize pass is done -- reset
+            // the counters for the next call (the claimed arena bytes stay readable as "last need")
+            uint64_t *c64 = reinterpret_cast<uint64_t *>(f.ctr);
+            c64[CTR_LASTNEED64] = c64[CTR_ARENA64];
+            c64[CTR_ARENA64] = 0;
+            f.ctr[0] = 0; f.ctr[1] = 0; f.ctr[2] = 0; f.ctr[3] = 0; f.ctr[4] = 0;
+            __hip_atomic_store(&f.ctr[CTR_TICKET], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s_ticket = t;
+    }
+    __syncthreads();
+    const uint64_t t = s_ticket;
+    const uint64_t s0 = t * 64;
+    const unsigned cnt = (unsigned)min((uint64_t)64, f.n_str - s0);
+    if (tid < 64) {
+        const uint64_t c = lane < cnt ? f.counts[s0 + lane] : 0ull;
+        const uint64_t incl = wave_incl_scan_add64(c, lane);
+        const uint64_t agg = uni64(((uint64_t)__builtin_amdgcn_readlane((unsigned)(incl >> 32), 63) << 32) |
+                                   __builtin_amdgcn_readlane((unsigned)incl, 63));
+        uint64_t excl = 0;
+        if (t == 0) {
+            if (lane == 0) __hip_atomic_store(&f.flags[0], flag_pack(f.epoch, 2, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            if (lane == 0) __hip_atomic_store(&f.flags[t], flag_pack(f.epoch, 1, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // look back 64 batches at a time: lane l reads batch jb - l; sum up to the nearest
+            // inclusive prefix once every batch before it in the window has published
+            uint64_t jb = t - 1;
+            for (unsigned spin = 0;;) {
+                const bool in = lane <= jb;
+                uint64_t fl = in ? __hip_atomic_load(&f.flags[jb - lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : flag_pack(f.epoch, 2, 0);
+                const unsigned st = (fl >> 48) == f.epoch ? (unsigned)(fl >> 46) & 3u : 0u;
+                const uint64_t pm = ballot(st == 2), ready = ballot(st != 0);
+                const unsigned p = pm ? (unsigned)__builtin_ctzll(pm) : 64u;          // nearest prefix in the window
+                const uint64_t need = p < 63 ? ((2ull << p) - 1) : ~0ull;             // lanes 0..p
+                if ((ready & need) != need) {                                         // not all published yet
+                    __builtin_amdgcn_s_sleep(1);
+                    if (++spin > (1u << 24)) break;   // never expected: bounded, so a broken protocol cannot hang the GPU
+                    continue;
+                }
+                uint64_t v = (lane <= p && in) ? (fl & ((1ull << 46) - 1)) : 0ull;
+                v = wave_incl_scan_add64(v, lane);
+                excl += uni64(((uint64_t)__builtin_amdgcn_readlane((unsigned)(v >> 32), 63) << 32) |
+                              __builtin_amdgcn_readlane((unsigned)v, 63));
+                if (p < 64) break;
+                jb -= 64;   // 64 aggregates, no prefix yet: the next window
+                spin = 0;
+            }
+            if (lane == 0) __hip_atomic_store(&f.flags[t], flag_pack(f.epoch, 2, excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (lane < cnt) f.id_off[s0 + lane + 1] = excl + incl;
+        if (t == 0 && lane == 0) f.id_off[0] = 0;
+        s_rel[lane] = incl - c;
+        if (lane == 63) s_rel[64] = incl;
+        s_src[lane] = lane < cnt ? f.str_off[s0 + lane] - f.str_off[0] : 0ull;
+        if (lane == 0) s_base = excl;
+    }
+    __syncthreads();
+    const ST *__restrict__ staging = reinterpret_cast<const ST *>(f.staging);
+    const uint64_t total = s_rel[64], o0 = s_base;
+    unsigned j = 0;   // the string of this thread's current id (monotone in k)
+    constexpr unsigned U = 8;
+    for (uint64_t k0 = 0; k0 < total; k0 += 256u * U) {
+        int32_t v[U];
+#pragma unroll
+        for (unsigned u = 0; u < U; u++) {
+            const uint64_t k = k0 + (uint64_t)u * 256u + tid;
+            v[u] = 0;
+            if (k < total) {
+                while (s_rel[j + 1] <= k) j++;
+                v[u] = (int32_t)staging[s_src[j] + (k - s_rel[j])];
+            }
+        }
+#pragma unroll
+        for (unsigned u = 0; u < U; u++) {
+            const uint64_t k = k0 + (uint64_t)u * 256u + tid;
+            if (k < total) f.ids[o0 + k] = v[u];
+        }
+    }
 }
 
 // ------------------------------------------------------------------ histogram
@@ -1715,7 +1797,7 @@ static void launch_tok(const EncodeArgs &a, const TrieView &tv, uint64_t n_units
     hipLaunchKernelGGL((tokenize_kernel<CH, G, BIG, WIDE, SW>), dim3((unsigned)blocks), dim3(64), lds, stream, a, tv);
 }
 
-hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t ev[6]) {
+hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t ev[2]) {
     EncodeArgs a;
     a.text = p.text; a.str_off = p.str_off; a.cut_mask = p.cut_mask; a.n_str = p.n_str;
     a.staging = p.staging; a.staging16 = p.staging16; a.counts = p.counts; a.status = p.status; a.capped = p.capped;
@@ -1729,7 +1811,7 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     TrieView tv{p.slots, p.slot_ids, p.slots4, p.root_base, p.n_slots};
     const bool wide = (p.mode & DPT_MODE_MASK) == DPT_MODE_ATOMS;   // atoms of up to 8 bytes
 
-    hipLaunchKernelGGL(zero_first, dim3(1), dim3(64), 0, stream, p.id_off, p.retry_count);
+    if (p.n_str == 0) return hipMemsetAsync(p.id_off, 0, sizeof(uint64_t), stream);
     if (ev) {
         const hipError_t er = hipEventRecord(ev[0], stream);
         if (er != hipSuccess) return er;
@@ -1776,39 +1858,18 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
         const hipError_t er = hipEventRecord(ev[1], stream);
         if (er != hipSuccess) return er;
     }
-    if (p.n_str > 0) {
-        size_t tb = p.scan_temp_bytes;
-        hipError_t e = hipcub::DeviceScan::InclusiveSum(p.scan_temp, tb, p.counts, p.id_off + 1, (int)p.n_str, stream);
-        if (e != hipSuccess) return e;
-    }
-    if (ev) {
-        const hipError_t er = hipEventRecord(ev[2], stream);
-        if (er != hipSuccess) return er;
-    }
-    if (p.n_str > 0) {
-        uint64_t fb = (p.n_str + 63) / 64;
-        if (fb > (uint64_t)p.max_blocks / 2) fb = p.max_blocks / 2;   // 32 waves per CU
-        if (p.staging16)
-            hipLaunchKernelGGL(compact_flat_kernel<int16_t>, dim3((unsigned)fb), dim3(64), 0, stream, p.staging16, p.str_off, p.id_off, p.n_str, p.ids);
-        else
-            hipLaunchKernelGGL(compact_flat_kernel<int32_t>, dim3((unsigned)fb), dim3(64), 0, stream, p.staging, p.str_off, p.id_off, p.n_str, p.ids);
-    }
-    if (ev) {
-        const hipError_t er = hipEventRecord(ev[3], stream);
-        if (er != hipSuccess) return er;
-    }
+    FinishArgs f;
+    f.staging = p.staging16 ? (const void *)p.staging16 : (const void *)p.staging;
+    f.str_off = p.str_off; f.counts = p.counts; f.n_str = p.n_str; f.id_off = p.id_off; f.ids = p.ids;
+    f.flags = p.flags; f.ctr = p.retry_count; f.epoch = p.epoch;
+    const uint64_t fb = (p.n_str + 63) / 64;
+    if (p.staging16) hipLaunchKernelGGL(finish_kernel<int16_t>, dim3((unsigned)fb), dim3(256), 0, stream, f);
+    else hipLaunchKernelGGL(finish_kernel<int32_t>, dim3((unsigned)fb), dim3(256), 0, stream, f);
     return hipGetLastError();
 }
 
 size_t wsl_scratch_bytes(unsigned max_blocks) {
     return (size_t)max_blocks * 4 * GroupLDS<SMALL_CH, 16>::WSL_STRIDE;   // NG x stride covers both G at CH = 256
-}
-
-size_t scan_temp_bytes(uint64_t n_str) {
-    size_t tb = 0;
-    if (hipcub::DeviceScan::InclusiveSum(nullptr, tb, (uint64_t *)nullptr, (uint64_t *)nullptr, (int)(n_str ? n_str : 1), (hipStream_t)0) != hipSuccess)
-        return 0;
-    return tb;
 }
 
 hipError_t launch_histogram(const uint64_t *id_off, const int32_t *status, uint64_t n_str, int64_t *hist,

@@ -164,10 +164,11 @@ int dpt_dp_host(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uint8_t *t
 int dpt_token_histogram(const uint64_t *id_off, const int32_t *status, uint64_t n_str,
                         int64_t *hist, uint32_t n_bins, void *hip_stream);
 
-/* Per-ctx kernel timing with HIP events on the encode stream (for bench.py's roofline). */
+/* Per-ctx kernel timing with HIP events on the encode stream (for bench.py's roofline): one event
+ * pair per call around the tokenize passes (first pass, 2048-byte pass, unbounded pass). */
 int dpt_ctx_profile(dpt_ctx *c, int enable);
 /* Sums over calls since the last read (synchronises on the recorded events):
- * ms[0] tokenize kernel, ms[1] scan, ms[2] compact; *launches = tokenize launches. */
+ * ms[0] tokenize passes; ms[1], ms[2] = -1 (not timed); *launches = calls timed. */
 int dpt_ctx_profile_read(dpt_ctx *c, double *ms, uint64_t *launches);
 
 #ifdef __cplusplus

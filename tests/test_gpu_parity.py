@@ -397,3 +397,64 @@ def test_histogram_statuses_and_overflow(engines, oracles):
     assert h[nb] == counts.sum() and h[nb + 1] == n
     assert np.array_equal(h[nb + 2: nb + 7], np.bincount(np.clip(rst, 0, 4), minlength=5))
     assert h[nb + 4] > 0   # empty strings were counted under status 2
+
+
+def test_finish_lookback_sizes_and_repeats(engines, oracles):
+    """The finish kernel (decoupled look-back over 64-string batches, ticket order, epoch-tagged
+    flags, counters reset by the last batch) on one ctx across calls of changing sizes -- flags a
+    larger earlier call left behind must never be read as this call's -- against the C oracle."""
+    torch = pytest.importorskip("torch")
+    from dptok import synth
+    enc = engines["llama32k"]
+    s = torch.cuda.current_stream().cuda_stream
+    rng = np.random.default_rng(8)
+    for k, n in enumerate([70000, 1, 64, 65, 130, 4097, 70000, 3, 129]):
+        lens = rng.integers(0, 300, size=n)
+        texts = [synth.unpack(*synth.random_ascii_corpus(1, int(L), seed=1000 * k + i))[0] if L else "" for i, L in enumerate(lens[:64])]
+        text, offs = synth.random_ascii_corpus(n, 256, seed=77 + k)
+        if n > 64:   # ragged: drop a random tail of every string (empty strings included)
+            cut = rng.integers(0, 257, size=n)
+            parts = [text[i * 256:i * 256 + int(cut[i])].tobytes() for i in range(n)]
+            offs = np.zeros(n + 1, np.uint64)
+            offs[1:] = np.cumsum([len(p) for p in parts])
+            text = np.frombuffer(b"".join(parts) + b"\0", np.uint8)
+        else:
+            text, offs = _csr(texts[:n])
+        nb = int(offs[-1])
+        dt = torch.from_numpy(np.array(text)).cuda()
+        do = torch.from_numpy(offs.view(np.int64)).cuda()
+        ids = torch.empty(max(nb, 1), dtype=torch.int32, device="cuda")
+        io = torch.full((n + 1,), -7, dtype=torch.int64, device="cuda")
+        st = torch.empty(n, dtype=torch.int32, device="cuda")
+        enc.encode_device(dt.data_ptr(), nb, do.data_ptr(), n, ids.data_ptr(), max(nb, 1), io.data_ptr(), st.data_ptr(), stream=s)
+        torch.cuda.synchronize()
+        rids, roff, rst, _ = oracles["llama32k"].encode_csr(text, offs)
+        off_h = io.cpu().numpy().view(np.uint64)
+        assert np.array_equal(off_h, roff), (n, np.nonzero(off_h != roff)[0][:5])
+        assert np.array_equal(st.cpu().numpy(), rst)
+        assert np.array_equal(ids[: int(roff[-1])].cpu().numpy(), rids)
+
+
+def test_finish_epoch_wrap(engines, oracles):
+    """65 540 calls on one ctx: the 16-bit flag epoch wraps (the host clears the flags) and the
+    results stay exact."""
+    torch = pytest.importorskip("torch")
+    from dptok import synth
+    enc = engines["toy1k"]
+    n = 130
+    text, offs = synth.random_ascii_corpus(n, 16, seed=5)
+    nb = int(offs[-1])
+    dt = torch.from_numpy(np.array(text)).cuda()
+    do = torch.from_numpy(offs.view(np.int64)).cuda()
+    ids = torch.empty(nb, dtype=torch.int32, device="cuda")
+    io = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    st = torch.empty(n, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    rids, roff, rst, _ = oracles["toy1k"].encode_csr(text, offs)
+    for k in range(65540):
+        enc.encode_device(dt.data_ptr(), nb, do.data_ptr(), n, ids.data_ptr(), nb, io.data_ptr(), st.data_ptr(), stream=s)
+        if k % 8192 == 0 or k >= 65530:
+            torch.cuda.synchronize()
+            assert np.array_equal(io.cpu().numpy().view(np.uint64), roff), k
+            assert np.array_equal(ids[: int(roff[-1])].cpu().numpy(), rids), k
+            assert np.array_equal(st.cpu().numpy(), rst), k

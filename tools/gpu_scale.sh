@@ -20,5 +20,5 @@ timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 
     bench.py --gpus 2 --steps 10 --warmup 3 --no-cpu-baseline --dist-backend gloo > $out/rehearse_2rank.log 2>&1 || { tail -20 $out/rehearse_2rank.log; exit 1; }
 grep '^{' $out/rehearse_2rank.log > $out/rehearse_2rank.json
 for f in $out/bench_*.json $out/rehearse_2rank.json; do
-  python3 -c "import json,sys; d=json.loads(open('$f').read()); print('$f', '%.2f GB/s' % (d['value']/1e9), 'ms/step %.3f' % d['ms_per_step'], 'exact', d['exact_match']['rate'], d['exact_match']['sample'], 'stages', {k: round(v,3) for k,v in d['stage_ms_per_step'].items()}, 'frac %.4f' % d['roofline']['frac'])"
+  python3 -c "import json,sys; d=json.loads(open('$f').read()); print('$f', '%.2f GB/s' % (d['value']/1e9), 'ms/step %.3f' % d['ms_per_step'], 'exact', d['exact_match']['rate'], d['exact_match']['sample'], 'stages', d['stage_ms_per_step'], 'frac %.4f' % d['roofline']['frac'])"
 done
