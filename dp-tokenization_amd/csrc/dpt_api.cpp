@@ -475,7 +475,7 @@ static int encode_host_impl(dpt_ctx *c, const dpt_vocab *v, int mode, const uint
             return hip_fail(e, "D2H counters");
         if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(e, "sync");
         uint64_t used = 0;
-        memcpy(&used, c->p_out + o_ctr + 40, sizeof(used));   // the call's claimed bytes (finish_kernel)
+        if (n_str) memcpy(&used, c->p_out + o_ctr + 40, sizeof(used));   // the call's claimed bytes (finish_kernel)
         if (used > n_bytes) return fail(DPT_E_HIP, "unbounded pass counter out of range");   // never expected
         if (used <= c->arena_cap) break;
         // the unbounded pass's arena was too small for the strings routed to it (those strings got

@@ -1811,7 +1811,12 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     TrieView tv{p.slots, p.slot_ids, p.slots4, p.root_base, p.n_slots};
     const bool wide = (p.mode & DPT_MODE_MASK) == DPT_MODE_ATOMS;   // atoms of up to 8 bytes
 
-    if (p.n_str == 0) return hipMemsetAsync(p.id_off, 0, sizeof(uint64_t), stream);
+    if (p.n_str == 0) {
+        // no finish kernel runs: id_off[0] = 0, and the call's claimed arena bytes ("last need") are 0
+        const hipError_t e0 = hipMemsetAsync(p.id_off, 0, sizeof(uint64_t), stream);
+        if (e0 != hipSuccess) return e0;
+        return hipMemsetAsync(reinterpret_cast<uint64_t *>(p.retry_count) + CTR_LASTNEED64, 0, sizeof(uint64_t), stream);
+    }
     if (ev) {
         const hipError_t er = hipEventRecord(ev[0], stream);
         if (er != hipSuccess) return er;
