@@ -28,7 +28,7 @@ struct EncodeLaunch {
     uint8_t *wsl_scratch;    // max_blocks x wsl_scratch_bytes(1) bytes
     int long_span;           // vocabulary tokens longer than 64 code points: words over 64 atoms -> unbounded pass
     uint32_t max_tok_bytes;  // longest vocabulary token, bytes
-    unsigned long long *flags;   // finish kernel's look-back flags, one per 64 strings
+    unsigned long long *flags;   // finish kernel's look-back flags (sized one per 64 strings; one per FIN_BATCH used)
     unsigned epoch;              // the ctx's call counter (1..65535)
     unsigned max_blocks;
     int variant;             // KERNEL_* below

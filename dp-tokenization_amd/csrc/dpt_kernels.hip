@@ -1582,17 +1582,22 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
 
 // Counter block (EncodeLaunch::retry_count, 64 bytes; zeroed once at allocation, then reset for the
 // next call by the finish kernel's last block): uint32 [0] retry count, [1] first-pass work, [2]
-// 2048-byte pass work, [3] long count, [4] long work, [5] finish ticket; uint64 [4] (byte 32) the
-// unbounded pass's claimed bytes, [5] (byte 40) the last call's claimed bytes (dpt_ctx_long_need),
-// [6] (byte 48) far edges listed (dpt_dp_host_far).
-constexpr unsigned CTR_TICKET = 5;
+// 2048-byte pass work, [3] long count, [4] long work, [5] finish ticket, [6] finish blocks done;
+// uint64 [4] (byte 32) the unbounded pass's claimed bytes, [5] (byte 40) the last call's claimed
+// bytes (dpt_ctx_long_need), [6] (byte 48) far edges listed (dpt_dp_host_far).
+constexpr unsigned CTR_TICKET = 5, CTR_DONE = 6;
 constexpr unsigned CTR_ARENA64 = 4, CTR_LASTNEED64 = 5;
+constexpr unsigned FIN_BATCH = 256;   // strings per finish batch = threads per finish block
 
-// Look-back flags, one uint64 per 64-string batch: epoch (16 bits, the ctx's call counter; 0 never
-// used, the host clears the array when it wraps) | state (2 bits: 1 = batch aggregate, 2 = inclusive
-// prefix) | value (46 bits of ids).
+// Look-back flags, one uint64 per FIN_BATCH-string batch: epoch (16 bits, the ctx's call counter; 0
+// never used, the host clears the array when it wraps) | state (2 bits: 1 = batch aggregate, 2 =
+// inclusive prefix) | value (46 bits of ids).
 __device__ __forceinline__ uint64_t flag_pack(unsigned epoch, unsigned st, uint64_t v) {
     return ((uint64_t)epoch << 48) | ((uint64_t)st << 46) | v;
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, unsigned l) {
+    return uni64(((uint64_t)__builtin_amdgcn_readlane((unsigned)(v >> 32), l) << 32) | __builtin_amdgcn_readlane((unsigned)v, l));
 }
 
 // 64-bit inclusive add-scan over the wave (ds_bpermute shifts)
@@ -1619,100 +1624,127 @@ struct FinishArgs {
     unsigned epoch;
 };
 
-// One block of 256 threads per 64 consecutive strings, in ticket order (a block waits only for
-// batches whose tickets were taken before its own, so by blocks already running): wave 0 scans the
-// batch's counts, publishes the aggregate, looks back over the earlier batches' flags for its
-// exclusive offset (decoupled look-back) and publishes the inclusive prefix; then the four waves
-// copy the batch's staged ids -- lanes over the batch's OUTPUT ids, so every store is a coalesced
-// row -- 8 independent loads in flight per lane.  Replaces the counter reset, the offset scan and
-// the compaction of round 1 (three launches and two more passes over the counts).
+// Exclusive id offset of batch t (t > 0) by decoupled look-back, one wave: lane l reads batch
+// jb - l's flag; once every batch from jb down to the nearest inclusive prefix in the window has
+// published, their values are summed (no prefix in the window: all 64 aggregates, then the next
+// window).  Batches before t hold tickets taken before t's, by blocks already running, so every
+// flag it waits for is published without t's help.
+__device__ __forceinline__ uint64_t finish_lookback(const FinishArgs &f, uint64_t t, unsigned lane) {
+    uint64_t excl = 0, jb = t - 1;
+    for (unsigned spin = 0;;) {
+        const bool in = lane <= jb;
+        const uint64_t fl = in ? __hip_atomic_load(&f.flags[jb - lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                               : flag_pack(f.epoch, 2, 0);
+        const unsigned st = (fl >> 48) == f.epoch ? (unsigned)(fl >> 46) & 3u : 0u;
+        const uint64_t pm = ballot(st == 2), ready = ballot(st != 0);
+        const unsigned p = pm ? (unsigned)__builtin_ctzll(pm) : 64u;   // nearest prefix in the window
+        const uint64_t need = p < 63 ? ((2ull << p) - 1) : ~0ull;      // lanes 0..p
+        if ((ready & need) != need) {                                  // not all published yet
+            __builtin_amdgcn_s_sleep(1);
+            if (++spin > (1u << 24)) return excl;   // never expected: bounded, so a broken protocol cannot hang the GPU
+            continue;
+        }
+        const uint64_t v = wave_incl_scan_add64((lane <= p && in) ? (fl & ((1ull << 46) - 1)) : 0ull, lane);
+        excl += readlane64(v, 63);
+        if (p < 64) return excl;
+        jb -= 64;
+        spin = 0;
+    }
+}
+
+// Offsets and CSR ids in one launch: a grid of at most 8 blocks per CU, FIN_BATCH threads each,
+// takes FIN_BATCH-string batches in ticket order.  Per batch: one count per thread, a block scan
+// (wave scans + the four wave sums in LDS); wave 0 publishes the batch aggregate, finds the batch's
+// first id by look-back and publishes the inclusive prefix; every thread writes its string's end
+// offset; then the block copies the batch's staged ids -- threads over the batch's OUTPUT ids, so
+// every store is a coalesced row -- FIN_U independent loads in flight per thread.  The last block
+// to finish resets the counter block for the next call.  Replaces round 1's counter reset, offset
+// scan and compaction (three launches, two more passes over the counts); a persistent grid because
+// one block per 64 strings spent more time dispatching blocks and chaining look-backs (0.19 ms per
+// 1M strings without any copy) than copying.
 template <typename ST>
-__global__ void __launch_bounds__(256) finish_kernel(FinishArgs f) {
-    __shared__ uint64_t s_rel[65];   // ids of the batch's strings before string k, + the batch total
-    __shared__ uint64_t s_src[64];   // staging element of each string's first id
-    __shared__ uint64_t s_base;      // the batch's first id
+__global__ void __launch_bounds__(FIN_BATCH) finish_kernel(FinishArgs f) {
+    __shared__ uint64_t s_rel[FIN_BATCH + 1];   // ids of the batch's strings before string k, + the batch total
+    __shared__ uint64_t s_src[FIN_BATCH];       // staging element of each string's first id
+    __shared__ uint64_t s_wsum[FIN_BATCH / 64];
+    __shared__ uint64_t s_base;                 // the batch's first id
     __shared__ unsigned s_ticket;
-    const unsigned tid = threadIdx.x, lane = tid & 63u;
-    const uint64_t n_batches = (f.n_str + 63) / 64;
+    const unsigned tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+    const uint64_t n_batches = (f.n_str + FIN_BATCH - 1) / FIN_BATCH;
+    const uint64_t base_off = f.str_off[0];
+    const ST *__restrict__ staging = reinterpret_cast<const ST *>(f.staging);
+    for (;;) {
+        if (tid == 0) s_ticket = atomicAdd(&f.ctr[CTR_TICKET], 1u);
+        __syncthreads();
+        const uint64_t t = s_ticket;
+        if (t >= n_batches) break;
+        const uint64_t s0 = t * FIN_BATCH;
+        const bool has = tid < f.n_str - s0;
+        const uint64_t c = has ? f.counts[s0 + tid] : 0ull;
+        const uint64_t src = has ? f.str_off[s0 + tid] - base_off : 0ull;
+        uint64_t incl = wave_incl_scan_add64(c, lane);
+        if (lane == 63) s_wsum[w] = incl;
+        __syncthreads();
+        uint64_t agg = 0;
+#pragma unroll
+        for (unsigned k = 0; k < FIN_BATCH / 64; k++) {
+            const uint64_t ws = s_wsum[k];
+            if (k < w) incl += ws;
+            agg += ws;
+        }
+        if (w == 0) {
+            uint64_t excl = 0;
+            if (t == 0) {
+                if (lane == 0) __hip_atomic_store(&f.flags[0], flag_pack(f.epoch, 2, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                if (lane == 0) __hip_atomic_store(&f.flags[t], flag_pack(f.epoch, 1, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                excl = finish_lookback(f, t, lane);
+                if (lane == 0) __hip_atomic_store(&f.flags[t], flag_pack(f.epoch, 2, excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (lane == 0) s_base = excl;
+        }
+        s_rel[tid] = incl - c;
+        if (tid == FIN_BATCH - 1) s_rel[FIN_BATCH] = incl;
+        s_src[tid] = src;
+        __syncthreads();
+        const uint64_t o0 = s_base, total = agg;
+        if (has) f.id_off[s0 + tid + 1] = o0 + incl;
+        if (t == 0 && tid == 0) f.id_off[0] = 0;
+#ifndef FIN_U
+#define FIN_U 16
+#endif
+        constexpr unsigned U = FIN_U;
+        unsigned j = 0;   // the string of this thread's current id (monotone in k)
+        for (uint64_t k0 = 0; k0 < total; k0 += FIN_BATCH * U) {
+            int32_t v[U];
+#pragma unroll
+            for (unsigned u = 0; u < U; u++) {
+                const uint64_t k = k0 + (uint64_t)u * FIN_BATCH + tid;
+                v[u] = 0;
+                if (k < total) {
+                    while (s_rel[j + 1] <= k) j++;
+                    v[u] = (int32_t)staging[s_src[j] + (k - s_rel[j])];
+                }
+            }
+#pragma unroll
+            for (unsigned u = 0; u < U; u++) {
+                const uint64_t k = k0 + (uint64_t)u * FIN_BATCH + tid;
+                if (k < total) f.ids[o0 + k] = v[u];
+            }
+        }
+        __syncthreads();   // s_rel / s_src / s_ticket are rewritten for the next batch
+    }
     if (tid == 0) {
-        const unsigned t = atomicAdd(&f.ctr[CTR_TICKET], 1u);
-        if ((uint64_t)t + 1 == n_batches) {
-            // the last ticket: every block has its batch, and every tokenize pass is done -- reset
-            // the counters for the next call (the claimed arena bytes stay readable as "last need")
+        const unsigned d = atomicAdd(&f.ctr[CTR_DONE], 1u);
+        if (d + 1 == gridDim.x) {
+            // the last block out: every ticket is taken and every tokenize pass is done -- reset the
+            // counters for the next call (the claimed arena bytes stay readable as "last need")
             uint64_t *c64 = reinterpret_cast<uint64_t *>(f.ctr);
             c64[CTR_LASTNEED64] = c64[CTR_ARENA64];
             c64[CTR_ARENA64] = 0;
             f.ctr[0] = 0; f.ctr[1] = 0; f.ctr[2] = 0; f.ctr[3] = 0; f.ctr[4] = 0;
-            __hip_atomic_store(&f.ctr[CTR_TICKET], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        s_ticket = t;
-    }
-    __syncthreads();
-    const uint64_t t = s_ticket;
-    const uint64_t s0 = t * 64;
-    const unsigned cnt = (unsigned)min((uint64_t)64, f.n_str - s0);
-    if (tid < 64) {
-        const uint64_t c = lane < cnt ? f.counts[s0 + lane] : 0ull;
-        const uint64_t incl = wave_incl_scan_add64(c, lane);
-        const uint64_t agg = uni64(((uint64_t)__builtin_amdgcn_readlane((unsigned)(incl >> 32), 63) << 32) |
-                                   __builtin_amdgcn_readlane((unsigned)incl, 63));
-        uint64_t excl = 0;
-        if (t == 0) {
-            if (lane == 0) __hip_atomic_store(&f.flags[0], flag_pack(f.epoch, 2, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            if (lane == 0) __hip_atomic_store(&f.flags[t], flag_pack(f.epoch, 1, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            // look back 64 batches at a time: lane l reads batch jb - l; sum up to the nearest
-            // inclusive prefix once every batch before it in the window has published
-            uint64_t jb = t - 1;
-            for (unsigned spin = 0;;) {
-                const bool in = lane <= jb;
-                uint64_t fl = in ? __hip_atomic_load(&f.flags[jb - lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : flag_pack(f.epoch, 2, 0);
-                const unsigned st = (fl >> 48) == f.epoch ? (unsigned)(fl >> 46) & 3u : 0u;
-                const uint64_t pm = ballot(st == 2), ready = ballot(st != 0);
-                const unsigned p = pm ? (unsigned)__builtin_ctzll(pm) : 64u;          // nearest prefix in the window
-                const uint64_t need = p < 63 ? ((2ull << p) - 1) : ~0ull;             // lanes 0..p
-                if ((ready & need) != need) {                                         // not all published yet
-                    __builtin_amdgcn_s_sleep(1);
-                    if (++spin > (1u << 24)) break;   // never expected: bounded, so a broken protocol cannot hang the GPU
-                    continue;
-                }
-                uint64_t v = (lane <= p && in) ? (fl & ((1ull << 46) - 1)) : 0ull;
-                v = wave_incl_scan_add64(v, lane);
-                excl += uni64(((uint64_t)__builtin_amdgcn_readlane((unsigned)(v >> 32), 63) << 32) |
-                              __builtin_amdgcn_readlane((unsigned)v, 63));
-                if (p < 64) break;
-                jb -= 64;   // 64 aggregates, no prefix yet: the next window
-                spin = 0;
-            }
-            if (lane == 0) __hip_atomic_store(&f.flags[t], flag_pack(f.epoch, 2, excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        if (lane < cnt) f.id_off[s0 + lane + 1] = excl + incl;
-        if (t == 0 && lane == 0) f.id_off[0] = 0;
-        s_rel[lane] = incl - c;
-        if (lane == 63) s_rel[64] = incl;
-        s_src[lane] = lane < cnt ? f.str_off[s0 + lane] - f.str_off[0] : 0ull;
-        if (lane == 0) s_base = excl;
-    }
-    __syncthreads();
-    const ST *__restrict__ staging = reinterpret_cast<const ST *>(f.staging);
-    const uint64_t total = s_rel[64], o0 = s_base;
-    unsigned j = 0;   // the string of this thread's current id (monotone in k)
-    constexpr unsigned U = 8;
-    for (uint64_t k0 = 0; k0 < total; k0 += 256u * U) {
-        int32_t v[U];
-#pragma unroll
-        for (unsigned u = 0; u < U; u++) {
-            const uint64_t k = k0 + (uint64_t)u * 256u + tid;
-            v[u] = 0;
-            if (k < total) {
-                while (s_rel[j + 1] <= k) j++;
-                v[u] = (int32_t)staging[s_src[j] + (k - s_rel[j])];
-            }
-        }
-#pragma unroll
-        for (unsigned u = 0; u < U; u++) {
-            const uint64_t k = k0 + (uint64_t)u * 256u + tid;
-            if (k < total) f.ids[o0 + k] = v[u];
+            f.ctr[CTR_TICKET] = 0;
+            f.ctr[CTR_DONE] = 0;
         }
     }
 }
@@ -1867,9 +1899,10 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     f.staging = p.staging16 ? (const void *)p.staging16 : (const void *)p.staging;
     f.str_off = p.str_off; f.counts = p.counts; f.n_str = p.n_str; f.id_off = p.id_off; f.ids = p.ids;
     f.flags = p.flags; f.ctr = p.retry_count; f.epoch = p.epoch;
-    const uint64_t fb = (p.n_str + 63) / 64;
-    if (p.staging16) hipLaunchKernelGGL(finish_kernel<int16_t>, dim3((unsigned)fb), dim3(256), 0, stream, f);
-    else hipLaunchKernelGGL(finish_kernel<int32_t>, dim3((unsigned)fb), dim3(256), 0, stream, f);
+    uint64_t fb = (p.n_str + FIN_BATCH - 1) / FIN_BATCH;
+    if (fb > p.max_blocks / 8) fb = p.max_blocks / 8;   // max_blocks = CUs x 64: at most 8 blocks per CU
+    if (p.staging16) hipLaunchKernelGGL(finish_kernel<int16_t>, dim3((unsigned)fb), dim3(FIN_BATCH), 0, stream, f);
+    else hipLaunchKernelGGL(finish_kernel<int32_t>, dim3((unsigned)fb), dim3(FIN_BATCH), 0, stream, f);
     return hipGetLastError();
 }
 
