@@ -41,8 +41,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=["cfg2", "cfg4", "cfg5"], default="cfg2",
-                    help="cfg2 (the metric's config): 256-byte random ASCII; cfg4: S2ORC-shaped; cfg5: Arabic-shaped")
+    ap.add_argument("--workload", choices=["cfg2", "cfg4", "cfg5", "bloom"], default="cfg2",
+                    help="cfg2 (the metric's config): 256-byte random ASCII; cfg4: S2ORC-shaped; cfg5: Arabic-shaped; "
+                         "bloom: row f3 at BLOOM scale (250,680-entry byte-level BPE, atoms mode, <= 256-byte strings)")
     ap.add_argument("--strings", type=int, default=None,
                     help="strings of the global corpus (strong) or per GPU (weak); default 1M (cfg4: 200k)")
     ap.add_argument("--scaling", choices=["strong", "weak"], default=None,
@@ -52,7 +53,11 @@ def parse():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--exact-sample", type=int, default=None,
                     help="strings checked against the C oracle (rank 0; default: every string of the rank's shard)")
-    ap.add_argument("--cpu-sample", type=int, default=2048, help="strings for the reference-port CPU baseline")
+    ap.add_argument("--cpu-sample", type=int, default=None,
+                    help="strings for the reference-port CPU baseline (default 2048; bloom 65536 -- bounded by --cpu-budget)")
+    ap.add_argument("--gen-procs", type=int, default=None,
+                    help="processes for the synthetic corpus (default: the CPU share, at most 16; 1 under a profiler "
+                         "that follows forks)")
     ap.add_argument("--cpu-budget", type=float, default=25.0, help="seconds of CPU-baseline wall time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--host-path", action="store_true",
@@ -62,6 +67,11 @@ def parse():
                     help="nccl (RCCL, the real path) or gloo -- gloo lets a rehearsal put several ranks "
                          "on one GPU (device = local_rank mod visible GPUs)")
     return ap.parse_args()
+
+
+def log(msg: str) -> None:
+    """Progress on stderr (the JSON line stays the only stdout line)."""
+    print("bench: " + msg, file=sys.stderr, flush=True)
 
 
 def exact_matches(ids_h, off_h, st_h, rids, roff, rst, S: int) -> int:
@@ -89,36 +99,65 @@ def exact_matches(ids_h, off_h, st_h, rids, roff, rst, S: int) -> int:
 _PORT = {}
 
 
-def _port_init():
+def _port_init(bloom: bool = False):
     from dptok import synth
     from oracle import ref_port
-    _PORT["t2i"] = synth.llama_shaped_vocab()
-    _PORT["f"] = ref_port.dp_tokenize_raw
+    if bloom:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from bloom_fixture import big_vocab
+        _PORT["t2i"] = big_vocab()
+        _PORT["f"] = ref_port.dp_tokenize_word_atoms
+    else:
+        _PORT["t2i"] = synth.llama_shaped_vocab()
+        _PORT["f"] = ref_port.dp_tokenize_raw
 
     def _alarm(signum, frame):
         raise TimeoutError()
     signal.signal(signal.SIGALRM, _alarm)
 
 
-def _port_one(text):
+def _port_one(item):
     signal.alarm(10)
     try:
-        _PORT["f"](text, _PORT["t2i"])
+        x = item[0]
+        if isinstance(x, tuple):   # bloom: (bytes, cut bytes) -> words of atoms, in the worker
+            b, c = x
+            x = words_of_atoms(np.frombuffer(b, np.uint8), np.array([0, len(b)], np.uint64), np.frombuffer(c, np.uint8))[0]
+        _PORT["f"](x, _PORT["t2i"])
         ok = True
     except TimeoutError:
         ok = False
     finally:
         signal.alarm(0)
-    return len(text.encode()), ok
+    return item[1], ok
 
 
-def cpu_baseline(texts, budget, cores):
-    """The reference's enumerate-then-select DP (oracle/ref_port.py) on `cores` processes."""
+def words_of_atoms(text: np.ndarray, offs: np.ndarray, cut: np.ndarray) -> list:
+    """Atoms-mode buffers -> per string, words of atoms (cut bit 1: atom start, bit 0: word start)."""
+    out = []
+    raw = text.tobytes()
+    for i in range(len(offs) - 1):
+        a, b = int(offs[i]), int(offs[i + 1])
+        words, atoms, p0 = [], [], a
+        for p in range(a + 1, b + 1):
+            if p == b or cut[p] & 2:
+                atoms.append(raw[p0:p].decode("utf-8"))
+                p0 = p
+                if p == b or cut[p] & 1:
+                    words.append(atoms)
+                    atoms = []
+        out.append(words)
+    return out
+
+
+def cpu_baseline(items, budget, cores, bloom=False):
+    """The reference's enumerate-then-select DP (oracle/ref_port.py) on `cores` processes; items =
+    (input, bytes) pairs."""
     done_bytes, n_done, n_to = 0, 0, 0
     ctx = mp.get_context("fork")
-    with ctx.Pool(cores, initializer=_port_init) as pool:
+    with ctx.Pool(cores, initializer=_port_init, initargs=(bloom,)) as pool:
         t0 = time.perf_counter()
-        it = pool.imap_unordered(_port_one, texts, chunksize=4)
+        it = pool.imap_unordered(_port_one, items, chunksize=4)
         for nb, ok in it:
             if ok:
                 done_bytes += nb
@@ -227,16 +266,31 @@ def main():
     scaling = args.scaling or "strong"   # N = 1: strong and weak are the same run
     from dptok import Encoder, Vocab, synth
     from dptok import dist as ddist
-    t2i = synth.llama_shaped_vocab()
+    bloom = args.workload == "bloom"
+    if bloom:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from bloom_fixture import big_vocab
+        t2i = big_vocab()
+    else:
+        t2i = synth.llama_shaped_vocab()
     Lb = args.length
     cores, cpus_visible = cpu_share()
-    gen_procs = max(1, min(16, cores))
-    default_n = 200_000 if args.workload == "cfg4" else 1_000_000
+    gen_procs = args.gen_procs or max(1, min(16, cores))
+    if args.cpu_sample is None:
+        args.cpu_sample = 262144 if bloom else 2048
+    default_n = {"cfg4": 200_000, "bloom": 500_000}.get(args.workload, 1_000_000)
     N = args.strings or default_n
     lo, hi = rank_strings(N, rank, world, scaling)
     M = hi - lo
     per = "corpus, sharded over the GPUs" if scaling == "strong" else "per GPU"
-    if args.workload == "cfg2":
+    cut = None
+    if bloom:
+        text, offs, cut = synth.bloom_like_parallel(M, t2i, start=lo, procs=gen_procs, length=Lb)
+        wl = (f"bloom: {N // 1000}k x <= {Lb}-byte pre-tokenized byte-level strings {per}, atoms mode, "
+              "BLOOM-scale vocabulary")
+        data = ("synthetic byte-level words (dptok.synth.bloom_like_corpus: 15% tokens > 16 code points); synthetic "
+                "250,680-entry byte-level BPE (tests/golden/bloom_big_tokenizer.json.xz)")
+    elif args.workload == "cfg2":
         text, offs = synth.random_ascii_corpus(M, Lb, seed=args.seed, start=lo)
         wl = f"cfg2: {N // 1000}k x {Lb}-byte random ASCII strings {per}, raw pre-tokenization"
         data = "synthetic random printable ASCII (Philox keyed by seed+global index); synthetic Llama-shaped 32k vocab"
@@ -249,11 +303,19 @@ def main():
         wl = f"cfg5: {N // 1000}k x ~{Lb}-byte Arabic-shaped strings {per} (2-byte code points), raw"
         data = "synthetic Arabic-shaped UTF-8 (dptok.synth.arabic_corpus); synthetic Llama-shaped 32k vocab + Arabic letters"
     Lb = int(offs[-1]) // max(M, 1)
+    log(f"corpus ready: {M} strings, {int(offs[-1])} bytes")
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # before any GPU call: the pool forks plain CPU workers
-        texts = synth.unpack(text[: int(offs[args.cpu_sample])], offs[: args.cpu_sample + 1])
-        v, nd, nto, cdt = cpu_baseline(texts, args.cpu_budget, cores)
+        args.cpu_sample = min(args.cpu_sample, M)
+        sub = offs[: args.cpu_sample + 1]
+        if bloom:
+            tb, cb = text.tobytes(), cut.tobytes()
+            inputs = [(tb[int(sub[i]):int(sub[i + 1])], cb[int(sub[i]):int(sub[i + 1])]) for i in range(args.cpu_sample)]
+        else:
+            inputs = synth.unpack(text[: int(offs[args.cpu_sample])], sub)
+        items = list(zip(inputs, np.diff(sub).astype(int).tolist()))
+        v, nd, nto, cdt = cpu_baseline(items, args.cpu_budget, cores, bloom)
         cpu = {"value": v, "unit": "bytes/s", "cores": cores, "host_cpus_visible": cpus_visible, "kind": "port",
                "sample": f"{nd} of the first {args.cpu_sample} {args.workload} strings in {cdt:.1f}s "
                          f"(enumerate-then-select, oracle/ref_port.py, {cores} processes = the box's CPU share "
@@ -271,6 +333,7 @@ def main():
     n_bytes = int(offs[-1] - offs[0])
     d_text = torch.from_numpy(text).to(dev)
     d_off = torch.from_numpy(offs.view(np.int64)).to(dev)
+    d_cut = torch.from_numpy(cut).to(dev) if cut is not None else None
     d_ids = torch.empty(max(n_bytes, 1), dtype=torch.int32, device=dev)
     d_idoff = torch.empty(M + 1, dtype=torch.int64, device=dev)
     d_status = torch.empty(max(M, 1), dtype=torch.int32, device=dev)
@@ -280,7 +343,8 @@ def main():
 
     def step():
         enc.encode_device(d_text.data_ptr(), n_bytes, d_off.data_ptr(), M, d_ids.data_ptr(), max(n_bytes, 1),
-                          d_idoff.data_ptr(), d_status.data_ptr(), stream=stream)
+                          d_idoff.data_ptr(), d_status.data_ptr(), stream=stream,
+                          cut_ptr=d_cut.data_ptr() if bloom else 0, mode="atoms" if bloom else "raw")
         d_hist.zero_()
         enc.histogram_device(d_idoff.data_ptr(), d_status.data_ptr(), M, d_hist.data_ptr(), N_BINS, stream=stream)
         if world > 1:   # the single collective: RCCL over xGMI with nccl, gloo in rehearsals
@@ -298,6 +362,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         return float(t.item())
 
+    log("GPU ready, warmup")
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -336,6 +401,7 @@ def main():
     alg_staged = algorithmic_bytes(n_bytes, M, n_tok_rank, id_bytes)
     achieved = alg_bytes / (k_ms * 1e-3) / 1e9
 
+    log(f"timed {args.steps} steps in {dt:.4f} s; exact-match check")
     # exact match vs the CPU DP (C oracle): every rank checks its own shard, counts are summed
     from oracle import oracle
     per_rank_threads = max(1, cores // max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1"))))
@@ -344,7 +410,8 @@ def main():
     off_h = d_idoff.cpu().numpy().view(np.uint64)
     st_h = d_status.cpu().numpy()
     ov = oracle.OracleVocab(t2i)
-    rids, roff, rst, _ = ov.encode_csr(text, offs[: S + 1], nthreads=per_rank_threads)
+    omode = oracle.ATOMS if bloom else oracle.RAW
+    rids, roff, rst, _ = ov.encode_csr(text, offs[: S + 1], mode=omode, cut_mask=cut, nthreads=per_rank_threads)
     same = exact_matches(ids_h, off_h, st_h, rids, roff, rst, S)
     same_all, checked_all = all_sum(float(same)), all_sum(float(S))
     exact = {"rate": same_all / max(checked_all, 1.0), "sample": int(checked_all), "checker": "oracle/dp_oracle.c",
@@ -352,7 +419,7 @@ def main():
     if rank == 0 and cpu is not None:
         t0c = time.perf_counter()
         S2 = min(65536, M)
-        ov.encode_csr(text, offs[: S2 + 1], nthreads=cores)
+        ov.encode_csr(text, offs[: S2 + 1], mode=omode, cut_mask=cut, nthreads=cores)
         cpu["c_restatement_bytes_per_s"] = int(offs[S2]) / (time.perf_counter() - t0c)
         cpu["c_restatement_threads"] = cores
 
@@ -373,7 +440,8 @@ def main():
             "dtype": "u8",
             "data": data,
             "config": {"workload": wl, "strings_total": strings_all,
-                       "strings_per_gpu": M, "bytes_per_string": Lb, "vocab": "synthetic llama-shaped 32000",
+                       "strings_per_gpu": M, "bytes_per_string": Lb,
+                       "vocab": "synthetic byte-level BPE 250680" if bloom else "synthetic llama-shaped 32000",
                        "parallelism": f"dp{world} ({scaling} scaling: corpus shards, 1 all-reduce of the histogram per step)"},
             "per_gpu_bytes_per_s": value / world,
             "tokens_per_byte": n_tok_all / max(bytes_all, 1.0),
@@ -383,7 +451,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic_for(M, Lb) if (args.workload == "cfg2" and world == 1) else None,
-                         "kernel": "tokenize_kernel<256,16,false,false,%d>" % (1 if id_bytes == 2 else 2),
+                         "kernel": ("tokenize_kernel<256,64,false,true>" if bloom else
+                                    "tokenize_kernel<256,16,false,false,%d>" % (1 if id_bytes == 2 else 2)),
                          "alg_bytes_per_launch": alg_bytes,
                          "alg_bytes_formula": "N_in + 4*N_tok + 8(N+1) + 8(N+1) + 4N (SURVEY.md 8d)",
                          "alg_bytes_staged_width": alg_staged, "staged_id_bytes": id_bytes,

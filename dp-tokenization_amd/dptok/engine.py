@@ -102,6 +102,31 @@ class Vocab:
             self.handle = None
 
 
+def pack_word_atoms(strings: Sequence[Sequence[Sequence[str]]]) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """Strings given as words of atoms -> DPT_MODE_ATOMS buffers (text u8, offsets u64[n+1], cut
+    mask u8: bit 1 at every atom's first byte, bit 0 at every word's).  Raises ValueError for an
+    empty atom or an empty word."""
+    parts, cuts, offs = [], [], [0]
+    for words in strings:
+        n = 0
+        for atoms in words:
+            for k, a in enumerate(atoms):
+                e = encode_utf8(a)
+                if not e:
+                    raise ValueError("empty atom")
+                c = bytearray(len(e))
+                c[0] = 3 if k == 0 else 2          # bit 1: atom start, bit 0: word start
+                parts.append(e)
+                cuts.append(bytes(c))
+                n += len(e)
+            if not atoms:
+                raise ValueError("empty word")
+        offs.append(offs[-1] + n)
+    text = np.frombuffer(b"".join(parts) + b"\0", dtype=np.uint8)
+    cut = np.frombuffer(b"".join(cuts) + b"\0", dtype=np.uint8)
+    return text, np.array(offs, dtype=np.uint64), cut
+
+
 class Encoder:
     """Batch shortest-tokenization on one GPU (one workspace; use from one stream at a time)."""
 
@@ -191,25 +216,7 @@ class Encoder:
         """Strings given as words of atoms (DPT_MODE_ATOMS), one launch for the batch: per string
         (ids, status).  A string with no words gives ([], ok) -- the BLOOM adapter's empty input
         (reference tokenizer_utils.py:166-178 loops over zero words)."""
-        parts, cuts, offs = [], [], [0]
-        for words in strings:
-            n = 0
-            for atoms in words:
-                for k, a in enumerate(atoms):
-                    e = encode_utf8(a)
-                    if not e:
-                        raise ValueError("empty atom")
-                    c = bytearray(len(e))
-                    c[0] = 3 if k == 0 else 2          # bit 1: atom start, bit 0: word start
-                    parts.append(e)
-                    cuts.append(bytes(c))
-                    n += len(e)
-                if not atoms:
-                    raise ValueError("empty word")
-            offs.append(offs[-1] + n)
-        text = np.frombuffer(b"".join(parts) + b"\0", dtype=np.uint8)
-        cut = np.frombuffer(b"".join(cuts) + b"\0", dtype=np.uint8)
-        o = np.array(offs, dtype=np.uint64)
+        text, o, cut = pack_word_atoms(strings)
         ids, id_off, st, _ = self.encode_csr(text, o, mode="atoms", cut_mask=cut)
         out = []
         for i, words in enumerate(strings):

@@ -216,3 +216,80 @@ def generate_parallel(kind: str, n: int, start: int = 0, procs: int = 8, **kw) -
     offs = np.zeros(n + 1, dtype=np.uint64)
     offs[1:] = np.cumsum(lens, dtype=np.uint64)
     return np.concatenate(texts), offs
+
+
+# --------------------------------------------------------------------------- BLOOM-scale (row f3)
+
+BYTE_SPACE = "Ġ"   # 'Ġ': the byte-level alphabet's space (GPT-2 bytes_to_unicode)
+
+
+def bloom_word_pool(vocab: Dict[str, int]) -> Tuple[List[str], List[str]]:
+    """(long, short): the vocabulary's all-ASCII-letter tokens (a leading 'Ġ' dropped), longer
+    than 16 code points and 2..16 -- the words of ``bloom_like_corpus``."""
+    words = sorted({t[1:] if t.startswith(BYTE_SPACE) else t for t in vocab})
+    words = [w for w in words if w.isascii() and w.isalpha()]
+    return [w for w in words if len(w) > 16], [w for w in words if 2 <= len(w) <= 16]
+
+
+def bloom_like_corpus(n: int, vocab_or_pool, length: int = 256, seed: int = 8,
+                      start: int = 0) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """The BLOOM-scale workload (``bench.py --workload bloom``): ``n`` pre-tokenized byte-level
+    strings of at most ``length`` bytes, as the BLOOM adapter hands them to the GPU (atoms mode:
+    every character an atom, words = the pre-tokenizer's blocks, 'Ġ'+word after the first).
+    Words: 15 % the vocabulary's long tokens (> 16 code points), 60 % its shorter letter tokens,
+    25 % random letter strings of 1..10.  Keyed by (seed, global index).
+    Returns (text u8, offsets u64[n+1], cut mask u8: bit 1 atom start, bit 0 word start)."""
+    longs, shorts = bloom_word_pool(vocab_or_pool) if isinstance(vocab_or_pool, dict) else vocab_or_pool
+    parts: List[bytes] = []
+    cuts: List[bytes] = []
+    sp = BYTE_SPACE.encode("utf-8")
+    for g in range(start, start + n):
+        # counter word 1 = the string: streams never overlap (word 0 advances within a string)
+        rng = np.random.Generator(np.random.Philox(key=np.uint64(seed), counter=np.array([0, g, 0, 0], dtype=np.uint64)))
+        r = rng.random(size=64)
+        pick = rng.integers(0, 1 << 62, size=64)
+        rl = rng.integers(1, 11, size=64)
+        lt = rng.integers(0, 26, size=(64, 10))
+        buf, cut = bytearray(), bytearray()
+        for k in range(64):
+            if r[k] < 0.15:
+                w = longs[int(pick[k]) % len(longs)]
+            elif r[k] < 0.75:
+                w = shorts[int(pick[k]) % len(shorts)]
+            else:
+                w = "".join(LETTERS[c] for c in lt[k, :rl[k]])
+            wb = w.encode("ascii")
+            pre = sp if buf else b""
+            room = length - len(buf) - len(pre)
+            if room <= 0:
+                break
+            wb = wb[:room]
+            cut += b"\x03" + b"\x00" * (len(pre) - 1) + b"\x02" * len(wb) if pre else b"\x03" + b"\x02" * (len(wb) - 1)
+            buf += pre + wb
+        parts.append(bytes(buf))
+        cuts.append(bytes(cut))
+    text, offs = _pack(parts)
+    return text, offs, np.frombuffer(b"".join(cuts), dtype=np.uint8).copy()
+
+
+def _bloom_chunk(args):
+    n, start, pool, kw = args
+    return bloom_like_corpus(n, pool, start=start, **kw)
+
+
+def bloom_like_parallel(n: int, vocab: Dict[str, int], start: int = 0, procs: int = 8,
+                        **kw) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """``bloom_like_corpus`` over [start, start+n) in ``procs`` forked processes (identical
+    output).  Call before any GPU work (fork)."""
+    import multiprocessing as mp
+    pool = bloom_word_pool(vocab)
+    if procs <= 1 or n < 4096:
+        return bloom_like_corpus(n, pool, start=start, **kw)
+    step = (n + procs - 1) // procs
+    jobs = [(min(step, n - s), start + s, pool, kw) for s in range(0, n, step)]
+    with mp.get_context("fork").Pool(len(jobs)) as p:
+        res = p.map(_bloom_chunk, jobs)
+    lens = np.concatenate([np.diff(o) for _, o, _ in res])
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens, dtype=np.uint64)
+    return np.concatenate([t for t, _, _ in res]), offs, np.concatenate([c for _, _, c in res])

@@ -16,7 +16,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "liboracle.so")
 
-RAW, PRESPLIT = 0, 1
+RAW, PRESPLIT, ATOMS = 0, 1, 2
 
 
 def build(force: bool = False) -> str:

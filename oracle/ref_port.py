@@ -116,6 +116,17 @@ def dp_tokenize_raw(text: str, t2i: Dict[str, int]) -> Tuple[List[int], int]:
     return ids, 0
 
 
+def dp_tokenize_word_atoms(words: Sequence[Sequence[str]], t2i: Dict[str, int]) -> Tuple[List[int], int]:
+    """The BLOOM adapter's composition (tokenizer_utils.py:164-178): words of given atoms."""
+    ids: List[int] = []
+    for atoms in words:
+        toks, _ = enumerate_shortest(atoms, t2i)
+        if not toks:
+            return [], 1
+        ids.extend(t2i[t] for t in longest_token_choice(toks))
+    return ids, 0
+
+
 def min_tokens_for_string(s: Iterable[str], vocabulary) -> float:
     """Uncapped minimum token count, inf when impossible (inspect_tokenizer.py:77-86)."""
     s = list(s)

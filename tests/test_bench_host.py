@@ -79,3 +79,16 @@ def test_cpu_share_reports_threads_used(monkeypatch):
     monkeypatch.delenv("OMP_NUM_THREADS")
     used, vis = bench.cpu_share()
     assert used == vis
+
+
+def test_words_of_atoms_round_trip():
+    """bench.py's atoms-mode unpacking (the bloom workload's CPU-baseline input) inverts
+    dptok.engine.pack_word_atoms, and the reference-port composition runs on it."""
+    from dptok.engine import pack_word_atoms
+    strings = [[["a", "b"], ["Ġ", "c", "é"]], [["x"]], [["Ġ", "Ġ"], ["😀", "z"], ["q"]]]
+    text, offs, cut = pack_word_atoms(strings)
+    assert bench.words_of_atoms(text, offs, cut) == strings
+    from oracle import ref_port
+    t2i = {"ab": 0, "Ġc": 1, "é": 2, "x": 3, "ĠĠ": 4, "😀z": 5, "q": 6, "a": 7, "b": 8, "Ġ": 9}
+    assert ref_port.dp_tokenize_word_atoms(strings[0], t2i) == ([0, 1, 2], 0)
+    assert ref_port.dp_tokenize_word_atoms(strings[2], t2i) == ([4, 5, 6], 0)
