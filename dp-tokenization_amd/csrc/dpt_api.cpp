@@ -340,7 +340,8 @@ int dpt_ctx_long_need(dpt_ctx *c, uint64_t *need, uint64_t *cap) {
 
 static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uint8_t *text, uint64_t n_bytes,
                        const uint64_t *str_off, const uint8_t *cut_mask, uint64_t n_str, int32_t *ids, uint64_t ids_cap,
-                       uint64_t *id_off, int32_t *status, int32_t *capped_len, uint64_t *edges, void *hip_stream) {
+                       uint64_t *id_off, int32_t *status, int32_t *capped_len, uint64_t *edges, void *hip_stream,
+                       uint64_t *far = nullptr, uint64_t far_cap = 0) {
     const int mode = mode_flags & DPT_MODE_MASK;
     if (!c || !v) return fail(DPT_E_ARG, "null ctx or vocab");
     if (mode != DPT_MODE_RAW && mode != DPT_MODE_PRESPLIT && mode != DPT_MODE_ATOMS) return fail(DPT_E_ARG, "bad mode");
@@ -358,6 +359,8 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
     dpt::EncodeLaunch p;
     p.mode = mode_flags;
     p.edges = edges;
+    p.far = edges ? far : nullptr;
+    p.far_cap = far_cap;
     p.text = text;
     p.str_off = str_off;
     p.cut_mask = cut_mask;
@@ -421,7 +424,7 @@ int dpt_encode(dpt_ctx *c, const dpt_vocab *v, int mode, const uint8_t *text, ui
 static int encode_host_impl(dpt_ctx *c, const dpt_vocab *v, int mode, const uint8_t *text, uint64_t n_bytes,
                             const uint64_t *str_off, const uint8_t *cut_mask, uint64_t n_str, int32_t *ids,
                             uint64_t ids_cap, uint64_t *id_off, int32_t *status, int32_t *capped_len,
-                            uint64_t *edges) {
+                            uint64_t *edges, uint64_t *far = nullptr, uint64_t far_cap = 0, uint64_t *n_far = nullptr) {
     // host arguments first (checkable without a device)
     if (!str_off || !id_off || (n_str && !status)) return fail(DPT_E_ARG, "null output/offsets");
     if (n_bytes && (!text || !ids)) return fail(DPT_E_ARG, "null text/ids");
@@ -441,10 +444,12 @@ static int encode_host_impl(dpt_ctx *c, const dpt_vocab *v, int mode, const uint
     auto al8 = [](uint64_t x) { return (x + 7) & ~7ull; };
     // in:  text | offsets rebased to 0 (the device view is self-contained) | cut mask
     const uint64_t o_off = al8(n_bytes + 1), o_cut = o_off + 8 * (n_str + 1), in_bytes = o_cut + al8(n_bytes + 1);
-    // out: id_off | status | capped | counters | ids | edges
+    // out: id_off | status | capped | counters | ids | edges | far edge pairs
     const uint64_t o_st = 8 * (n_str + 1), o_cap = o_st + al8(4 * n_str + 4), o_ctr = o_cap + al8(4 * n_str + 4);
     const uint64_t o_ids = o_ctr + COUNTER_BYTES, o_edges = o_ids + al8(4 * (n_bytes + 1));
-    const uint64_t out_bytes = o_edges + (edges ? 8 * (n_bytes + 1) : 0);
+    const uint64_t o_far = o_edges + (edges ? 8 * (n_bytes + 1) : 0);
+    const bool want_far = edges && far;
+    const uint64_t out_bytes = o_far + (want_far ? 16 * far_cap : 0);
     if ((e = grow(&c->d_in, &c->cap_in, in_bytes)) != hipSuccess) return hip_fail(e, "hipMalloc(host-path in)");
     if ((e = grow(&c->d_out, &c->cap_out, out_bytes)) != hipSuccess) return hip_fail(e, "hipMalloc(host-path out)");
     if ((e = grow_pinned(&c->p_in, &c->cap_pin_in, in_bytes)) != hipSuccess) return hip_fail(e, "hipHostMalloc(in)");
@@ -460,13 +465,14 @@ static int encode_host_impl(dpt_ctx *c, const dpt_vocab *v, int mode, const uint
     int32_t *d_capped = reinterpret_cast<int32_t *>(c->d_out + o_cap);
     int32_t *d_ids = reinterpret_cast<int32_t *>(c->d_out + o_ids);
     uint64_t *d_edges = edges ? reinterpret_cast<uint64_t *>(c->d_out + o_edges) : nullptr;
+    uint64_t *d_far = want_far ? reinterpret_cast<uint64_t *>(c->d_out + o_far) : nullptr;
     const uint64_t *p_idoff = reinterpret_cast<const uint64_t *>(c->p_out);
     // small batches: everything in one copy (ids up to the n_bytes bound); large: the head, then the ids
     const bool one_copy = 4 * n_bytes <= (4ull << 20);
     for (int attempt = 0;; attempt++) {
         int rc = encode_impl(c, v, mode, c->d_in, n_bytes, reinterpret_cast<const uint64_t *>(c->d_in + o_off),
                              cut ? c->d_in + o_cut : nullptr, n_str, d_ids, n_bytes ? n_bytes : 1, d_idoff, d_status,
-                             d_capped, d_edges, st);
+                             d_capped, d_edges, st, d_far, far_cap);
         if (rc) return rc;
         if ((e = hipMemcpyAsync(c->p_out, c->d_out, one_copy ? out_bytes : o_ctr, hipMemcpyDeviceToHost, st)) != hipSuccess)
             return hip_fail(e, "D2H");
@@ -485,12 +491,20 @@ static int encode_host_impl(dpt_ctx *c, const dpt_vocab *v, int mode, const uint
     }
     const uint64_t total = p_idoff[n_str];
     if (total > ids_cap) return fail(DPT_E_CAP, "ids overflow");
+    uint64_t nf = 0;
+    if (want_far) {
+        if (n_str) memcpy(&nf, c->p_out + o_ctr + 56, sizeof(nf));   // the call's far edge pairs (finish_kernel)
+        if (n_far) *n_far = nf;
+        if (nf > far_cap) return fail(DPT_E_CAP, "far edge list overflow (*n_far holds the pairs needed)");
+    }
     if (!one_copy) {
         if (total && (e = hipMemcpyAsync(c->p_out + o_ids, d_ids, 4 * total, hipMemcpyDeviceToHost, st)) != hipSuccess)
             return hip_fail(e, "D2H ids");
         if (edges && n_bytes &&
             (e = hipMemcpyAsync(c->p_out + o_edges, d_edges, 8 * n_bytes, hipMemcpyDeviceToHost, st)) != hipSuccess)
             return hip_fail(e, "D2H edges");
+        if (nf && (e = hipMemcpyAsync(c->p_out + o_far, d_far, 16 * nf, hipMemcpyDeviceToHost, st)) != hipSuccess)
+            return hip_fail(e, "D2H far edges");
         if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(e, "sync");
     }
     memcpy(id_off, c->p_out, 8 * (n_str + 1));
@@ -498,6 +512,7 @@ static int encode_host_impl(dpt_ctx *c, const dpt_vocab *v, int mode, const uint
     if (capped_len && n_str) memcpy(capped_len, c->p_out + o_cap, 4 * n_str);
     if (total) memcpy(ids, c->p_out + o_ids, 4 * total);
     if (edges && n_bytes) memcpy(edges, c->p_out + o_edges, 8 * n_bytes);
+    if (nf) memcpy(far, c->p_out + o_far, 16 * nf);
     return DPT_OK;
 }
 
@@ -519,6 +534,21 @@ int dpt_dp_host(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uint8_t *t
     int32_t dummy_ids[1];
     return encode_host_impl(c, v, mode_flags, text, n_bytes, str_off, cut_mask, n_str, dummy_ids, n_bytes ? n_bytes : 1,
                             id_off.data(), status, lengths ? lengths : len_tmp.data(), edges);
+}
+
+int dpt_dp_host_far(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uint8_t *text, uint64_t n_bytes,
+                    const uint64_t *str_off, const uint8_t *cut_mask, uint64_t n_str, int32_t *status, int32_t *lengths,
+                    uint64_t *edges, uint64_t *far, uint64_t far_cap, uint64_t *n_far) {
+    if (!edges || !n_far || (far_cap && !far)) return fail(DPT_E_ARG, "dpt_dp_host_far needs edges, far and n_far");
+    *n_far = 0;
+    if (!(mode_flags & (DPT_FLAG_UNCAPPED | DPT_FLAG_LEN_ONLY))) mode_flags |= DPT_FLAG_LEN_ONLY;
+    std::vector<uint64_t> id_off(n_str + 1);
+    std::vector<int32_t> len_tmp(lengths ? 0 : n_str + 1);
+    int32_t dummy_ids[1];
+    uint64_t dummy_far[2];
+    return encode_host_impl(c, v, mode_flags, text, n_bytes, str_off, cut_mask, n_str, dummy_ids, n_bytes ? n_bytes : 1,
+                            id_off.data(), status, lengths ? lengths : len_tmp.data(), edges, far ? far : dummy_far,
+                            far_cap, n_far);
 }
 
 int dpt_token_histogram(const uint64_t *id_off, const int32_t *status, uint64_t n_str, int64_t *hist, uint32_t n_bins,

@@ -11,6 +11,8 @@ namespace dpt {
 struct EncodeLaunch {
     int mode;                // DPT_MODE_* | DPT_FLAG_*
     uint64_t *edges;         // nullable: per atom end E(i)&reachable masks (n_bytes entries)
+    uint64_t *far;           // nullable (with edges): optimal predecessors more than 64 atoms back, as
+    uint64_t far_cap;        //   (end index, back distance) pairs -- far_cap pairs; the count is in the counter block
     const uint8_t *text;
     const uint64_t *str_off;
     const uint8_t *cut_mask;
@@ -65,6 +67,9 @@ struct LongLaunch {
     int32_t *status;
     int32_t *capped;
     uint64_t *edges;
+    uint64_t *far;                    // as EncodeLaunch
+    uint64_t far_cap;
+    unsigned long long *far_count;    // pairs found (all of them; > far_cap: the host grows and reruns)
     const uint32_t *list;
     const uint32_t *list_count;
     uint32_t *work_next;

@@ -1584,9 +1584,10 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
 // next call by the finish kernel's last block): uint32 [0] retry count, [1] first-pass work, [2]
 // 2048-byte pass work, [3] long count, [4] long work, [5] finish ticket, [6] finish blocks done;
 // uint64 [4] (byte 32) the unbounded pass's claimed bytes, [5] (byte 40) the last call's claimed
-// bytes (dpt_ctx_long_need), [6] (byte 48) far edges listed (dpt_dp_host_far).
+// bytes (dpt_ctx_long_need), [6] (byte 48) far edge pairs found, [7] (byte 56) the last call's
+// far edge pairs (dpt_dp_host_far).
 constexpr unsigned CTR_TICKET = 5, CTR_DONE = 6;
-constexpr unsigned CTR_ARENA64 = 4, CTR_LASTNEED64 = 5;
+constexpr unsigned CTR_ARENA64 = 4, CTR_LASTNEED64 = 5, CTR_FAR64 = 6, CTR_LASTFAR64 = 7;
 constexpr unsigned FIN_BATCH = 256;   // strings per finish batch = threads per finish block
 
 // Look-back flags, one uint64 per FIN_BATCH-string batch: epoch (16 bits, the ctx's call counter; 0
@@ -1742,6 +1743,8 @@ __global__ void __launch_bounds__(FIN_BATCH) finish_kernel(FinishArgs f) {
             uint64_t *c64 = reinterpret_cast<uint64_t *>(f.ctr);
             c64[CTR_LASTNEED64] = c64[CTR_ARENA64];
             c64[CTR_ARENA64] = 0;
+            c64[CTR_LASTFAR64] = c64[CTR_FAR64];
+            c64[CTR_FAR64] = 0;
             f.ctr[0] = 0; f.ctr[1] = 0; f.ctr[2] = 0; f.ctr[3] = 0; f.ctr[4] = 0;
             f.ctr[CTR_TICKET] = 0;
             f.ctr[CTR_DONE] = 0;
@@ -1844,10 +1847,11 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     const bool wide = (p.mode & DPT_MODE_MASK) == DPT_MODE_ATOMS;   // atoms of up to 8 bytes
 
     if (p.n_str == 0) {
-        // no finish kernel runs: id_off[0] = 0, and the call's claimed arena bytes ("last need") are 0
+        // no finish kernel runs: id_off[0] = 0, and the call's claimed arena bytes ("last need") and
+        // far edge pairs are 0 (bytes 40..63 of the counter block; the running counters are 0 already)
         const hipError_t e0 = hipMemsetAsync(p.id_off, 0, sizeof(uint64_t), stream);
         if (e0 != hipSuccess) return e0;
-        return hipMemsetAsync(reinterpret_cast<uint64_t *>(p.retry_count) + CTR_LASTNEED64, 0, sizeof(uint64_t), stream);
+        return hipMemsetAsync(reinterpret_cast<uint64_t *>(p.retry_count) + CTR_LASTNEED64, 0, 3 * sizeof(uint64_t), stream);
     }
     if (ev) {
         const hipError_t er = hipEventRecord(ev[0], stream);
@@ -1884,7 +1888,9 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
         l.staging = p.staging; l.staging16 = p.staging16; l.counts = p.counts; l.status = p.status; l.capped = p.capped;
         l.arena = p.arena; l.arena_cap = p.arena_cap;
         l.arena_used = reinterpret_cast<unsigned long long *>(p.retry_count + 8);
-        l.edges = p.edges; l.list = a.long_list; l.list_count = a.long_count; l.work_next = p.retry_count + 4;
+        l.edges = p.edges; l.far = p.far; l.far_cap = p.far_cap;
+        l.far_count = reinterpret_cast<unsigned long long *>(p.retry_count) + CTR_FAR64;
+        l.list = a.long_list; l.list_count = a.long_count; l.work_next = p.retry_count + 4;
         l.slots = p.slots; l.slots4 = p.slots4; l.n_slots = p.n_slots; l.root_base = p.root_base;
         l.max_tok_bytes = p.max_tok_bytes; l.long_span = p.long_span;
         const uint64_t lb = p.n_str < (uint64_t)(p.max_blocks / 16) ? p.n_str : (uint64_t)(p.max_blocks / 16);

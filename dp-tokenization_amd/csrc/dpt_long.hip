@@ -115,6 +115,9 @@ struct Args {
     int32_t *status;
     int32_t *capped;
     uint64_t *edges;
+    uint64_t *far;
+    uint64_t far_cap;
+    unsigned long long *far_count;
     const uint32_t *list;
     const uint32_t *list_count;
     uint32_t *work_next;
@@ -384,9 +387,42 @@ __global__ void __launch_bounds__(64) long_kernel(Args a) {
                 const bool wend = (cur.y & WS) != 0;
                 if (lane == 0) {
                     S.rec[i - 1].z = (dg & 0xFFFFu) | (de << 16);
-                    if (a.edges) {
-                        a.edges[sb + i - 1] = emb;
-                        if (rl != NONE && (rl >> 31) == (r >> 31)) status = 3;   // E(i) has a span the 64-bit edge mask cannot hold
+                    if (a.edges) a.edges[sb + i - 1] = emb;
+                }
+                if (a.edges && rl != NONE && (rl >> 31) == (r >> 31)) {
+                    // E(i) has starts more than 64 atoms back, which the 64-bit edge mask cannot
+                    // hold: list every one of them as an (end, back distance) pair (the far scan
+                    // again, against the final key), or report status 3 without a far list
+                    if (!a.far) {
+                        status = 3;
+                    } else {
+                        const unsigned lo = (i > a.max_tok_bytes && i - a.max_tok_bytes > ws) ? i - a.max_tok_bytes : ws;
+                        for (unsigned jb = i - 65; i >= 65 + lo; jb -= 64) {
+                            const unsigned jj = jb - lane;
+                            bool hit = false;
+                            if (lane <= jb - lo && span_is_token(a, S, jj, i)) {
+                                const uint64_t st = (S.rec[jj].y & WS) ? SK0
+                                    : (((uint64_t)(uint32_t)S.stg[jj] << 32) | S.rec[jj].w);
+                                if (st != NONE) {
+                                    const unsigned span = (cpi - (S.rec[jj].y & CPM)) & CPM;
+                                    const uint64_t k2 = (st | 0x7FFFFFFFull) - span;
+                                    hit = (((st < k2 ? st : k2) ^ r) >> 31) == 0;
+                                }
+                            }
+                            const uint64_t hm = ballot(hit);
+                            if (hm) {
+                                unsigned long long base = 0;
+                                if (lane == 0) base = atomicAdd(a.far_count, (unsigned long long)__builtin_popcountll(hm));
+                                base = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(base >> 32)) << 32) |
+                                       __builtin_amdgcn_readfirstlane((unsigned)base);
+                                const uint64_t k = base + __builtin_amdgcn_mbcnt_hi((unsigned)(hm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)hm, 0u));
+                                if (hit && k < a.far_cap) {
+                                    a.far[2 * k] = sb + i - 1;
+                                    a.far[2 * k + 1] = i - 1 - jj;
+                                }
+                            }
+                            if (jb < lo + 64) break;
+                        }
                     }
                 }
                 // state of position i in key form; "inf" (no candidate, uncapped) stays inf
@@ -525,7 +561,7 @@ void launch_long(const LongLaunch &p, hipStream_t stream) {
     a.stg = reinterpret_cast<int32_t *>(p.arena + 16 * p.arena_cap);
     a.arena_cap = p.arena_cap;
     a.arena_used = p.arena_used;
-    a.edges = p.edges; a.list = p.list; a.list_count = p.list_count; a.work_next = p.work_next;
+    a.edges = p.edges; a.far = p.far; a.far_cap = p.far_cap; a.far_count = p.far_count; a.list = p.list; a.list_count = p.list_count; a.work_next = p.work_next;
     a.slots = p.slots; a.slots4 = p.slots4; a.n_slots = p.n_slots; a.root_base = p.root_base;
     a.max_tok_bytes = p.max_tok_bytes; a.long_span = p.long_span; a.mode = p.mode;
     hipLaunchKernelGGL(lng::long_kernel, dim3(p.blocks), dim3(64), 0, stream, a);

@@ -227,10 +227,12 @@ class Encoder:
         return out
 
     def dp(self, text: np.ndarray, offs: np.ndarray, mode="atoms", cut_mask: Optional[np.ndarray] = None,
-           uncapped: bool = False, edges: bool = False):
-        """DP by-products without ids (dpt_dp_host): (status, lengths, edges or None).  lengths are
-        the capped len_dp[-1] sums (reference dp_tokenize.py:70) or, with ``uncapped``, the minimum
-        token counts (65535 per impossible word, inspect_tokenizer.py:77-86)."""
+           uncapped: bool = False, edges: bool = False, far: bool = False):
+        """DP by-products without ids (dpt_dp_host): (status, lengths, edges or None), and with ``far``
+        (edges only) a 4th value: the (edges index, back distance) pairs of optimal predecessors more
+        than 64 atoms back (dpt_dp_host_far), an int array of shape (k, 2).  lengths are the capped
+        len_dp[-1] sums (reference dp_tokenize.py:70) or, with ``uncapped``, the minimum token counts
+        (65535 per impossible word, inspect_tokenizer.py:77-86)."""
         text = np.ascontiguousarray(text, dtype=np.uint8)
         offs = np.ascontiguousarray(offs, dtype=np.uint64)
         if len(offs) and int(offs[0]) != 0:
@@ -239,13 +241,26 @@ class Encoder:
         n_bytes = int(offs[-1] - offs[0])
         status = np.empty(max(n, 1), dtype=np.int32)
         lengths = np.empty(max(n, 1), dtype=np.int32)
-        ed = np.zeros(max(n_bytes, 1), dtype=np.uint64) if edges else None
+        ed = np.zeros(max(n_bytes, 1), dtype=np.uint64) if (edges or far) else None
         m = MODES[mode] | (DPT_FLAG_UNCAPPED if uncapped else DPT_FLAG_LEN_ONLY)
         if cut_mask is not None:
             cut_mask = np.ascontiguousarray(cut_mask, dtype=np.uint8)
-        check(_lib.lib().dpt_dp_host(self.handle, self.vocab.handle, m, _ptr(text), n_bytes, _ptr(offs), _ptr(cut_mask),
-                                     n, _ptr(status), _ptr(lengths), _ptr(ed)), "dpt_dp_host")
-        return status[:n], lengths[:n], ed
+        L = _lib.lib()
+        if not far:
+            check(L.dpt_dp_host(self.handle, self.vocab.handle, m, _ptr(text), n_bytes, _ptr(offs), _ptr(cut_mask),
+                                n, _ptr(status), _ptr(lengths), _ptr(ed)), "dpt_dp_host")
+            return status[:n], lengths[:n], ed
+        cap = 1024
+        while True:
+            fp = np.zeros((cap, 2), dtype=np.uint64)
+            nf = ctypes.c_uint64(0)
+            rc = L.dpt_dp_host_far(self.handle, self.vocab.handle, m, _ptr(text), n_bytes, _ptr(offs), _ptr(cut_mask),
+                                   n, _ptr(status), _ptr(lengths), _ptr(ed), _ptr(fp), cap, ctypes.byref(nf))
+            if rc == _lib.DPT_E_CAP and nf.value > cap:
+                cap = int(nf.value)   # the DP runs again with room for every pair
+                continue
+            check(rc, "dpt_dp_host_far")
+            return status[:n], lengths[:n], ed, fp[: nf.value].astype(np.int64)
 
     # ---------------------------------------------------------------- device buffers
     def encode_device(self, text_ptr: int, n_bytes: int, off_ptr: int, n_str: int, ids_ptr: int, ids_cap: int,

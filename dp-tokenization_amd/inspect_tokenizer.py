@@ -27,7 +27,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 if _HERE not in sys.path:
     sys.path.insert(0, _HERE)
 
-from packages.dp_tokenize import _dp_edges, compute_shortest_tokenizations as _packaged_cst  # noqa: E402
+from packages.dp_tokenize import _dp_length, compute_shortest_tokenizations as _packaged_cst  # noqa: E402
 
 _INF_WORD = 0xFFFF
 
@@ -55,7 +55,7 @@ def _uncapped_min(atoms, vocabulary) -> float:
         return 0
     if not any(isinstance(t, str) and t for t in vocabulary):
         return float("inf")
-    status, length, _ = _dp_edges(atoms, vocabulary, uncapped=True, edges=False)
+    status, length = _dp_length(atoms, vocabulary, uncapped=True)
     if status not in (0, 1) or length >= _INF_WORD:
         return float("inf")
     return length

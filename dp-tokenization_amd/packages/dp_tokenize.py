@@ -61,13 +61,20 @@ def _engine_for(vocabulary) -> Encoder:
     return enc
 
 
-def _dp_edges(atoms: Sequence[str], vocabulary, uncapped: bool = False, edges: bool = True):
-    """GPU DP over one atom list: (status, length, per-end reachable-predecessor masks or None)."""
+def _dp_edges(atoms: Sequence[str], vocabulary):
+    """GPU DP over one atom list: (status, length, per-end reachable-predecessor masks, far pairs)."""
     enc = _engine_for(vocabulary)
     text, offs, cut = atoms_to_csr([atoms])
-    status, lengths, edges = enc.dp(text, offs, mode="atoms", cut_mask=cut, uncapped=uncapped, edges=edges)
     # edges are indexed by the byte offset of the string + atom end - 1; one string at offset 0
-    return int(status[0]), int(lengths[0]), edges
+    return enc.dp(text, offs, mode="atoms", cut_mask=cut, edges=True, far=True)
+
+
+def _dp_length(atoms: Sequence[str], vocabulary, uncapped: bool = False):
+    """GPU DP over one atom list, lengths only: (status, capped len_dp[-1] or uncapped minimum)."""
+    enc = _engine_for(vocabulary)
+    text, offs, cut = atoms_to_csr([atoms])
+    status, lengths, _ = enc.dp(text, offs, mode="atoms", cut_mask=cut, uncapped=uncapped)
+    return int(status[0]), int(lengths[0])
 
 
 def compute_shortest_tokenizations(base_representation_s, vocabulary, disregard_word_initial_marker,
@@ -79,20 +86,22 @@ def compute_shortest_tokenizations(base_representation_s, vocabulary, disregard_
     n = len(atoms)
     if n == 0:
         raise IndexError("list index out of range")
-    status, length, edges = _dp_edges(atoms, vocabulary)
-    if status == 3:
-        # an optimal predecessor more than 64 atoms back (a token of > 64 code points): the
-        # 64-bit per-end edge masks of dpt_dp_host cannot list it
-        raise DptError("a shortest tokenization uses a token spanning more than 64 atoms; "
-                       "enumeration is limited to 64-atom tokens")
+    status, lengths, edges, far = _dp_edges(atoms, vocabulary)
+    status, length = int(status[0]), int(lengths[0])
     if status not in (0, 1):
         raise DptError("engine status %d" % status)
     if status == 1:
         return [], length
-    # preds[i]: reachable optimal predecessors of end i, ascending (= segment_index_dp[i-1] order)
+    # optimal reachable predecessors more than 64 atoms back (tokens of more than 64 atoms), which
+    # the 64-bit masks cannot hold: per end index, their back distances
+    far_by_end = {}
+    for e, d in far.tolist():
+        far_by_end.setdefault(e, []).append(d)
+
+    # preds(i): reachable optimal predecessors of end i, ascending (= segment_index_dp[i-1] order)
     def preds(i: int) -> List[int]:
         m = int(edges[i - 1])
-        out = []
+        out = [i - 1 - d for d in far_by_end.get(i - 1, ())]
         while m:
             d = (m & -m).bit_length() - 1
             out.append(i - 1 - d)

@@ -154,6 +154,18 @@ int dpt_encode_host(dpt_ctx *c, const dpt_vocab *v, int mode, const uint8_t *tex
 int dpt_dp_host(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uint8_t *text, uint64_t n_bytes,
                 const uint64_t *str_off, const uint8_t *cut_mask, uint64_t n_str, int32_t *status,
                 int32_t *lengths, uint64_t *edges);
+/*
+ * dpt_dp_host with edges, without the 64-atom limit of the masks: an optimal reachable predecessor
+ * more than 64 atoms back (a token of more than 64 atoms -- vocabularies with tokens of more than 64
+ * code points) is listed in far[] as the pair far[2k] = the edges[] index of the end (str_off[s] -
+ * str_off[0] + i - 1), far[2k+1] = the back distance d >= 64 (start i-1-d), in no particular order,
+ * instead of status 3.  far_cap counts pairs; *n_far = the pairs found.  Returns DPT_E_CAP (and the
+ * needed *n_far) when they do not fit: call again with far_cap >= *n_far.  Replaces the status 3 of
+ * reference dp_tokenize.py:40-46's unbounded segment_index_dp (no span limit there).
+ */
+int dpt_dp_host_far(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uint8_t *text, uint64_t n_bytes,
+                    const uint64_t *str_off, const uint8_t *cut_mask, uint64_t n_str, int32_t *status,
+                    int32_t *lengths, uint64_t *edges, uint64_t *far, uint64_t far_cap, uint64_t *n_far);
 
 /*
  * Token-count histogram (device pointers): hist[0..n_bins) counts strings by

@@ -458,3 +458,48 @@ def test_finish_epoch_wrap(engines, oracles):
             assert np.array_equal(io.cpu().numpy().view(np.uint64), roff), k
             assert np.array_equal(ids[: int(roff[-1])].cpu().numpy(), rids), k
             assert np.array_equal(st.cpu().numpy(), rst), k
+
+
+@pytest.mark.gpu
+def test_enumeration_with_tokens_longer_than_64_atoms():
+    """compute_shortest_tokenizations (reference dp_tokenize.py:6-70, no span limit) when optimal
+    tokens span more than 64 atoms: the far predecessors come from dpt_dp_host_far's pair list, so
+    the full list and its DFS order equal oracle/ref_port.enumerate_shortest (was DptError)."""
+    from oracle import ref_port
+    from packages.dp_tokenize import compute_shortest_tokenizations
+    rng = np.random.default_rng(11)
+    longs = ["".join(chr(c) for c in rng.integers(0x61, 0x64, size=L)) for L in (65, 66, 70, 80, 100, 150, 300)]
+    u, w = longs[2], longs[3]
+    vocab = {"a", "b", "c", "x", "ab", "bc", "ca"} | set(longs)
+    vocab |= {u + w[:3], w[3:], u[:-2], u[-2:] + w}      # several far predecessors at one end
+    words = [u + w, "x" + u + w, u + w + "ab", longs[0] + longs[1], longs[6] + "abc" + longs[5]]
+    for k in range(25):
+        a, b = longs[k % 7], longs[(3 * k + 1) % 7]
+        words.append(a + "".join(chr(c) for c in rng.integers(0x61, 0x64, size=k % 6)) + b[: 60 + k])
+    seen_multi = 0
+    for wd in words:
+        got = compute_shortest_tokenizations(list(wd), vocab, False, None)
+        ref = ref_port.enumerate_shortest(list(wd), vocab)
+        assert got == ref, wd[:40]
+        seen_multi += len(ref[0]) > 1 and any(len(t) > 64 for tk in ref[0] for t in tk)
+    got, n = compute_shortest_tokenizations(list(u + w), vocab, False, None)
+    assert n == 2 and sorted(got) == sorted([[u, w], [u + w[:3], w[3:]], [u[:-2], u[-2:] + w]])
+    assert seen_multi >= 5
+
+
+@pytest.mark.gpu
+def test_dp_host_without_far_list_reports_status_3():
+    """dpt_dp_host (no far list) keeps its contract: an optimal predecessor more than 64 atoms back
+    gives status 3; dpt_dp_host_far lists it instead."""
+    from dptok import Encoder, Vocab
+    from dptok.engine import atoms_to_csr
+    rng = np.random.default_rng(12)
+    t = "".join(chr(c) for c in rng.integers(0x61, 0x64, size=90))
+    t2i = {"a": 0, "b": 1, "c": 2, t: 3}
+    enc = Encoder(Vocab(t2i, 0))
+    text, offs, cut = atoms_to_csr([list("ab" + t)])
+    st, ln, ed = enc.dp(text, offs, cut_mask=cut, edges=True)
+    assert int(st[0]) == 3
+    st, ln, ed, far = enc.dp(text, offs, cut_mask=cut, edges=True, far=True)
+    assert int(st[0]) == 0 and int(ln[0]) == 3
+    assert far.tolist() == [[len(t) + 2 - 1, len(t) - 1]]

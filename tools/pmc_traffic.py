@@ -10,7 +10,7 @@ keyed by the sha256 of the kernel sources so bench.py only reports it for the sa
 import csv, glob, hashlib, json, os, re, subprocess, sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SRC = ["dpt_kernels.hip", "dpt_lane.hip", "dpt_long.hip", "dpt_api.cpp", "dpt_vocab.cpp", "dpt_internal.h"]
+SRC = ["dpt_kernels.hip", "dpt_long.hip", "dpt_api.cpp", "dpt_vocab.cpp", "dpt_internal.h"]
 
 
 def normalized(src: str) -> str:
