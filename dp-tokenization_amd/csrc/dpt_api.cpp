@@ -36,7 +36,8 @@ struct dpt_ctx {
     uint64_t *counts = nullptr;
     uint32_t *retry_list = nullptr;
     uint64_t cap_str = 0;
-    uint32_t *retry_count = nullptr;  // 64 bytes: 8 uint32 counters, the uint64 arena counter at byte 32
+    uint32_t *retry_count = nullptr;  // counter block (dpt::CTR_ALLOC_BYTES): 8 uint32 counters, the uint64 arena
+                                      // counter at byte 32, ..., the first pass's partition counters at byte 256
     uint8_t *wsl_scratch = nullptr;   // word lists of the 256-byte pass (dpt::wsl_scratch_bytes)
     unsigned long long *flags = nullptr;   // finish kernel's look-back flags (one per 64 strings)
     uint64_t cap_flags = 0;
@@ -147,8 +148,8 @@ int ensure_workspace(dpt_ctx *c, const dpt_vocab *v, uint64_t n_bytes, uint64_t 
     }
     if (!c->retry_count) {
         // zeroed once here; every call's finish kernel resets it for the next call
-        e = hipMalloc((void **)&c->retry_count, COUNTER_BYTES);
-        if (e == hipSuccess) e = hipMemset(c->retry_count, 0, COUNTER_BYTES);
+        e = hipMalloc((void **)&c->retry_count, dpt::CTR_ALLOC_BYTES);
+        if (e == hipSuccess) e = hipMemset(c->retry_count, 0, dpt::CTR_ALLOC_BYTES);
         if (e != hipSuccess) return hip_fail(e, "hipMalloc(retry_count)");
     }
     return DPT_OK;
@@ -322,7 +323,7 @@ int dpt_ctx_workspace_bytes(const dpt_ctx *c, uint64_t *device_path, uint64_t *h
     if (device_path)
         *device_path = c->cap16 * 2 + c->cap32 * 4 + c->arena_cap * ARENA_PER_BYTE + c->cap_str * (8 + 2 * 4) +
                        c->cap_flags * 8 + (c->wsl_scratch ? dpt::wsl_scratch_bytes(c->max_blocks) : 0) +
-                       (c->retry_count ? COUNTER_BYTES : 0);
+                       (c->retry_count ? dpt::CTR_ALLOC_BYTES : 0);
     if (host_path) *host_path = c->cap_in + c->cap_out;
     return DPT_OK;
 }
@@ -407,7 +408,7 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
     }
     hipError_t e = dpt::launch_encode(p, st, evp);
     if (e != hipSuccess) {
-        (void)hipMemsetAsync(c->retry_count, 0, COUNTER_BYTES, st);   // the finish kernel did not reset them
+        (void)hipMemsetAsync(c->retry_count, 0, dpt::CTR_ALLOC_BYTES, st);   // the finish kernel did not reset them
         return hip_fail(e, "encode launch");
     }
     return DPT_OK;

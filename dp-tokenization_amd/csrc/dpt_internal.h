@@ -44,6 +44,14 @@ struct EncodeLaunch {
     int32_t root_base;
 };
 
+// first-pass work partitions (dpt_kernels.hip tokenize_kernel): up to NPART_MAX counters, one per
+// PART_STRIDE uint32 (a 256-byte line each), from byte PART_CTR_OFFSET of the counter block, then the
+// used-up mask; the counter block is CTR_ALLOC_BYTES long (the host path copies its first 64 bytes)
+constexpr unsigned NPART_MAX = 32;
+constexpr unsigned PART_STRIDE = 64;
+constexpr size_t PART_CTR_OFFSET = 256;
+constexpr size_t CTR_ALLOC_BYTES = PART_CTR_OFFSET + (NPART_MAX + 1) * PART_STRIDE * 4;
+
 // child filter bit of next byte b (slots4[].w, host and device): XOR with b >> 5 permutes the
 // low five bits inside each 32-byte block, so the 26 lowercase letters get distinct bits
 __host__ __device__ inline unsigned child_bit(unsigned b) { return (b ^ (b >> 5)) & 31u; }

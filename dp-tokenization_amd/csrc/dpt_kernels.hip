@@ -286,7 +286,8 @@ struct EncodeArgs {
     uint32_t *long_count;
     const uint32_t *work_list;  // 2048-byte pass: the retry list
     const uint32_t *work_count;
-    uint32_t *work_next;        // dynamic work distribution counter (zeroed per launch)
+    uint32_t *work_next;        // 2048-byte pass: its work counter (zeroed per launch)
+    uint32_t *part_ctr;         // first pass: NPART partition counters (PART_STRIDE apart), then the used-up mask
     uint8_t *wsl_scratch;       // word lists of the 256-byte pass: grid x NG x WSL_STRIDE bytes
     int long_span;              // the vocabulary has tokens longer than 64 code points
     uint64_t *edges;            // nullable: per atom end, the E(i) & reachable back-distance mask
@@ -542,11 +543,21 @@ __device__ bool prep_window(GroupLDS<CH, G> &L, uint8_t *gw, const WinRegs<CH> &
 
 // ------------------------------------------------------------------ the tokenize kernel
 
+#ifndef CLAIM
+#define CLAIM 4       // strings per claim of the work counters
+#endif
+#ifndef NPART
+#define NPART 16      // first-pass work partitions (<= NPART_MAX)
+#endif
+static_assert(NPART >= 1 && NPART <= NPART_MAX, "NPART");
 #ifndef A_REFILL
 #define A_REFILL 32   // phase A: idle lanes needed before a batched refill (1/8/16/32 within 2 %)
 #endif
 #ifndef DPT_DOUBLE   // diagnostic builds only: run one phase twice to measure its marginal cost
 #define DPT_DOUBLE 0
+#endif
+#ifndef DPT_STOP     // diagnostic builds only (wrong results): 1 = prep only, 2 = + A, 3 = + B/C0/C1
+#define DPT_STOP 9
 #endif
 
 // 256-byte 16-lane rows: 6 waves per SIMD by VGPRs (<= 80), so LDS (22 waves per CU) binds
@@ -577,7 +588,46 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
     const bool raw = mode == 0;
     const bool uncapped = (a.mode & DPT_FLAG_UNCAPPED) != 0;   // f2: inspect_tokenizer's inf-initialised DP
     const bool len_only = (a.mode & (DPT_FLAG_UNCAPPED | DPT_FLAG_LEN_ONLY)) != 0;
-    bool exhausted = false;              // strings are handed out by a device counter
+    // Strings are handed out in chunks of CLAIM strings by npart device counters, one per
+    // contiguous partition of the batch (strings [p n/npart, (p+1) n/npart) -- each in its own
+    // 256-byte line); a wave starts on partition blockIdx mod npart, keeps its claimed range
+    // [q_next, q_end) and, when a claim reaches its partition's end, marks the partition in a shared
+    // mask and moves to the next unmarked one.  Round 1's single counter with one atomic per 4
+    // strings bound the whole kernel: a prep-only build ran 2.91 of the full build's 2.99 ms, every
+    // wave queued behind ~5.6k same-address atomics (profiles/r02_phase_diag.txt).
+    const unsigned npart = BIG ? 1u : (unsigned)min((uint64_t)NPART, max((uint64_t)1, n_work / 4096u));
+    unsigned part = BIG ? 0u : blockIdx.x % npart;
+    bool exhausted = false, claimed_all = false;
+    uint64_t q_next = 0, q_end = 0;
+    // one claim of up to req strings (uniform): [nb, ne), possibly empty once every partition is used up
+    auto claim = [&](unsigned req, uint64_t &nb, uint64_t &ne) {
+        for (;;) {
+            uint32_t *ctr = BIG ? a.work_next : a.part_ctr + part * PART_STRIDE;
+            const uint64_t lo = BIG ? 0u : n_work * part / npart, hi = BIG ? n_work : n_work * (part + 1) / npart;
+            unsigned b = 0;
+            if (lane == 0) b = atomicAdd(ctr, req);
+            nb = lo + __builtin_amdgcn_readlane(b, 0);
+            ne = nb < hi ? (nb + req < hi ? nb + req : hi) : nb;
+            if (nb + req >= hi) {   // the partition is used up (by this claim or earlier ones)
+                if (BIG) {
+                    claimed_all = true;
+                } else {
+                    unsigned m = 0;
+                    if (lane == 0) m = atomicOr(a.part_ctr + (unsigned)NPART * PART_STRIDE, 1u << part);
+                    m = __builtin_amdgcn_readlane(m, 0) | (1u << part);
+                    const unsigned all = (npart >= 32u ? 0u : (1u << npart)) - 1u;
+                    if ((m & all) == all) {
+                        claimed_all = true;
+                    } else {   // the next unmarked partition after this one
+                        const unsigned free = ~m & all;
+                        const unsigned hi_free = free & ~((2u << part) - 1u);
+                        part = (unsigned)__builtin_ctz(hi_free ? hi_free : free);
+                    }
+                }
+            }
+            if (ne > nb || claimed_all) return;
+        }
+    };
     STAMP_DECL
 
     if (lane < (unsigned)NG) SS[lane].active = 0;
@@ -595,13 +645,16 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
             for (int g = 0; g < NG; g++) need |= uni(SS[g].active) ? 0u : (1u << g);
             if (need && !exhausted) {
                 const unsigned n_need = (unsigned)__builtin_popcount(need);
-                unsigned base = 0;
-                if (lane == 0) base = atomicAdd(a.work_next, n_need);
-                base = __builtin_amdgcn_readlane(base, 0);
-                if ((uint64_t)base + n_need >= n_work) exhausted = true;
+                // the wave's claimed range first; when it runs short, one claim (the leftover of the
+                // old range is taken first, then the new one)
+                const uint64_t avail = q_end - q_next;
+                uint64_t nb = q_end, ne = q_end;   // the new chunk [nb, ne)
+                if (avail < n_need && !claimed_all) claim((unsigned)CLAIM, nb, ne);
+                const uint64_t take_old = avail < n_need ? avail : n_need;
                 if (lane < (unsigned)NG && ((need >> lane) & 1u)) {
-                    const uint64_t idx = (uint64_t)base + (unsigned)__builtin_popcount(need & ((1u << lane) - 1u));
-                    if (idx < n_work) {
+                    const unsigned k = (unsigned)__builtin_popcount(need & ((1u << lane) - 1u));
+                    const uint64_t idx = k < take_old ? q_next + k : nb + (k - take_old);
+                    if (k < take_old || idx < ne) {
                         const uint64_t s = BIG ? (uint64_t)a.work_list[idx] : idx;
                         const uint64_t o0 = a.str_off[s], o1 = a.str_off[s + 1];
                         SlotState &S = SS[lane];
@@ -610,6 +663,14 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                         S.ntok = 0; S.capsum = 0; S.abase = 0;
                     }
                 }
+                if (avail < n_need) {
+                    const uint64_t used = nb + (n_need - take_old);
+                    q_next = used < ne ? used : ne;
+                    q_end = ne;
+                } else {
+                    q_next += n_need;
+                }
+                if (claimed_all && q_next >= q_end) exhausted = true;
                 wave_sync();
             }
             unsigned todo = 0;
@@ -672,7 +733,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
         for (int rep_ = 0; rep_ < 2; rep_++) {
             if (rep_) wave_sync();
 #endif
-        {
+        if (DPT_STOP > 1) {
             // A0 (16-lane rows, raw mode): slots whose window is pure ASCII -- atoms are its bytes --
             // get every walk's first lookup here, byte-parallel with four loads in flight per lane;
             // the walks it cannot finish (word starts, the string's first atom, '\n', and walks that
@@ -932,7 +993,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
 
         // ---------------------------------------------------------- B: forward recurrence
         bool lane_mode = false;   // B ran per chunk and did C0 and C1 itself (G = 16, capless, no edges)
-        {
+        if (DPT_STOP > 2) {
             GL &L = grp(mg);
             const unsigned na = SS[mg].n_atoms;
             unsigned imax = 0;
@@ -1309,7 +1370,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
 
         // ---------------------------------------------------------- C0: per-window token counts and validity
         // (word w ends at atom word_end(w); its final state is in fin[word_end(w)])
-        if (!lane_mode) {
+        if (DPT_STOP > 2 && !lane_mode) {
             unsigned pre[NG + 1];
             pre[0] = 0;
 #pragma unroll
@@ -1354,7 +1415,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
         for (int rep_ = 0; rep_ < 2; rep_++) {
             if (rep_) wave_sync();
 #endif
-        if (!lane_mode) {
+        if (DPT_STOP > 2 && !lane_mode) {
             unsigned pre[NG + 1], tokpre[NG + 1], inv_g[NG];
             pre[0] = 0; tokpre[0] = 0;
 #pragma unroll
@@ -1417,7 +1478,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
         for (int rep_ = 0; rep_ < 2; rep_++) {
             if (rep_) wave_sync();
 #endif
-        {
+        if (DPT_STOP > 3) {
             unsigned pre[NG + 1], na_g[NG];
             uint8_t *obase[NG];       // staging row of the window's first token, per slot
             const bool n16 = SW == 1 || (SW == 0 && a.staging16 != nullptr);   // int16 staging (uniform)
@@ -1580,12 +1641,13 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
 
 // ------------------------------------------------------------------ finish: offsets + CSR ids in one pass
 
-// Counter block (EncodeLaunch::retry_count, 64 bytes; zeroed once at allocation, then reset for the
-// next call by the finish kernel's last block): uint32 [0] retry count, [1] first-pass work, [2]
+// Counter block (EncodeLaunch::retry_count, CTR_ALLOC_BYTES; zeroed once at allocation, then reset for
+// the next call by the finish kernel's last block): uint32 [0] retry count, [1] unused, [2]
 // 2048-byte pass work, [3] long count, [4] long work, [5] finish ticket, [6] finish blocks done;
 // uint64 [4] (byte 32) the unbounded pass's claimed bytes, [5] (byte 40) the last call's claimed
 // bytes (dpt_ctx_long_need), [6] (byte 48) far edge pairs found, [7] (byte 56) the last call's
-// far edge pairs (dpt_dp_host_far).
+// far edge pairs (dpt_dp_host_far); from byte PART_CTR_OFFSET the first pass's partition counters
+// and their used-up mask (dpt_internal.h).
 constexpr unsigned CTR_TICKET = 5, CTR_DONE = 6;
 constexpr unsigned CTR_ARENA64 = 4, CTR_LASTNEED64 = 5, CTR_FAR64 = 6, CTR_LASTFAR64 = 7;
 constexpr unsigned FIN_BATCH = 256;   // strings per finish batch = threads per finish block
@@ -1746,6 +1808,8 @@ __global__ void __launch_bounds__(FIN_BATCH) finish_kernel(FinishArgs f) {
             c64[CTR_LASTFAR64] = c64[CTR_FAR64];
             c64[CTR_FAR64] = 0;
             f.ctr[0] = 0; f.ctr[1] = 0; f.ctr[2] = 0; f.ctr[3] = 0; f.ctr[4] = 0;
+            uint32_t *pc = f.ctr + PART_CTR_OFFSET / 4;
+            for (unsigned q = 0; q <= NPART; q++) pc[q * PART_STRIDE] = 0;   // the partition counters and the mask
             f.ctr[CTR_TICKET] = 0;
             f.ctr[CTR_DONE] = 0;
         }
@@ -1841,6 +1905,7 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     a.mode = p.mode;
     a.edges = p.edges;
     a.work_next = p.retry_count + 1;
+    a.part_ctr = p.retry_count + PART_CTR_OFFSET / 4;
     a.wsl_scratch = p.wsl_scratch;
     a.long_span = p.long_span;
     TrieView tv{p.slots, p.slot_ids, p.slots4, p.root_base, p.n_slots};
