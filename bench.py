@@ -5,8 +5,8 @@ metric: input bytes/sec (whole job, all GPUs) + exact-match rate vs the CPU DP,
 256-byte random printable-ASCII strings, synthetic Llama-shaped 32k vocab (no
 Llama-2 tokenizer file is available offline: SURVEY.md §0 finding 6).
 
-A step = one pass of the hot path (dpt_encode: tokenize kernel(s) + offset scan +
-CSR compaction, then the token-count histogram and, for N>1, ONE RCCL all-reduce
+A step = one pass of the hot path (dpt_encode: the tokenize passes + the finish kernel's
+offsets and CSR ids, then the token-count histogram and, for N>1, ONE RCCL all-reduce
 of it) over the rank's resident shard (BASELINE.json configs[1] at N=1, configs[2] at N=8).
 Strong scaling (the default for N > 1): ONE global corpus of --strings
 (1M) strings keyed by (seed, global index) is split by dptok.dist.shard_range -- rank r
