@@ -1,0 +1,59 @@
+"""CPU model of the tokenize kernel's work distribution (dpt_kernels.hip tokenize_kernel, the
+`claim` lambda): npart = min(NPART, max(1, n / 4096)) partition counters over contiguous string
+ranges, claims of CLAIM strings, a used-up mask; each wave starts on partition blockIdx mod npart
+and moves to the next unmarked partition after a claim reaches its partition's end.  Under random
+interleavings of the waves' atomics every string is handed out exactly once and every wave stops."""
+import random
+
+import pytest
+
+NPART, CLAIM = 16, 4
+
+
+def run(n_work, n_waves, seed):
+    rnd = random.Random(seed)
+    npart = min(NPART, max(1, n_work // 4096))
+    ctr = [0] * npart
+    mask = 0
+    allm = (1 << npart) - 1
+    got = [0] * n_work
+    waves = [{"part": w % npart, "q": [], "done": False} for w in range(n_waves)]
+
+    def claim(wv):
+        nonlocal mask
+        while True:
+            p = wv["part"]
+            lo, hi = n_work * p // npart, n_work * (p + 1) // npart
+            b = ctr[p]; ctr[p] += CLAIM               # atomicAdd
+            nb = lo + b
+            ne = min(nb + CLAIM, hi) if nb < hi else nb
+            claimed_all = False
+            if nb + CLAIM >= hi:
+                old = mask; mask |= 1 << p            # atomicOr
+                m = old | (1 << p)
+                if m & allm == allm:
+                    claimed_all = True
+                else:
+                    free = ~m & allm
+                    hi_free = free & ~((2 << p) - 1)
+                    pick = hi_free if hi_free else free
+                    wv["part"] = (pick & -pick).bit_length() - 1
+            if ne > nb or claimed_all:
+                return list(range(nb, ne)), claimed_all
+
+    live = list(range(n_waves))
+    while live:
+        w = rnd.choice(live)                           # any wave may take the next atomic
+        wv = waves[w]
+        idx, claimed_all = claim(wv)
+        for i in idx:
+            got[i] += 1
+        if claimed_all:
+            live.remove(w)
+    return got
+
+
+@pytest.mark.parametrize("n_work,n_waves", [(1, 1), (3, 64), (4095, 50), (4096 * 16 + 3, 300), (100003, 700), (70000, 5632)])
+def test_every_string_exactly_once(n_work, n_waves):
+    for seed in range(3):
+        assert run(n_work, n_waves, seed) == [1] * n_work

@@ -503,3 +503,23 @@ def test_dp_host_without_far_list_reports_status_3():
     st, ln, ed, far = enc.dp(text, offs, cut_mask=cut, edges=True, far=True)
     assert int(st[0]) == 0 and int(ln[0]) == 3
     assert far.tolist() == [[len(t) + 2 - 1, len(t) - 1]]
+
+
+@pytest.mark.parametrize("n", [4095, 8192, 65535, 65536, 100003])
+def test_work_partitions_vs_oracle(n, engines, oracles):
+    """First-pass work distribution (tokenize_kernel: min(16, n / 4096) partition counters, claims of
+    4 strings, a used-up mask): batch sizes at and around the partition-count steps, ragged strings
+    (uneven work, so waves leave their first partition), three calls on one ctx (the counters and
+    the mask are reset by the finish kernel's last block) -- every string exactly once, vs the oracle."""
+    from dptok import synth
+    rng = np.random.default_rng(n)
+    text, offs = synth.random_ascii_corpus(n, 64, seed=n)
+    cut = rng.integers(0, 65, size=n)
+    cut[rng.random(n) < 0.02] = 0
+    parts = [text[i * 64:i * 64 + int(cut[i])].tobytes() for i in range(n)]
+    offs = np.zeros(n + 1, np.uint64)
+    offs[1:] = np.cumsum([len(p) for p in parts])
+    text = np.frombuffer(b"".join(parts) + b"\0", np.uint8)
+    ref = oracles["llama32k"].encode_csr(text, offs)
+    for _ in range(3):
+        _cmp_csr(engines["llama32k"].encode_csr(text, offs), ref)
