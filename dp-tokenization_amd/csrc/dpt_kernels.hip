@@ -556,9 +556,12 @@ static_assert(NPART >= 1 && NPART <= NPART_MAX, "NPART");
 #ifndef DPT_DOUBLE   // diagnostic builds only: run one phase twice to measure its marginal cost
 #define DPT_DOUBLE 0
 #endif
-#ifndef DPT_STOP     // diagnostic builds only (wrong results): 1 = prep only, 2 = + A, 3 = + B/C0/C1
+#ifndef DPT_STOP     // diagnostic builds only (wrong results): 1 = prep only, 21 = + A0, 2 = + A, 25 / 26 / 27 =
+                     // + lane-mode B's cut points / recurrence / transfer scan + fix-up, 3 = + B/C0/C1
 #define DPT_STOP 9
 #endif
+#define DPT_RUN_B (DPT_STOP >= 3 && DPT_STOP != 21)
+#define DPT_RUN_C2 (DPT_STOP == 9)
 
 // 256-byte 16-lane rows: 6 waves per SIMD by VGPRs (<= 80), so LDS (22 waves per CU) binds
 #ifndef WPE16
@@ -915,7 +918,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
             // Refills are batched: idle lanes take new starts only once A_REFILL of them are idle
             // (or the remaining starts fit), so the refill code runs on a fraction of the steps.
             bool active = false;
-            unsigned nxt = 0;
+            unsigned nxt = DPT_STOP == 21 ? total : 0u;   // diagnostic: A0 only
             for (;;) {
                 {
                     const uint64_t im = ballot(!active);
@@ -993,7 +996,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
 
         // ---------------------------------------------------------- B: forward recurrence
         bool lane_mode = false;   // B ran per chunk and did C0 and C1 itself (G = 16, capless, no edges)
-        if (DPT_STOP > 2) {
+        if (DPT_RUN_B) {
             GL &L = grp(mg);
             const unsigned na = SS[mg].n_atoms;
             unsigned imax = 0;
@@ -1162,6 +1165,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 rs = min(rs, (unsigned)__builtin_amdgcn_update_dpp((int)na, (int)rs, 0x104, 0xF, 0xF, false));
                 rs = min(rs, (unsigned)__builtin_amdgcn_update_dpp((int)na, (int)rs, 0x108, 0xF, 0xF, false));
                 const unsigned re = (unsigned)__builtin_amdgcn_update_dpp((int)na, (int)rs, 0x101, 0xF, 0xF, false);
+                if (DPT_STOP == 25) return;   // diagnostic: cut points only
 
                 // ---- the recurrence over ends (rs, re], one position per iteration
                 unsigned i = rs, ws = rs, sprev = FRESH, pe = 0;
@@ -1205,6 +1209,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                         cprev = cpi;
                     }
                 }
+                if (DPT_STOP == 26) return;   // diagnostic: + the recurrence
                 // P1 = the piece walked first in C1 (the one ending at re); p1in: no word start in
                 // (rs, re), so P1 is the chunk's first piece too and starts from the incoming state
                 const bool re_ws = i > rs && sprev == FRESH;   // re is a word start (its word ended)
@@ -1240,6 +1245,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                     }
                 }
                 const unsigned gre = p1in ? max(gin, gl1) : gl1;   // G at re of P1's word (its L* if re_ws)
+                if (DPT_STOP == 27) return;   // diagnostic: + the transfer scan and fix-up
 
                 // ---- C1 (replaces C0 + C1 for the wave): the selection walks, one chunk per lane.
                 // Every tokenization passes through the cuts, so a chunk's tokens are the ones its
@@ -1370,7 +1376,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
 
         // ---------------------------------------------------------- C0: per-window token counts and validity
         // (word w ends at atom word_end(w); its final state is in fin[word_end(w)])
-        if (DPT_STOP > 2 && !lane_mode) {
+        if (DPT_RUN_B && !lane_mode) {
             unsigned pre[NG + 1];
             pre[0] = 0;
 #pragma unroll
@@ -1415,7 +1421,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
         for (int rep_ = 0; rep_ < 2; rep_++) {
             if (rep_) wave_sync();
 #endif
-        if (DPT_STOP > 2 && !lane_mode) {
+        if (DPT_RUN_B && !lane_mode) {
             unsigned pre[NG + 1], tokpre[NG + 1], inv_g[NG];
             pre[0] = 0; tokpre[0] = 0;
 #pragma unroll
@@ -1478,7 +1484,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
         for (int rep_ = 0; rep_ < 2; rep_++) {
             if (rep_) wave_sync();
 #endif
-        if (DPT_STOP > 3) {
+        if (DPT_RUN_C2) {
             unsigned pre[NG + 1], na_g[NG];
             uint8_t *obase[NG];       // staging row of the window's first token, per slot
             const bool n16 = SW == 1 || (SW == 0 && a.staging16 != nullptr);   // int16 staging (uniform)
@@ -1650,7 +1656,12 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
 // and their used-up mask (dpt_internal.h).
 constexpr unsigned CTR_TICKET = 5, CTR_DONE = 6;
 constexpr unsigned CTR_ARENA64 = 4, CTR_LASTNEED64 = 5, CTR_FAR64 = 6, CTR_LASTFAR64 = 7;
-constexpr unsigned FIN_BATCH = 256;   // strings per finish batch = threads per finish block
+#ifndef FIN_THREADS
+#define FIN_THREADS 512   // threads per finish block (>= FIN_BATCH): all of them copy
+#endif
+#ifndef FIN_BATCH
+#define FIN_BATCH 256   // strings per finish batch = threads per finish block (>= 64: the flags are sized per 64 strings)
+#endif
 
 // Look-back flags, one uint64 per FIN_BATCH-string batch: epoch (16 bits, the ctx's call counter; 0
 // never used, the host clears the array when it wraps) | state (2 bits: 1 = batch aggregate, 2 =
@@ -1715,18 +1726,19 @@ __device__ __forceinline__ uint64_t finish_lookback(const FinishArgs &f, uint64_
     }
 }
 
-// Offsets and CSR ids in one launch: a grid of at most 8 blocks per CU, FIN_BATCH threads each,
-// takes FIN_BATCH-string batches in ticket order.  Per batch: one count per thread, a block scan
-// (wave scans + the four wave sums in LDS); wave 0 publishes the batch aggregate, finds the batch's
-// first id by look-back and publishes the inclusive prefix; every thread writes its string's end
-// offset; then the block copies the batch's staged ids -- threads over the batch's OUTPUT ids, so
-// every store is a coalesced row -- FIN_U independent loads in flight per thread.  The last block
-// to finish resets the counter block for the next call.  Replaces round 1's counter reset, offset
-// scan and compaction (three launches, two more passes over the counts); a persistent grid because
-// one block per 64 strings spent more time dispatching blocks and chaining look-backs (0.19 ms per
-// 1M strings without any copy) than copying.
+// Offsets and CSR ids in one launch: a persistent grid (32 waves per CU) of FIN_THREADS-thread blocks
+// takes FIN_BATCH-string batches in ticket order.  Per batch: one count per thread of the first
+// FIN_BATCH, a block scan (wave scans + the wave sums in LDS); wave 0 publishes the batch aggregate,
+// finds the batch's first id by look-back and publishes the inclusive prefix; every string's end
+// offset is written; then ALL the block's threads copy the batch's staged ids -- threads over the
+// batch's OUTPUT ids, so every store is a coalesced row -- FIN_U independent loads in flight per
+// thread.  The last block out resets the counter block for the next call.  Replaces round 1's counter
+// reset, offset scan and compaction (three launches, two more passes over the counts).  512 threads
+// for 256-string batches: 0.345 vs 0.361 ms per 1M strings and 0.067 vs 0.092 ms per 125k than 256
+// (a quarter of the copy parallelism at small batches); smaller batches lengthen the look-back
+// chains (64-string batches: 1.85 ms per 1M) (profiles/r02_ab_issue_model.log).
 template <typename ST>
-__global__ void __launch_bounds__(FIN_BATCH) finish_kernel(FinishArgs f) {
+__global__ void __launch_bounds__(FIN_THREADS) finish_kernel(FinishArgs f) {
     __shared__ uint64_t s_rel[FIN_BATCH + 1];   // ids of the batch's strings before string k, + the batch total
     __shared__ uint64_t s_src[FIN_BATCH];       // staging element of each string's first id
     __shared__ uint64_t s_wsum[FIN_BATCH / 64];
@@ -1742,11 +1754,12 @@ __global__ void __launch_bounds__(FIN_BATCH) finish_kernel(FinishArgs f) {
         const uint64_t t = s_ticket;
         if (t >= n_batches) break;
         const uint64_t s0 = t * FIN_BATCH;
-        const bool has = tid < f.n_str - s0;
+        // the first FIN_BATCH threads hold one string each; every thread copies
+        const bool has = tid < FIN_BATCH && tid < f.n_str - s0;
         const uint64_t c = has ? f.counts[s0 + tid] : 0ull;
         const uint64_t src = has ? f.str_off[s0 + tid] - base_off : 0ull;
         uint64_t incl = wave_incl_scan_add64(c, lane);
-        if (lane == 63) s_wsum[w] = incl;
+        if (lane == 63 && w < FIN_BATCH / 64) s_wsum[w] = incl;
         __syncthreads();
         uint64_t agg = 0;
 #pragma unroll
@@ -1766,9 +1779,11 @@ __global__ void __launch_bounds__(FIN_BATCH) finish_kernel(FinishArgs f) {
             }
             if (lane == 0) s_base = excl;
         }
-        s_rel[tid] = incl - c;
+        if (tid < FIN_BATCH) {
+            s_rel[tid] = incl - c;
+            s_src[tid] = src;
+        }
         if (tid == FIN_BATCH - 1) s_rel[FIN_BATCH] = incl;
-        s_src[tid] = src;
         __syncthreads();
         const uint64_t o0 = s_base, total = agg;
         if (has) f.id_off[s0 + tid + 1] = o0 + incl;
@@ -1778,11 +1793,11 @@ __global__ void __launch_bounds__(FIN_BATCH) finish_kernel(FinishArgs f) {
 #endif
         constexpr unsigned U = FIN_U;
         unsigned j = 0;   // the string of this thread's current id (monotone in k)
-        for (uint64_t k0 = 0; k0 < total; k0 += FIN_BATCH * U) {
+        for (uint64_t k0 = 0; k0 < total; k0 += FIN_THREADS * U) {
             int32_t v[U];
 #pragma unroll
             for (unsigned u = 0; u < U; u++) {
-                const uint64_t k = k0 + (uint64_t)u * FIN_BATCH + tid;
+                const uint64_t k = k0 + (uint64_t)u * FIN_THREADS + tid;
                 v[u] = 0;
                 if (k < total) {
                     while (s_rel[j + 1] <= k) j++;
@@ -1791,7 +1806,7 @@ __global__ void __launch_bounds__(FIN_BATCH) finish_kernel(FinishArgs f) {
             }
 #pragma unroll
             for (unsigned u = 0; u < U; u++) {
-                const uint64_t k = k0 + (uint64_t)u * FIN_BATCH + tid;
+                const uint64_t k = k0 + (uint64_t)u * FIN_THREADS + tid;
                 if (k < total) f.ids[o0 + k] = v[u];
             }
         }
@@ -1971,9 +1986,9 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     f.str_off = p.str_off; f.counts = p.counts; f.n_str = p.n_str; f.id_off = p.id_off; f.ids = p.ids;
     f.flags = p.flags; f.ctr = p.retry_count; f.epoch = p.epoch;
     uint64_t fb = (p.n_str + FIN_BATCH - 1) / FIN_BATCH;
-    if (fb > p.max_blocks / 8) fb = p.max_blocks / 8;   // max_blocks = CUs x 64: at most 8 blocks per CU
-    if (p.staging16) hipLaunchKernelGGL(finish_kernel<int16_t>, dim3((unsigned)fb), dim3(FIN_BATCH), 0, stream, f);
-    else hipLaunchKernelGGL(finish_kernel<int32_t>, dim3((unsigned)fb), dim3(FIN_BATCH), 0, stream, f);
+    if (fb > (uint64_t)p.max_blocks * 32u / FIN_THREADS) fb = (uint64_t)p.max_blocks * 32u / FIN_THREADS;   // max_blocks = CUs x 64: 32 waves per CU
+    if (p.staging16) hipLaunchKernelGGL(finish_kernel<int16_t>, dim3((unsigned)fb), dim3(FIN_THREADS), 0, stream, f);
+    else hipLaunchKernelGGL(finish_kernel<int32_t>, dim3((unsigned)fb), dim3(FIN_THREADS), 0, stream, f);
     return hipGetLastError();
 }
 
