@@ -543,9 +543,6 @@ __device__ bool prep_window(GroupLDS<CH, G> &L, uint8_t *gw, const WinRegs<CH> &
 
 // ------------------------------------------------------------------ the tokenize kernel
 
-#ifndef CLAIM
-#define CLAIM 4       // strings per claim of the work counters
-#endif
 #ifndef NPART
 #define NPART 16      // first-pass work partitions (<= NPART_MAX)
 #endif
@@ -591,17 +588,18 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
     const bool raw = mode == 0;
     const bool uncapped = (a.mode & DPT_FLAG_UNCAPPED) != 0;   // f2: inspect_tokenizer's inf-initialised DP
     const bool len_only = (a.mode & (DPT_FLAG_UNCAPPED | DPT_FLAG_LEN_ONLY)) != 0;
-    // Strings are handed out in chunks of CLAIM strings by npart device counters, one per
-    // contiguous partition of the batch (strings [p n/npart, (p+1) n/npart) -- each in its own
-    // 256-byte line); a wave starts on partition blockIdx mod npart, keeps its claimed range
-    // [q_next, q_end) and, when a claim reaches its partition's end, marks the partition in a shared
-    // mask and moves to the next unmarked one.  Round 1's single counter with one atomic per 4
-    // strings bound the whole kernel: a prep-only build ran 2.91 of the full build's 2.99 ms, every
-    // wave queued behind ~5.6k same-address atomics (profiles/r02_phase_diag.txt).
+    // Strings are handed out by npart device counters, one per contiguous partition of the batch
+    // (strings [p n/npart, (p+1) n/npart) -- each counter in its own 256-byte line): a wave claims as
+    // many strings as it has free slots from its current partition (starting on blockIdx mod npart)
+    // and, when a claim reaches the partition's end, marks the partition in a shared mask and moves
+    // to the next unmarked one.  Round 1's single counter (one same-address atomic per refill) bound
+    // the whole kernel: a prep-only build ran 2.91 of the full build's 2.99 ms, every wave queued
+    // behind ~5.6k others' atomics (profiles/r02_phase_diag.txt).  No string is claimed ahead of a
+    // free slot: strings held in reserve by one wave left others idle at the end of multi-window
+    // batches (cfg4 4.35 -> 4.56 ms with 4-string claims).
     const unsigned npart = BIG ? 1u : (unsigned)min((uint64_t)NPART, max((uint64_t)1, n_work / 4096u));
     unsigned part = BIG ? 0u : blockIdx.x % npart;
     bool exhausted = false, claimed_all = false;
-    uint64_t q_next = 0, q_end = 0;
     // one claim of up to req strings (uniform): [nb, ne), possibly empty once every partition is used up
     auto claim = [&](unsigned req, uint64_t &nb, uint64_t &ne) {
         for (;;) {
@@ -647,33 +645,29 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
 #pragma unroll
             for (int g = 0; g < NG; g++) need |= uni(SS[g].active) ? 0u : (1u << g);
             if (need && !exhausted) {
-                const unsigned n_need = (unsigned)__builtin_popcount(need);
-                // the wave's claimed range first; when it runs short, one claim (the leftover of the
-                // old range is taken first, then the new one)
-                const uint64_t avail = q_end - q_next;
-                uint64_t nb = q_end, ne = q_end;   // the new chunk [nb, ne)
-                if (avail < n_need && !claimed_all) claim((unsigned)CLAIM, nb, ne);
-                const uint64_t take_old = avail < n_need ? avail : n_need;
-                if (lane < (unsigned)NG && ((need >> lane) & 1u)) {
-                    const unsigned k = (unsigned)__builtin_popcount(need & ((1u << lane) - 1u));
-                    const uint64_t idx = k < take_old ? q_next + k : nb + (k - take_old);
-                    if (k < take_old || idx < ne) {
-                        const uint64_t s = BIG ? (uint64_t)a.work_list[idx] : idx;
-                        const uint64_t o0 = a.str_off[s], o1 = a.str_off[s + 1];
-                        SlotState &S = SS[lane];
-                        S.s = (uint32_t)s; S.sb = o0 - base_off; S.slen = (uint32_t)(o1 - o0); S.pos = 0; S.active = 1;
-                        S.status = o1 == o0 ? 2u : 0u;  // pretokenize_raw('') == [[]] -> IndexError
-                        S.ntok = 0; S.capsum = 0; S.abase = 0;
+                // claims until every free slot has a string or every partition is used up (a claim
+                // that reaches a partition's end may return fewer strings than asked)
+                unsigned rem = need;
+                while (rem && !claimed_all) {
+                    const unsigned n_need = (unsigned)__builtin_popcount(rem);
+                    uint64_t nb = 0, ne = 0;
+                    claim(n_need, nb, ne);
+                    const unsigned got = (unsigned)(ne - nb);
+                    if (lane < (unsigned)NG && ((rem >> lane) & 1u)) {
+                        const unsigned k = (unsigned)__builtin_popcount(rem & ((1u << lane) - 1u));
+                        if (k < got) {
+                            const uint64_t idx = nb + k;
+                            const uint64_t s = BIG ? (uint64_t)a.work_list[idx] : idx;
+                            const uint64_t o0 = a.str_off[s], o1 = a.str_off[s + 1];
+                            SlotState &S = SS[lane];
+                            S.s = (uint32_t)s; S.sb = o0 - base_off; S.slen = (uint32_t)(o1 - o0); S.pos = 0; S.active = 1;
+                            S.status = o1 == o0 ? 2u : 0u;  // pretokenize_raw('') == [[]] -> IndexError
+                            S.ntok = 0; S.capsum = 0; S.abase = 0;
+                        }
                     }
+                    for (unsigned q = 0; q < got; q++) rem &= rem - 1u;   // those slots are filled
                 }
-                if (avail < n_need) {
-                    const uint64_t used = nb + (n_need - take_old);
-                    q_next = used < ne ? used : ne;
-                    q_end = ne;
-                } else {
-                    q_next += n_need;
-                }
-                if (claimed_all && q_next >= q_end) exhausted = true;
+                if (claimed_all) exhausted = true;
                 wave_sync();
             }
             unsigned todo = 0;

@@ -1,13 +1,14 @@
 """CPU model of the tokenize kernel's work distribution (dpt_kernels.hip tokenize_kernel, the
-`claim` lambda): npart = min(NPART, max(1, n / 4096)) partition counters over contiguous string
-ranges, claims of CLAIM strings, a used-up mask; each wave starts on partition blockIdx mod npart
-and moves to the next unmarked partition after a claim reaches its partition's end.  Under random
-interleavings of the waves' atomics every string is handed out exactly once and every wave stops."""
+`claim` lambda and the refill loop): npart = min(NPART, max(1, n / 4096)) partition counters over
+contiguous string ranges, claims of as many strings as the wave has free slots (1..4), a used-up
+mask; each wave starts on partition blockIdx mod npart and moves to the next unmarked partition
+after a claim reaches its partition's end.  Under random interleavings of the waves' atomics every
+string is handed out exactly once and every wave stops."""
 import random
 
 import pytest
 
-NPART, CLAIM = 16, 4
+NPART = 16
 
 
 def run(n_work, n_waves, seed):
@@ -19,16 +20,16 @@ def run(n_work, n_waves, seed):
     got = [0] * n_work
     waves = [{"part": w % npart, "q": [], "done": False} for w in range(n_waves)]
 
-    def claim(wv):
+    def claim(wv, req):
         nonlocal mask
         while True:
             p = wv["part"]
             lo, hi = n_work * p // npart, n_work * (p + 1) // npart
-            b = ctr[p]; ctr[p] += CLAIM               # atomicAdd
+            b = ctr[p]; ctr[p] += req                 # atomicAdd
             nb = lo + b
-            ne = min(nb + CLAIM, hi) if nb < hi else nb
+            ne = min(nb + req, hi) if nb < hi else nb
             claimed_all = False
-            if nb + CLAIM >= hi:
+            if nb + req >= hi:
                 old = mask; mask |= 1 << p            # atomicOr
                 m = old | (1 << p)
                 if m & allm == allm:
@@ -45,7 +46,7 @@ def run(n_work, n_waves, seed):
     while live:
         w = rnd.choice(live)                           # any wave may take the next atomic
         wv = waves[w]
-        idx, claimed_all = claim(wv)
+        idx, claimed_all = claim(wv, rnd.randint(1, 4))   # the wave's free slots
         for i in idx:
             got[i] += 1
         if claimed_all:
