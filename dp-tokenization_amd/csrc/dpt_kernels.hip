@@ -11,30 +11,30 @@
 //          offsets, code-point prefix sums (cp(span) = cpos[i]-cpos[j], the len(t) of
 //          dp_tokenize.py:82) with word-start bits, and the word list -- one packed DPP scan.
 //          Atoms are expanded ('▁'+c first, ' '->'▁', '\n'->'<0x0A>') on the fly later.
-//   A      match discovery: lanes walk the byte double-array trie (L2-resident)
-//          from every atom start of every slot, two walks per lane; bit (L-1) of smask[j]
-//          records that the L-atom span from atom j is a vocabulary token ("join(atoms[j:i])
-//          in vocabulary", dp_tokenize.py:39).  Walks that finish take the next start
-//          (ballot + mbcnt), so the wave stays busy.
-//   B      forward recurrence, sequential over end positions i; lane d of a group
-//          holds candidate j = i-1-d and forms ONE 32-bit key
+//   A      match discovery: one walk per lane over the byte double-array trie (L2-resident)
+//          from every atom start of every slot (pure-ASCII raw windows: every walk's first
+//          lookup byte-parallel first, A0); a token of L atoms ending at e clears bit L-1 of e's
+//          inverted END mask ("join(atoms[j:i]) in vocabulary", dp_tokenize.py:39).  Walks that
+//          finish take the next start (ballot + mbcnt), so the wave stays busy.
+//   B      forward recurrence (cost capped at the atom index within
+//          the word, dp_tokenize.py:28; reachability; the max-of-max token length G[i]).  Lane
+//          mode (every atom a token by itself, the common case): each lane runs the recurrence
+//          sequentially over a chunk cut at cut points (boundaries no token crosses), a row scan
+//          of the chunk transfers supplies each chunk's incoming state.  Row mode (otherwise):
+//          lane d of a group holds candidate j = i-1-d and forms one key
 //              (cost[j]+1) << 16 | invalid[j] << 15 | (0x7FFF - max(G[j], cp(span)))
-//          a DPP group-min gives cost[i] (capped at the atom index within the word,
-//          dp_tokenize.py:28), reachability and the max-of-max token length G[i]
-//          (SURVEY.md Appendix A 1-3).  Two ballots give, per end i, the largest j in E(i)
-//          (dp_tokenize.py:40-46) that is reachable (de) and the largest that attains G[i]
-//          (dg); both are packed with the key into fin[i].  The per-lane state moves one
-//          lane per step by DPP row_shr:1 / wave_shr:1 -- no LDS on the recurrence.
-//   C0     per-slot token counts and validity of the window (one lane per word).
-//   C1     selection, one lane per word: walking right to left, take dg while the longest
-//          token so far is below G[n], de once it is reached.  That is the reference's first
-//          argmax in DFS order (dp_tokenize.py:58 pops the largest j first; :84 takes the
-//          first max).
+//          whose DPP group-min is the state of i; two ballots give the largest j in E(i)
+//          (dp_tokenize.py:40-46) that is reachable (de) and the largest that attains G[i] (dg).
+//   C0/C1  token counts, validity and the selection: walking right to left, take dg while the
+//          longest token so far is below G[n], de once it is reached -- the reference's first
+//          argmax in DFS order (dp_tokenize.py:58 pops the largest j first; :84 takes the first
+//          max).  Lane mode walks its chunks, row mode one word per lane.
 //   C2     id resolution: lanes re-walk each selected span through the trie and write
 //          t2i[token] (tokenizer_utils.py:76-79) to the slot's staging row.
 //
-// Strings whose single word exceeds CH bytes are re-run by the 2048-byte, one-string-per-wave
-// instantiation.  A scan + compaction turns the staging rows into CSR ids.
+// Strings are claimed from 16 partition counters (see tokenize_kernel).  Strings whose single word
+// exceeds CH bytes are re-run by the 2048-byte, one-string-per-wave instantiation, longer ones by
+// the unbounded pass (dpt_long.hip).  The finish kernel turns the staging rows into CSR ids.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
