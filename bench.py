@@ -386,6 +386,35 @@ def main():
     ms_stage, launches = enc.profile_read()
     enc.profile(False)
 
+    # secondary: the encode alone through dpt_encode_padded (ids left at each string's byte offset,
+    # per-string counts; no finish pass, no histogram) -- reported beside `value`, never as it
+    d_pids = torch.empty(max(n_bytes, 1), dtype=torch.int32, device=dev)
+    d_cnt = torch.empty(max(M, 1), dtype=torch.int64, device=dev)
+    d_pst = torch.empty(max(M, 1), dtype=torch.int32, device=dev)
+
+    def step_padded():
+        enc.encode_device_padded(d_text.data_ptr(), n_bytes, d_off.data_ptr(), M, d_pids.data_ptr(), max(n_bytes, 1),
+                                 d_cnt.data_ptr(), d_pst.data_ptr(), stream=stream,
+                                 cut_ptr=d_cut.data_ptr() if bloom else 0, mode="atoms" if bloom else "raw")
+
+    for _ in range(args.warmup):
+        step_padded()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0p = time.perf_counter()
+    for _ in range(args.steps):
+        step_padded()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dtp = time.perf_counter() - t0p
+    if world > 1:
+        t = torch.tensor([dtp], dtype=torch.float64, device=red_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dtp = float(t.item())
+    padded_same = bool(torch.equal(d_cnt[:M], (d_idoff[1:] - d_idoff[:-1])[:M]) and torch.equal(d_pst[:M], d_status[:M]))
+
     hist = d_hist.cpu().numpy()
     n_tok_rank = int(d_idoff[-1].item())
     n_tok_all = int(hist[N_BINS])          # after the all-reduce: all ranks' ids
@@ -458,6 +487,9 @@ def main():
                          "alg_bytes_staged_width": alg_staged, "staged_id_bytes": id_bytes,
                          "frac_staged_width": alg_staged / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
             "cpu_baseline": cpu,
+            "padded_layout": {"api": "dpt_encode_padded (ids at each string's byte offset + per-string counts, no CSR pass); encode only, no histogram",
+                              "ms_per_step": dtp / args.steps * 1e3, "bytes_per_s": bytes_all * args.steps / dtp,
+                              "counts_and_status_equal_csr": padded_same},
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -116,10 +116,12 @@ uint64_t default_long_bytes(uint64_t n_bytes) {
 constexpr uint64_t ARENA_PER_BYTE = 20;   // uint4 rec + int32 stg (dpt_long.hip)
 constexpr size_t COUNTER_BYTES = 64;
 
-// v == nullptr: both staging widths (the vocabulary is not known yet)
-int ensure_workspace(dpt_ctx *c, const dpt_vocab *v, uint64_t n_bytes, uint64_t n_str, uint64_t long_bytes) {
+// v == nullptr: both staging widths (the vocabulary is not known yet); staging = false: no staging
+// (dpt_encode_padded writes the ids into the caller's buffer)
+int ensure_workspace(dpt_ctx *c, const dpt_vocab *v, uint64_t n_bytes, uint64_t n_str, uint64_t long_bytes,
+                     bool staging = true) {
     hipError_t e;
-    const bool need16 = !v || v->ids16, need32 = !v || !v->ids16;
+    const bool need16 = staging && (!v || v->ids16), need32 = staging && (!v || !v->ids16);
     if (need16 && (e = grow(&c->staging16, &c->cap16, n_bytes)) != hipSuccess) return hip_fail(e, "hipMalloc(staging16)");
     if (need32 && (e = grow(&c->staging32, &c->cap32, n_bytes)) != hipSuccess) return hip_fail(e, "hipMalloc(staging32)");
     const uint64_t lb = long_bytes ? long_bytes : default_long_bytes(n_bytes);
@@ -342,19 +344,20 @@ int dpt_ctx_long_need(dpt_ctx *c, uint64_t *need, uint64_t *cap) {
 static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uint8_t *text, uint64_t n_bytes,
                        const uint64_t *str_off, const uint8_t *cut_mask, uint64_t n_str, int32_t *ids, uint64_t ids_cap,
                        uint64_t *id_off, int32_t *status, int32_t *capped_len, uint64_t *edges, void *hip_stream,
-                       uint64_t *far = nullptr, uint64_t far_cap = 0) {
+                       uint64_t *far = nullptr, uint64_t far_cap = 0, uint64_t *padded_counts = nullptr) {
     const int mode = mode_flags & DPT_MODE_MASK;
     if (!c || !v) return fail(DPT_E_ARG, "null ctx or vocab");
     if (mode != DPT_MODE_RAW && mode != DPT_MODE_PRESPLIT && mode != DPT_MODE_ATOMS) return fail(DPT_E_ARG, "bad mode");
     if (mode_flags & ~(DPT_MODE_MASK | DPT_FLAG_UNCAPPED | DPT_FLAG_LEN_ONLY)) return fail(DPT_E_ARG, "bad flags");
-    if (!str_off || !id_off || (n_str && !status)) return fail(DPT_E_ARG, "null output/offsets");
+    const bool padded = padded_counts != nullptr;
+    if (!str_off || (!id_off && !padded) || (n_str && !status)) return fail(DPT_E_ARG, "null output/offsets");
     if (n_bytes && (!text || !ids)) return fail(DPT_E_ARG, "null text/ids");
     if (mode != DPT_MODE_RAW && n_bytes && !cut_mask) return fail(DPT_E_ARG, "PRESPLIT/ATOMS need cut_mask");
     if (ids_cap < n_bytes) return fail(DPT_E_CAP, "ids_cap must be >= n_bytes");
     if (n_str > 0x7FFFFFFFull) return fail(DPT_E_ARG, "too many strings for one call (max 2^31-1)");
     if (c->device != v->device) return fail(DPT_E_ARG, "ctx and vocab on different devices");
     DeviceGuard g(c->device);
-    int rc = ensure_workspace(c, v, n_bytes, n_str, 0);
+    int rc = ensure_workspace(c, v, n_bytes, n_str, 0, !padded);
     if (rc) return rc;
     hipStream_t st = (hipStream_t)hip_stream;
     dpt::EncodeLaunch p;
@@ -390,6 +393,12 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
     p.variant = kernel_variant(v->stats.max_cp);
     // int16 staging when every id fits in 0..32767 (half the staging traffic)
     p.staging16 = v->ids16 ? c->staging16 : nullptr;
+    p.padded = padded;
+    if (padded) {   // the ids go straight to their final place (int32), the counts to the caller's array
+        p.staging = ids;
+        p.staging16 = nullptr;
+        p.counts = padded_counts;
+    }
     p.slots = v->d_slots;
     p.slot_ids = v->d_ids;
     p.n_slots = v->stats.n_slots;
@@ -420,6 +429,15 @@ int dpt_encode(dpt_ctx *c, const dpt_vocab *v, int mode, const uint8_t *text, ui
     if (mode & ~DPT_MODE_MASK) return fail(DPT_E_ARG, "flags are for dpt_dp_host");
     return encode_impl(c, v, mode, text, n_bytes, str_off, cut_mask, n_str, ids, ids_cap, id_off, status, capped_len,
                        nullptr, hip_stream);
+}
+
+int dpt_encode_padded(dpt_ctx *c, const dpt_vocab *v, int mode, const uint8_t *text, uint64_t n_bytes,
+                      const uint64_t *str_off, const uint8_t *cut_mask, uint64_t n_str, int32_t *ids, uint64_t ids_cap,
+                      uint64_t *counts, int32_t *status, int32_t *capped_len, void *hip_stream) {
+    if (mode & ~DPT_MODE_MASK) return fail(DPT_E_ARG, "flags are for dpt_dp_host");
+    if (!counts) return fail(DPT_E_ARG, "null counts");
+    return encode_impl(c, v, mode, text, n_bytes, str_off, cut_mask, n_str, ids, ids_cap, nullptr, status, capped_len,
+                       nullptr, hip_stream, nullptr, 0, counts);
 }
 
 static int encode_host_impl(dpt_ctx *c, const dpt_vocab *v, int mode, const uint8_t *text, uint64_t n_bytes,

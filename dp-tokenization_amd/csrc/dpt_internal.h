@@ -34,6 +34,7 @@ struct EncodeLaunch {
     unsigned epoch;              // the ctx's call counter (1..65535)
     unsigned max_blocks;
     int variant;             // KERNEL_* below
+    bool padded;             // dpt_encode_padded: staging = the caller's ids, counts = the caller's; no finish pass
     uint8_t *arena;          // the unbounded pass's scratch: 20 bytes per input byte of the strings it takes
     uint64_t arena_cap;      // input bytes the arena holds
     // vocabulary

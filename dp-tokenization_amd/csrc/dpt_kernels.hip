@@ -1731,6 +1731,21 @@ __device__ __forceinline__ uint64_t finish_lookback(const FinishArgs &f, uint64_
 // for 256-string batches: 0.345 vs 0.361 ms per 1M strings and 0.067 vs 0.092 ms per 125k than 256
 // (a quarter of the copy parallelism at small batches); smaller batches lengthen the look-back
 // chains (64-string batches: 1.85 ms per 1M) (profiles/r02_ab_issue_model.log).
+// Reset the counter block for the next call (the claimed arena bytes and far pairs stay readable as
+// the call's "last need" / "last far").
+__device__ __forceinline__ void reset_counters(uint32_t *ctr) {
+    uint64_t *c64 = reinterpret_cast<uint64_t *>(ctr);
+    c64[CTR_LASTNEED64] = c64[CTR_ARENA64];
+    c64[CTR_ARENA64] = 0;
+    c64[CTR_LASTFAR64] = c64[CTR_FAR64];
+    c64[CTR_FAR64] = 0;
+    ctr[0] = 0; ctr[1] = 0; ctr[2] = 0; ctr[3] = 0; ctr[4] = 0;
+    uint32_t *pc = ctr + PART_CTR_OFFSET / 4;
+    for (unsigned q = 0; q <= NPART; q++) pc[q * PART_STRIDE] = 0;   // the partition counters and the mask
+    ctr[CTR_TICKET] = 0;
+    ctr[CTR_DONE] = 0;
+}
+
 template <typename ST>
 __global__ void __launch_bounds__(FIN_THREADS) finish_kernel(FinishArgs f) {
     __shared__ uint64_t s_rel[FIN_BATCH + 1];   // ids of the batch's strings before string k, + the batch total
@@ -1808,21 +1823,14 @@ __global__ void __launch_bounds__(FIN_THREADS) finish_kernel(FinishArgs f) {
     }
     if (tid == 0) {
         const unsigned d = atomicAdd(&f.ctr[CTR_DONE], 1u);
-        if (d + 1 == gridDim.x) {
-            // the last block out: every ticket is taken and every tokenize pass is done -- reset the
-            // counters for the next call (the claimed arena bytes stay readable as "last need")
-            uint64_t *c64 = reinterpret_cast<uint64_t *>(f.ctr);
-            c64[CTR_LASTNEED64] = c64[CTR_ARENA64];
-            c64[CTR_ARENA64] = 0;
-            c64[CTR_LASTFAR64] = c64[CTR_FAR64];
-            c64[CTR_FAR64] = 0;
-            f.ctr[0] = 0; f.ctr[1] = 0; f.ctr[2] = 0; f.ctr[3] = 0; f.ctr[4] = 0;
-            uint32_t *pc = f.ctr + PART_CTR_OFFSET / 4;
-            for (unsigned q = 0; q <= NPART; q++) pc[q * PART_STRIDE] = 0;   // the partition counters and the mask
-            f.ctr[CTR_TICKET] = 0;
-            f.ctr[CTR_DONE] = 0;
-        }
+        // the last block out: every ticket is taken and every tokenize pass is done
+        if (d + 1 == gridDim.x) reset_counters(f.ctr);
     }
+}
+
+// dpt_encode_padded runs no finish pass: one lane resets the counter block after the tokenize passes
+__global__ void __launch_bounds__(64) reset_kernel(uint32_t *ctr) {
+    if (threadIdx.x == 0) reset_counters(ctr);
 }
 
 // ------------------------------------------------------------------ histogram
@@ -1923,8 +1931,10 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     if (p.n_str == 0) {
         // no finish kernel runs: id_off[0] = 0, and the call's claimed arena bytes ("last need") and
         // far edge pairs are 0 (bytes 40..63 of the counter block; the running counters are 0 already)
-        const hipError_t e0 = hipMemsetAsync(p.id_off, 0, sizeof(uint64_t), stream);
-        if (e0 != hipSuccess) return e0;
+        if (p.id_off) {   // (dpt_encode_padded has no offsets)
+            const hipError_t e0 = hipMemsetAsync(p.id_off, 0, sizeof(uint64_t), stream);
+            if (e0 != hipSuccess) return e0;
+        }
         return hipMemsetAsync(reinterpret_cast<uint64_t *>(p.retry_count) + CTR_LASTNEED64, 0, 3 * sizeof(uint64_t), stream);
     }
     if (ev) {
@@ -1974,6 +1984,10 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     if (ev) {
         const hipError_t er = hipEventRecord(ev[1], stream);
         if (er != hipSuccess) return er;
+    }
+    if (p.padded) {   // dpt_encode_padded: the ids are in place; only the counters need their reset
+        hipLaunchKernelGGL(reset_kernel, dim3(1), dim3(64), 0, stream, p.retry_count);
+        return hipGetLastError();
     }
     FinishArgs f;
     f.staging = p.staging16 ? (const void *)p.staging16 : (const void *)p.staging;

@@ -273,6 +273,17 @@ class Encoder:
                                     ctypes.c_void_p(status_ptr), ctypes.c_void_p(capped_ptr or None),
                                     ctypes.c_void_p(stream or None)), "dpt_encode")
 
+    def encode_device_padded(self, text_ptr: int, n_bytes: int, off_ptr: int, n_str: int, ids_ptr: int, ids_cap: int,
+                             counts_ptr: int, status_ptr: int, capped_ptr: int = 0, cut_ptr: int = 0, stream: int = 0,
+                             mode="raw") -> None:
+        """dpt_encode_padded: string s's ids stay at its byte offset, ids[str_off[s]-str_off[0] + k] for
+        k < counts[s] (uint64); no CSR packing pass.  Device addresses, stream-ordered, no sync."""
+        check(_lib.lib().dpt_encode_padded(self.handle, self.vocab.handle, MODES[mode], ctypes.c_void_p(text_ptr), n_bytes,
+                                           ctypes.c_void_p(off_ptr), ctypes.c_void_p(cut_ptr or None), n_str,
+                                           ctypes.c_void_p(ids_ptr), ids_cap, ctypes.c_void_p(counts_ptr),
+                                           ctypes.c_void_p(status_ptr), ctypes.c_void_p(capped_ptr or None),
+                                           ctypes.c_void_p(stream or None)), "dpt_encode_padded")
+
     def reserve(self, n_bytes: int, n_str: int, long_bytes: int = 0) -> None:
         """Pre-size the workspace for this vocabulary's staging width (a later call of that size is
         capture-safe); ``long_bytes``: input bytes the unbounded pass holds per call (0: default)."""

@@ -136,6 +136,19 @@ int dpt_encode(dpt_ctx *c, const dpt_vocab *v, int mode, const uint8_t *text, ui
                uint64_t ids_cap, uint64_t *id_off, int32_t *status, int32_t *capped_len,
                void *hip_stream);
 
+/*
+ * dpt_encode without the CSR packing: the ids of string s stay at the string's own byte offset,
+ * ids[str_off[s]-str_off[0] + k] for k < counts[s] (uint64 per string; 0 when status[s] != 0) --
+ * the layout the tokenize passes write, so the finish pass (offsets + compaction, about 11 % of a
+ * cfg2 call) does not run.  For callers that consume per-string id lists -- the dp_tokenize
+ * closure's List[int] per string (reference packages/tokenizer_utils.py:66-80) -- rather than
+ * one packed array.  Same arguments, limits and stream semantics as dpt_encode; ids_cap >= n_bytes.
+ */
+int dpt_encode_padded(dpt_ctx *c, const dpt_vocab *v, int mode, const uint8_t *text, uint64_t n_bytes,
+                      const uint64_t *str_off, const uint8_t *cut_mask, uint64_t n_str, int32_t *ids,
+                      uint64_t ids_cap, uint64_t *counts, int32_t *status, int32_t *capped_len,
+                      void *hip_stream);
+
 /* Same with HOST pointers: copies in, runs, copies out, synchronises. */
 int dpt_encode_host(dpt_ctx *c, const dpt_vocab *v, int mode, const uint8_t *text, uint64_t n_bytes,
                     const uint64_t *str_off, const uint8_t *cut_mask, uint64_t n_str, int32_t *ids,

@@ -39,6 +39,10 @@ def test_errors_without_device_or_args():
     assert rc == -1
     rc = L.dpt_vocab_create(None, None, None, 0, 0, ctypes.byref(h))
     assert rc == -1 and L.dpt_last_error()
+    # dpt_encode_padded checks its arguments before any device work: null ctx / vocab, null counts
+    off0 = (ctypes.c_uint64 * 1)(0)
+    assert L.dpt_encode_padded(None, None, 0, None, 0, off0, None, 0, None, 0, None, None, None, None) == -1
+    assert b"counts" in L.dpt_last_error()
     if not torch.cuda.is_available():
         off = (ctypes.c_uint64 * 2)(0, 1)
         blob = ctypes.create_string_buffer(b"a")

@@ -523,3 +523,44 @@ def test_work_partitions_vs_oracle(n, engines, oracles):
     ref = oracles["llama32k"].encode_csr(text, offs)
     for _ in range(3):
         _cmp_csr(engines["llama32k"].encode_csr(text, offs), ref)
+
+
+def test_encode_padded_matches_csr(vocabs, engines):
+    """dpt_encode_padded (ids left at each string's byte offset, per-string counts, no finish pass)
+    equals dpt_encode's CSR output on ragged strings -- empty ones, words over 256 bytes (the
+    2048-byte pass) and over 2048 bytes (the unbounded pass, which writes into the caller's buffer) --
+    over repeated calls on one ctx interleaved with dpt_encode (the counter resets of both paths)."""
+    torch = pytest.importorskip("torch")
+    from dptok import synth
+    enc = engines["llama32k"]
+    s = torch.cuda.current_stream().cuda_stream
+    rng = np.random.default_rng(5)
+    text, offs = synth.random_ascii_corpus(30000, 128, seed=51)
+    parts = [text[i * 128:i * 128 + int(rng.integers(0, 129))].tobytes() for i in range(30000)]
+    parts[7] = b"x" * 900                  # one word over 256 bytes
+    parts[9] = b"ab" * 1500                # one word over 2048 bytes
+    parts[11] = b""
+    offs = np.zeros(len(parts) + 1, np.uint64)
+    offs[1:] = np.cumsum([len(p) for p in parts])
+    text = np.frombuffer(b"".join(parts) + b"\0", np.uint8)
+    n, nb = len(parts), int(offs[-1])
+    dt = torch.from_numpy(np.array(text)).cuda()
+    do = torch.from_numpy(offs.view(np.int64)).cuda()
+    for rep in range(3):
+        ids = torch.full((nb,), -9, dtype=torch.int32, device="cuda")
+        io = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+        st = torch.empty(n, dtype=torch.int32, device="cuda")
+        enc.encode_device(dt.data_ptr(), nb, do.data_ptr(), n, ids.data_ptr(), nb, io.data_ptr(), st.data_ptr(), stream=s)
+        pids = torch.full((nb,), -9, dtype=torch.int32, device="cuda")
+        cnt = torch.full((n,), 7, dtype=torch.int64, device="cuda")
+        pst = torch.empty(n, dtype=torch.int32, device="cuda")
+        enc.encode_device_padded(dt.data_ptr(), nb, do.data_ptr(), n, pids.data_ptr(), nb, cnt.data_ptr(), pst.data_ptr(), stream=s)
+        torch.cuda.synchronize()
+        off_h = io.cpu().numpy().view(np.uint64)
+        ids_h, pids_h, cnt_h = ids.cpu().numpy(), pids.cpu().numpy(), cnt.cpu().numpy()
+        assert np.array_equal(pst.cpu().numpy(), st.cpu().numpy())
+        assert np.array_equal(cnt_h.astype(np.uint64), np.diff(off_h)), rep
+        for i in range(n):
+            a, b = int(offs[i]), int(off_h[i])
+            c = int(cnt_h[i])
+            assert np.array_equal(pids_h[a:a + c], ids_h[b:b + c]), (rep, i)
