@@ -169,7 +169,8 @@ class Encoder:
     def encode_strs(self, texts: Sequence[str]) -> List[Tuple[List[int], int]]:
         text, offs = pack_strings(texts)
         ids, id_off, st, _ = self.encode_csr(text, offs)
-        return [(ids[int(id_off[i]):int(id_off[i + 1])].tolist(), int(st[i])) for i in range(len(texts))]
+        flat, o, sl = ids.tolist(), id_off.tolist(), st.tolist()   # one conversion each, then list slices
+        return [(flat[o[i]:o[i + 1]], sl[i]) for i in range(len(texts))]
 
     def encode_presplit(self, strings: Sequence[Sequence[str]]) -> List[Tuple[List[int], int]]:
         """Many strings, each pre-split into words (llama mode, DPT_MODE_PRESPLIT), in ONE launch:
