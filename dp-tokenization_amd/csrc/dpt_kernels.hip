@@ -1480,9 +1480,8 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
 #endif
         if (DPT_RUN_C2) {
             unsigned pre[NG + 1], na_g[NG];
-            uint8_t *obase[NG];       // staging row of the window's first token, per slot
+            uint64_t obase[NG];       // staging element of the window's first token, per slot
             const bool n16 = SW == 1 || (SW == 0 && a.staging16 != nullptr);   // int16 staging (uniform)
-            const unsigned esh = n16 ? 1u : 2u;
             unsigned firstmask = 0;   // groups whose window starts the string (raw '▁' + first atom)
             pre[0] = 0;
 #pragma unroll
@@ -1492,7 +1491,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 na_g[g] = uni(SS[g].n_atoms);
                 firstmask |= (uni64(SS[g].pos) == 0 ? 1u : 0u) << g;
                 const uint64_t e0 = uni64(SS[g].sb) + uni(SS[g].ntok);
-                obase[g] = n16 ? reinterpret_cast<uint8_t *>(a.staging16 + e0) : reinterpret_cast<uint8_t *>(a.staging + e0);
+                obase[g] = e0;
             }
             const unsigned total = pre[NG];
             // per-slot token range, atom count, first-window flag and staging row, in the slot's
@@ -1500,7 +1499,9 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
             // instead of selecting among NG sets of registers
             struct C2Slot {
                 uint32_t base, ntk, na, fw;
-                uint8_t *ob;
+                uint64_t ob;   // staging element (an offset, not a pointer: stores through a.staging* stay
+                               // global_store -- a pointer read back from LDS becomes a flat store, whose
+                               // lgkmcnt makes the next LDS wait on the store's completion)
             };
             static_assert(sizeof(typename GR::Fin) * GL::NA >= sizeof(C2Slot), "C2Slot fits fin[]");
             if (lane == 0) {
@@ -1519,7 +1520,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
             struct Tok {
                 unsigned jj, j1, cnt, lbase;
                 uint64_t seq;
-                uint8_t *out;
+                uint64_t out;
             };
             auto tstart = [&](unsigned t) -> Tok {
                 Tok T;
@@ -1534,7 +1535,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 const unsigned nx = (unsigned)L.rec[k + 1].smask;   // k + 1 <= ntk < NA
                 T.j1 = k + 1 < q.ntk ? nx : q.na;
                 T.seq = atom_from_info<CH, WIDE>(L.bytes, AInfo<CH>::pack(L.aoff[T.jj], L.atom_len(T.jj), 0, (raw ? 1u : 0u) & q.fw & (unsigned)(T.jj == 0)), raw, T.cnt);
-                T.out = q.ob + (k << esh);
+                T.out = q.ob + k;
                 return T;
             };
 #ifndef C2_WALKS
@@ -1550,7 +1551,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
 #pragma unroll
             for (int w = 0; w < NW; w++) {
                 active[w] = lane + 64u * w < total;
-                C[w].jj = C[w].j1 = C[w].cnt = C[w].lbase = 0; C[w].seq = 0; C[w].out = nullptr;
+                C[w].jj = C[w].j1 = C[w].cnt = C[w].lbase = 0; C[w].seq = 0; C[w].out = 0;
                 if (active[w]) C[w] = tstart(lane + 64u * w);
                 node[w] = 0; nb[w] = tv.root_base; ok[w] = true;
             }
@@ -1591,8 +1592,8 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                     const uint64_t dm = ballot(done[w]);
                     if (done[w]) {
                         const int32_t idv = ok[w] ? ent[w].z : -1;   // the id arrives with the token's last node
-                        if (n16) *reinterpret_cast<int16_t *>(C[w].out) = (int16_t)idv;
-                        else *reinterpret_cast<int32_t *>(C[w].out) = idv;
+                        if (n16) a.staging16[C[w].out] = (int16_t)idv;
+                        else a.staging[C[w].out] = idv;
                         const unsigned uu = nxt + __builtin_amdgcn_mbcnt_hi((unsigned)(dm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)dm, 0u));
                         active[w] = uu < total;
                         if (active[w]) C[w] = tstart(uu);
