@@ -325,6 +325,15 @@ def main():
     if gpu != local and args.dist_backend == "nccl":
         raise SystemExit(f"local rank {local} has no GPU of its own; use --dist-backend gloo to share one")
     ddist.init_from_env(args.dist_backend, device=gpu)
+    # DPT_BENCH_COLL=1: run the per-step all-reduce even at world size 1 (a rehearsal of the async RCCL
+    # path on a one-GPU box; the real runs have world > 1)
+    coll = world > 1 or os.environ.get("DPT_BENCH_COLL") == "1"
+    if coll and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29655")
+        torch.cuda.set_device(gpu)
+        dist.init_process_group(args.dist_backend, rank=0, world_size=1,
+                                **({"device_id": torch.device("cuda", gpu)} if args.dist_backend == "nccl" else {}))
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
     red_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
@@ -337,23 +346,39 @@ def main():
     d_ids = torch.empty(max(n_bytes, 1), dtype=torch.int32, device=dev)
     d_idoff = torch.empty(M + 1, dtype=torch.int64, device=dev)
     d_status = torch.empty(max(M, 1), dtype=torch.int32, device=dev)
-    d_hist = torch.zeros(N_BINS + 8, dtype=torch.int64, device=dev)
+    # two histogram buffers: step k's all-reduce (RCCL, on its own stream, async) overlaps step k+1's
+    # tokenize, which fills the other buffer; a buffer is reused only after its all-reduce completed
+    d_hists = [torch.zeros(N_BINS + 8, dtype=torch.int64, device=dev) for _ in range(2)]
+    pending = [None, None]
+    n_step = [0]
     enc.reserve(n_bytes, M)
     stream = torch.cuda.current_stream(dev).cuda_stream
 
     def step():
+        b = n_step[0] % 2
+        n_step[0] += 1
+        h = d_hists[b]
         enc.encode_device(d_text.data_ptr(), n_bytes, d_off.data_ptr(), M, d_ids.data_ptr(), max(n_bytes, 1),
                           d_idoff.data_ptr(), d_status.data_ptr(), stream=stream,
                           cut_ptr=d_cut.data_ptr() if bloom else 0, mode="atoms" if bloom else "raw")
-        d_hist.zero_()
-        enc.histogram_device(d_idoff.data_ptr(), d_status.data_ptr(), M, d_hist.data_ptr(), N_BINS, stream=stream)
-        if world > 1:   # the single collective: RCCL over xGMI with nccl, gloo in rehearsals
+        if pending[b] is not None:   # the stream waits for this buffer's previous all-reduce
+            pending[b].wait()
+            pending[b] = None
+        h.zero_()
+        enc.histogram_device(d_idoff.data_ptr(), d_status.data_ptr(), M, h.data_ptr(), N_BINS, stream=stream)
+        if coll:   # the single collective: RCCL over xGMI with nccl, gloo in rehearsals
             if red_dev.type == "cpu":
-                h = d_hist.cpu()
-                ddist.allreduce_histogram(h)
-                d_hist.copy_(h)
+                hc = h.cpu()
+                ddist.allreduce_histogram(hc)
+                h.copy_(hc)
             else:
-                ddist.allreduce_histogram(d_hist)
+                pending[b] = ddist.allreduce_histogram(h, async_op=True)
+
+    def drain():   # every outstanding all-reduce is ordered before what the stream does next
+        for b in range(2):
+            if pending[b] is not None:
+                pending[b].wait()
+                pending[b] = None
 
     def all_sum(x: float) -> float:
         if world == 1:
@@ -365,6 +390,7 @@ def main():
     log("GPU ready, warmup")
     for _ in range(args.warmup):
         step()
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -375,6 +401,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -415,7 +442,7 @@ def main():
         dtp = float(t.item())
     padded_same = bool(torch.equal(d_cnt[:M], (d_idoff[1:] - d_idoff[:-1])[:M]) and torch.equal(d_pst[:M], d_status[:M]))
 
-    hist = d_hist.cpu().numpy()
+    hist = d_hists[(n_step[0] - 1) % 2].cpu().numpy()   # the last step's reduced histogram
     n_tok_rank = int(d_idoff[-1].item())
     n_tok_all = int(hist[N_BINS])          # after the all-reduce: all ranks' ids
     ok_strings = int(hist[N_BINS + 2])

@@ -34,12 +34,15 @@ def histogram_layout(n_bins: int) -> dict:
             "status": slice(n_bins + 2, n_bins + 7)}
 
 
-def allreduce_histogram(hist, group=None):
-    """Sum a histogram tensor (int64, n_bins + N_EXTRA) over all ranks in place."""
+def allreduce_histogram(hist, group=None, async_op: bool = False):
+    """Sum a histogram tensor (int64, n_bins + N_EXTRA) over all ranks in place.  async_op: return
+    the collective's work handle (``wait()`` orders it before the caller's stream continues) -- the
+    RCCL all-reduce then overlaps whatever the stream does next; None when there is nothing to do."""
     import torch.distributed as dist
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
-        dist.all_reduce(hist, op=dist.ReduceOp.SUM, group=group)
-    return hist
+    if dist.is_available() and dist.is_initialized():
+        work = dist.all_reduce(hist, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
+        return work if async_op else hist
+    return None if async_op else hist
 
 
 def init_from_env(backend: str = "nccl", device=None):

@@ -26,10 +26,16 @@ h = np.zeros(NB + ddist.N_EXTRA, dtype=np.int64)
 np.add.at(h, np.minimum(cnt, NB - 1), 1)
 h[NB] = cnt.sum(); h[NB + 1] = hi - lo
 np.add.at(h, NB + 2 + st, 1)
-t = torch.from_numpy(h)
+t = torch.from_numpy(h.copy())
 ddist.allreduce_histogram(t)
+# bench.py's overlapped form: two buffers in flight as async collectives, waited out of order
+a, b = torch.from_numpy(h.copy()), torch.from_numpy(2 * h)
+wa = ddist.allreduce_histogram(a, async_op=True)
+wb = ddist.allreduce_histogram(b, async_op=True)
+wb.wait(); wa.wait()
 if rank == 0:
     print("HIST", json.dumps(t.tolist()))
+    print("ASYNC", int(torch.equal(a, t) and torch.equal(b, 2 * t)))
 dist.destroy_process_group()
 '''
 
@@ -78,3 +84,4 @@ def test_histogram_allreduce_world2(tmp_path):
     import json
     got = np.array(json.loads(line[5:]), dtype=np.int64)
     assert np.array_equal(got, _single_process_hist())
+    assert "ASYNC 1" in out.stdout
