@@ -87,3 +87,33 @@ def test_bloom_scale_synthetic_corpus_vs_oracle(big):
     assert np.array_equal(st, rst)
     assert np.array_equal(np.asarray(id_off, dtype=np.uint64), np.asarray(roff, dtype=np.uint64))
     assert np.array_equal(ids[: int(roff[-1])], rids)
+
+
+@pytest.mark.gpu
+def test_bloom_scale_padded_layout_vs_oracle(big):
+    """dpt_encode_padded with the 250k-entry vocabulary (64-lane rows kernel, int32 ids, atoms mode):
+    each string's ids at its byte offset equal the C oracle's."""
+    torch = pytest.importorskip("torch")
+    from dptok import Encoder, Vocab, synth
+    from oracle import oracle
+    v = big["vocab"]
+    text, offs, cut = synth.bloom_like_corpus(2000, v, seed=11)
+    enc = Encoder(Vocab(v, 0))
+    n, nb = len(offs) - 1, int(offs[-1])
+    dt = torch.from_numpy(np.array(text)).cuda()
+    do = torch.from_numpy(np.asarray(offs, dtype=np.uint64).view(np.int64)).cuda()
+    dc = torch.from_numpy(np.array(cut)).cuda()
+    pids = torch.full((nb,), -9, dtype=torch.int32, device="cuda")
+    cnt = torch.empty(n, dtype=torch.int64, device="cuda")
+    pst = torch.empty(n, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    enc.encode_device_padded(dt.data_ptr(), nb, do.data_ptr(), n, pids.data_ptr(), nb, cnt.data_ptr(), pst.data_ptr(),
+                             cut_ptr=dc.data_ptr(), stream=s, mode="atoms")
+    torch.cuda.synchronize()
+    rids, roff, rst, _ = oracle.OracleVocab(v).encode_csr(text, offs, mode=oracle.ATOMS, cut_mask=cut)
+    p, c = pids.cpu().numpy(), cnt.cpu().numpy()
+    assert np.array_equal(pst.cpu().numpy(), rst)
+    assert np.array_equal(c.astype(np.uint64), np.diff(np.asarray(roff, dtype=np.uint64)))
+    for i in range(n):
+        a, b = int(offs[i]), int(roff[i])
+        assert np.array_equal(p[a:a + int(c[i])], rids[b:b + int(c[i])]), i
