@@ -20,6 +20,7 @@ struct dpt_vocab {
     int32_t *d_ids = nullptr;
     int4 *d_slots4 = nullptr;         // {base | TERM, check, id, 0} for the lane kernel
     int32_t root_base = 0;
+    int32_t ws_node = -1, ws_base = 0, ws_id = -1;   // the trie node after U+2581 (-1: no such path)
     bool ids16 = false;               // every id in 0..32767: ids are staged as int16 (half the staging traffic)
     dpt_vocab_stats stats{};
 };
@@ -39,6 +40,7 @@ struct dpt_ctx {
     uint32_t *retry_count = nullptr;  // counter block (dpt::CTR_ALLOC_BYTES): 8 uint32 counters, the uint64 arena
                                       // counter at byte 32, ..., the first pass's partition counters at byte 256
     uint8_t *wsl_scratch = nullptr;   // word lists of the 256-byte pass (dpt::wsl_scratch_bytes)
+    uint4 *pend = nullptr;            // pending residual tokens of the 256-byte pass (dpt::pend_scratch_bytes)
     unsigned long long *flags = nullptr;   // finish kernel's look-back flags (one per 64 strings)
     uint64_t cap_flags = 0;
     unsigned epoch = 0;               // call counter for the flags (1..65535; the array is cleared on wrap)
@@ -148,6 +150,10 @@ int ensure_workspace(dpt_ctx *c, const dpt_vocab *v, uint64_t n_bytes, uint64_t 
         e = hipMalloc((void **)&c->wsl_scratch, dpt::wsl_scratch_bytes(c->max_blocks));
         if (e != hipSuccess) return hip_fail(e, "hipMalloc(wsl_scratch)");
     }
+    if (!c->pend) {
+        e = hipMalloc((void **)&c->pend, dpt::pend_scratch_bytes(c->max_blocks));
+        if (e != hipSuccess) return hip_fail(e, "hipMalloc(pend)");
+    }
     if (!c->retry_count) {
         // zeroed once here; every call's finish kernel resets it for the next call
         e = hipMalloc((void **)&c->retry_count, dpt::CTR_ALLOC_BYTES);
@@ -203,9 +209,9 @@ int dpt_vocab_create(const uint8_t *utf8_blob, const uint64_t *tok_off, const in
     // none) | 1 << 30 if b0 is a root child | 1 << 31 if b0 alone is a token.  Phase A's first
     // lookup of every walk consumes two bytes through it.
     // slots4: {base, check, id, child filter} per slot, then the root table again as
-    // {.x, .y, 0, child filter of the node reached} -- phase A of tokenize_kernel reads only these
+    // {.x, .y, id of the node reached (-1 if none), child filter of the node reached} -- phase A of tokenize_kernel reads only these
     // (a filter bit per possible next byte, dpt::child_bit: a walk whose next byte has no bit ends
-    // without the failing lookup)
+    // without the failing lookup), and its id serves C2's one-lookup tokens of two bytes
     std::vector<int2> slots((size_t)da.n_slots + 65536);
     std::vector<int4> slots4((size_t)da.n_slots + 65536);
     std::vector<uint32_t> filt(da.n_slots, 0u);
@@ -231,7 +237,8 @@ int dpt_vocab_create(const uint8_t *utf8_blob, const uint64_t *tok_off, const in
             const bool e2 = e1 && !leaf1 && s2 < da.n_slots && da.check[s2] == (int32_t)s1;
             const uint32_t y = (e2 ? s2 : 0u) | (e1 ? 0x40000000u : 0u) | (term1 ? 0x80000000u : 0u);
             slots[(size_t)da.n_slots + (b0 << 8) + b1] = make_int2(e2 ? da.base[s2] : 0, (int32_t)y);
-            slots4[(size_t)da.n_slots + (b0 << 8) + b1] = make_int4(e2 ? da.base[s2] : 0, (int32_t)y, 0, e2 ? (int32_t)filt[s2] : 0);
+            slots4[(size_t)da.n_slots + (b0 << 8) + b1] = make_int4(e2 ? da.base[s2] : 0, (int32_t)y, e2 ? da.id[s2] : -1,
+                                                                    e2 ? (int32_t)filt[s2] : 0);
         }
     }
     e = hipMalloc((void **)&v->d_slots, sizeof(int2) * slots.size());
@@ -249,6 +256,17 @@ int dpt_vocab_create(const uint8_t *utf8_blob, const uint64_t *tok_off, const in
         return hip_fail(e, "vocab upload");
     }
     v->root_base = da.root_base;
+    {   // the node after '\u2581' (E2 96 81): the pending-token walks start word-start tokens there
+        int32_t node = 0;
+        for (uint32_t c : {0xE2u, 0x96u, 0x81u}) {
+            const uint32_t t = (uint32_t)(da.base[node] & 0x3FFFFFFF) + c;
+            if (node < 0 || t >= da.n_slots || da.check[t] != node) { node = -1; break; }
+            node = (int32_t)t;
+        }
+        v->ws_node = node;
+        v->ws_base = node >= 0 ? (da.base[node] & 0x3FFFFFFF) : 0;
+        v->ws_id = node >= 0 ? da.id[node] : -1;
+    }
     v->ids16 = true;
     for (uint32_t t = 0; t < da.n_slots; t++)
         if (da.check[t] >= 0 && (da.base[t] & (int32_t)0x80000000) && (da.id[t] < 0 || da.id[t] > 32767)) { v->ids16 = false; break; }
@@ -299,7 +317,7 @@ int dpt_ctx_destroy(dpt_ctx *c) {
     if (!c) return DPT_OK;
     DeviceGuard g(c->device);
     void *ps[] = {c->staging32, c->staging16, c->arena, c->counts, c->retry_list, c->retry_count, c->wsl_scratch,
-                  c->flags, c->d_in, c->d_out};
+                  c->pend, c->flags, c->d_in, c->d_out};
     for (void *p : ps)
         if (p) (void)hipFree(p);
     if (c->p_in) (void)hipHostFree(c->p_in);
@@ -325,6 +343,7 @@ int dpt_ctx_workspace_bytes(const dpt_ctx *c, uint64_t *device_path, uint64_t *h
     if (device_path)
         *device_path = c->cap16 * 2 + c->cap32 * 4 + c->arena_cap * ARENA_PER_BYTE + c->cap_str * (8 + 2 * 4) +
                        c->cap_flags * 8 + (c->wsl_scratch ? dpt::wsl_scratch_bytes(c->max_blocks) : 0) +
+                       (c->pend ? dpt::pend_scratch_bytes(c->max_blocks) : 0) +
                        (c->retry_count ? dpt::CTR_ALLOC_BYTES : 0);
     if (host_path) *host_path = c->cap_in + c->cap_out;
     return DPT_OK;
@@ -394,6 +413,7 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
     // int16 staging when every id fits in 0..32767 (half the staging traffic)
     p.staging16 = v->ids16 ? c->staging16 : nullptr;
     p.padded = padded;
+    p.pend = c->pend;
     if (padded) {   // the ids go straight to their final place (int32), the counts to the caller's array
         p.staging = ids;
         p.staging16 = nullptr;
@@ -404,6 +424,7 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
     p.n_slots = v->stats.n_slots;
     p.slots4 = v->d_slots4;
     p.root_base = v->root_base;
+    p.ws_node = v->ws_node; p.ws_base = v->ws_base; p.ws_id = v->ws_id;
     hipEvent_t ev[2];
     hipEvent_t *evp = nullptr;
     if (c->profile) {

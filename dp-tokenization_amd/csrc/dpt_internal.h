@@ -35,6 +35,7 @@ struct EncodeLaunch {
     unsigned max_blocks;
     int variant;             // KERNEL_* below
     bool padded;             // dpt_encode_padded: staging = the caller's ids, counts = the caller's; no finish pass
+    uint4 *pend;             // 16-lane first pass: each wave's pending residual tokens (pend_scratch_bytes)
     uint8_t *arena;          // the unbounded pass's scratch: 20 bytes per input byte of the strings it takes
     uint64_t arena_cap;      // input bytes the arena holds
     // vocabulary
@@ -43,6 +44,7 @@ struct EncodeLaunch {
     const int4 *slots4;      // {base | TERM<<31 | LEAF<<30, check, id, child filter}
     uint32_t n_slots;
     int32_t root_base;
+    int32_t ws_node, ws_base, ws_id;   // the trie node after U+2581, its base word and id (-1: none)
 };
 
 // first-pass work partitions (dpt_kernels.hip tokenize_kernel): up to NPART_MAX counters, one per
@@ -94,6 +96,7 @@ void launch_long(const LongLaunch &p, hipStream_t stream);
 
 hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t ev[2]);
 size_t wsl_scratch_bytes(unsigned max_blocks);
+size_t pend_scratch_bytes(unsigned max_blocks);
 hipError_t launch_histogram(const uint64_t *id_off, const int32_t *status, uint64_t n_str, int64_t *hist,
                             uint32_t n_bins, hipStream_t stream);
 hipError_t kernel_init();

@@ -29,8 +29,11 @@
 //          longest token so far is below G[n], de once it is reached -- the reference's first
 //          argmax in DFS order (dp_tokenize.py:58 pops the largest j first; :84 takes the first
 //          max).  Lane mode walks its chunks, row mode one word per lane.
-//   C2     id resolution: lanes re-walk each selected span through the trie and write
-//          t2i[token] (tokenizer_utils.py:76-79) to the slot's staging row.
+//   C2     id resolution, t2i[token] (tokenizer_utils.py:76-79) into the slot's staging row.  16-lane
+//          first pass: a bulk pass takes every selected token of one or two expanded bytes with ONE
+//          lookup (root child / two-byte root table) and lists the rest; a short list (< 64) waits
+//          in the wave's pending row and is walked 64 at a time from its stored bytes, a long one
+//          by the refill walker.  Other passes: the refill walker re-walks every selected span.
 //
 // Strings are claimed from 16 partition counters (see tokenize_kernel).  Strings whose single word
 // exceeds CH bytes are re-run by the 2048-byte, one-string-per-wave instantiation, longer ones by
@@ -289,6 +292,8 @@ struct EncodeArgs {
     uint32_t *work_next;        // 2048-byte pass: its work counter (zeroed per launch)
     uint32_t *part_ctr;         // first pass: NPART partition counters (PART_STRIDE apart), then the used-up mask
     uint8_t *wsl_scratch;       // word lists of the 256-byte pass: grid x NG x WSL_STRIDE bytes
+    uint4 *pend;                // 16-lane first pass: per wave, 64 pending residual tokens (walk_pending)
+    int32_t ws_node, ws_base, ws_id;   // the trie node after U+2581, its base word and id (-1: none)
     int long_span;              // the vocabulary has tokens longer than 64 code points
     uint64_t *edges;            // nullable: per atom end, the E(i) & reachable back-distance mask
     int mode;                   // DPT_MODE_* | DPT_FLAG_*
@@ -600,6 +605,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
     const unsigned npart = BIG ? 1u : (unsigned)min((uint64_t)NPART, max((uint64_t)1, n_work / 4096u));
     unsigned part = BIG ? 0u : blockIdx.x % npart;
     bool exhausted = false, claimed_all = false;
+    unsigned n_pend = 0;   // 16-lane first pass: residual tokens waiting in the wave's pending row
     // one claim of up to req strings (uniform): [nb, ne), possibly empty once every partition is used up
     auto claim = [&](unsigned req, uint64_t &nb, uint64_t &ne) {
         for (;;) {
@@ -627,6 +633,52 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 }
             }
             if (ne > nb || claimed_all) return;
+        }
+    };
+    // The wave's pending residual tokens (16-lane first pass, C2): one walk per lane from the entry's
+    // bytes -- the C2 walker's byte rule (atom_from_info: raw mode expands the string's first atom to
+    // '\u2581' + its bytes, ' ' to '\u2581', '\n' to "<0x0A>") as a byte generator, so one trie step
+    // per expanded byte from one call site -- starting at the node after '\u2581' when the token
+    // starts with it; the id of the node reached when every step's check held, else -1.  Entry:
+    // staging element (.x, .y bits 0..15), byte length (.y bits 16..23, <= 8), first atom of the
+    // string (.y bit 24), the bytes (.z, .w).
+    auto walk_pending = [&](unsigned P) {
+        wave_sync();   // the entries other lanes stored
+        if (lane < P) {
+            const uint4 e = a.pend[(uint64_t)blockIdx.x * 64u + lane];
+            const uint64_t out = (uint64_t)e.x | ((uint64_t)(e.y & 0xFFFFu) << 32);
+            const unsigned len = (e.y >> 16) & 0xFFu;
+            const bool fi = raw && ((e.y >> 24) & 1u);
+            const uint64_t by = (uint64_t)e.z | ((uint64_t)e.w << 32);
+            const unsigned b0 = (unsigned)(by & 0xFFu);
+            const bool ws = (fi || (raw && b0 == ' ')) && a.ws_node >= 0;
+            int32_t node = ws ? a.ws_node : 0, nb = ws ? a.ws_base : tv.root_base, id = ws ? a.ws_id : -1;
+            bool ok = true;
+            unsigned k = (ws && !fi) ? 1u : 0u;   // ws: '\u2581' is consumed (a first atom still emits its bytes)
+            uint64_t pnd = 0;
+            unsigned pc = 0;
+            while (k < len || pc) {
+                if (!pc) {
+                    const unsigned b = (unsigned)(by >> (8u * k)) & 0xFFu;
+                    const bool first = k == 0 && fi;
+                    pnd = b; pc = 1;
+                    if (first && !ws) { pnd = 0x8196E2ull | ((uint64_t)b << 24); pc = 4; }
+                    else if (!first && raw && b == ' ') { pnd = 0x8196E2ull; pc = 3; }
+                    else if (!first && raw && b == '\n') { pnd = 0x3E413078303Cull; pc = 6; }
+                    k++;
+                }
+                const int32_t sl = nb + (int32_t)(pnd & 0xFFu);
+                pnd >>= 8;
+                pc--;
+                const int4 en = trie_slot4(tv, sl);
+                ok = ok && en.y == node;
+                node = sl;
+                nb = en.x & BASE_MASK;
+                id = en.z;
+            }
+            id = ok ? id : -1;
+            if (SW == 1 || (SW == 0 && a.staging16 != nullptr)) a.staging16[out] = (int16_t)id;
+            else a.staging[out] = id;
         }
     };
     STAMP_DECL
@@ -1512,6 +1564,110 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 }
             }
             wave_sync();
+            // 16-lane first pass: a bulk pass resolves every token of one or two expanded bytes with
+            // ONE lookup (a one-byte token's root child, a two-byte token's root-table entry: .z = the
+            // id of the node reached) and lists the rest -- word starts ('\u2581'), newlines, tokens of
+            // three or more bytes -- by their token number in the rec[].cpos halves (dead in C2:
+            // entry i in group i / 256's rec[i % 256]).  A short list (< 64 tokens of <= 8 bytes: the
+            // walker would run with idle lanes) joins the wave's pending row, which is walked from
+            // the stored bytes once a round would overflow it (walk_pending); a longer one is walked
+            // below by the refill walker.
+            constexpr bool BULK = G == 16 && !BIG;
+            unsigned wbeg = 0, wend = total;
+            auto list_ref = [&](unsigned i) -> uint16_t & {
+                return *reinterpret_cast<uint16_t *>(smem + (i >> 8) * (unsigned)group_lds_bytes<CH, G>() + (i & 255u) * 4u);
+            };
+            if constexpr (BULK) {
+                const bool i16 = n16;
+                unsigned r = 0;
+                for (unsigned t0 = 0; t0 < total; t0 += 64u * 4u) {
+                    int32_t ix[4];
+                    unsigned kind[4];   // 0: not here, 1 / 2: a token of that many bytes
+                    uint64_t oq[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const unsigned t = t0 + 64u * (unsigned)u + lane;
+                        const bool in = t < total;
+                        unsigned g = 0;
+#pragma unroll
+                        for (int k = 1; k < NG; k++) g += t >= pre[k] ? 1u : 0u;
+                        const GL &L = *reinterpret_cast<const GL *>(smem + g * (unsigned)group_lds_bytes<CH, G>());
+                        const C2Slot q = *reinterpret_cast<const C2Slot *>(&L.fin[0]);
+                        const unsigned k = in ? t - q.base : 0u;
+                        const unsigned jj = (unsigned)L.rec[k].smask;
+                        const unsigned nx = (unsigned)L.rec[k + 1].smask;   // k + 1 <= ntk < NA
+                        const unsigned j1 = k + 1 < q.ntk ? nx : q.na;
+                        const unsigned p0 = L.aoff[jj];
+                        const unsigned nbytes = (uint8_t)(L.aoff[j1] - p0);
+                        const uint32_t *w = reinterpret_cast<const uint32_t *>(L.bytes) + (p0 >> 2);
+                        const unsigned two = __builtin_amdgcn_alignbyte(w[1], w[0], p0 & 3u);
+                        const unsigned b0 = two & 0xFFu, b1 = (two >> 8) & 0xFFu;
+                        // raw mode expands ' ' (a word start), '\n' and the string's first atom
+                        const unsigned expd = (raw ? 1u : 0u) &
+                                              ((unsigned)(b0 == ' ') | (unsigned)(b0 == '\n') | (q.fw & (unsigned)(jj == 0)) |
+                                               ((unsigned)(nbytes == 2u) & ((unsigned)(b1 == ' ') | (unsigned)(b1 == '\n'))));
+                        const unsigned bulk = (unsigned)in & (unsigned)(nbytes - 1u <= 1u) & (expd ^ 1u);
+                        ix[u] = bulk ? (nbytes == 1u ? tv.root_base + (int32_t)b0 : (int32_t)(tv.n_slots + (b0 << 8) + b1)) : 0;
+                        kind[u] = bulk ? nbytes : 0u;
+                        oq[u] = q.ob + k;
+                        const bool res = in && !bulk;
+                        const uint64_t m = ballot(res);
+                        if (res) list_ref(r + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u))) = (uint16_t)t;
+                        r += (unsigned)__builtin_popcountll(m);
+                    }
+                    int4 ent[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) ent[u] = trie_slotA(tv, ix[u]);
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        if (kind[u]) {
+                            // the walker's rule: the id of the node reached when every step's check held
+                            const bool ok = kind[u] == 1u ? ent[u].y == 0 : (ent[u].y & 0x3FFFFFFF) != 0;
+                            const int32_t idv = ok ? ent[u].z : -1;
+                            if (i16) a.staging16[oq[u]] = (int16_t)idv;
+                            else a.staging[oq[u]] = idv;
+                        }
+                    }
+                }
+                wave_sync();
+                wend = r;
+                if (r > 0 && r < 64u) {
+                    uint4 ent = make_uint4(0u, 0u, 0u, 0u);
+                    bool lng = false;
+                    if (lane < r) {
+                        const unsigned t = list_ref(lane);
+                        unsigned g = 0;
+#pragma unroll
+                        for (int k = 1; k < NG; k++) g += t >= pre[k] ? 1u : 0u;
+                        const GL &L = *reinterpret_cast<const GL *>(smem + g * (unsigned)group_lds_bytes<CH, G>());
+                        const C2Slot q = *reinterpret_cast<const C2Slot *>(&L.fin[0]);
+                        const unsigned k = t - q.base;
+                        const unsigned jj = (unsigned)L.rec[k].smask;
+                        const unsigned nx = (unsigned)L.rec[k + 1].smask;
+                        const unsigned j1 = k + 1 < q.ntk ? nx : q.na;
+                        const unsigned p0 = L.aoff[jj];
+                        const unsigned len = (uint8_t)(L.aoff[j1] - p0);
+                        const unsigned fi = (raw ? 1u : 0u) & q.fw & (unsigned)(jj == 0);
+                        lng = len > 8u;
+                        const uint64_t by = load_bytes(L.bytes, p0, lng ? 8u : len);
+                        const uint64_t out = q.ob + k;
+                        ent = make_uint4((uint32_t)out, ((uint32_t)(out >> 32) & 0xFFFFu) | (len << 16) | (fi << 24), (uint32_t)by, (uint32_t)(by >> 32));
+                    }
+                    if (!ballot(lng)) {
+                        if (n_pend + r > 64u) {
+                            walk_pending(n_pend);
+                            n_pend = 0;
+                        }
+                        if (lane < r) a.pend[(uint64_t)blockIdx.x * 64u + n_pend + lane] = ent;
+                        n_pend += r;
+                        wend = 0;
+                    }
+                }
+            }
+            auto tok_at = [&](unsigned i) -> unsigned {
+                if constexpr (BULK) return list_ref(i);
+                else return i;
+            };
             // One token walk per lane; a lane whose token is resolved writes the id and takes the
             // next token (ballot + mbcnt), so each iteration is one trie step for 64 tokens.  A
             // token's bytes do not depend on the trie, so each iteration issues the trie load
@@ -1550,12 +1706,12 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
             bool ok[NW];
 #pragma unroll
             for (int w = 0; w < NW; w++) {
-                active[w] = lane + 64u * w < total;
+                active[w] = wbeg + lane + 64u * w < wend;
                 C[w].jj = C[w].j1 = C[w].cnt = C[w].lbase = 0; C[w].seq = 0; C[w].out = 0;
-                if (active[w]) C[w] = tstart(lane + 64u * w);
+                if (active[w]) C[w] = tstart(tok_at(wbeg + lane + 64u * w));
                 node[w] = 0; nb[w] = tv.root_base; ok[w] = true;
             }
-            unsigned nxt = 64u * NW;
+            unsigned nxt = wbeg + 64u * NW;
             for (;;) {
                 bool any = false;
 #pragma unroll
@@ -1595,8 +1751,8 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                         if (n16) a.staging16[C[w].out] = (int16_t)idv;
                         else a.staging[C[w].out] = idv;
                         const unsigned uu = nxt + __builtin_amdgcn_mbcnt_hi((unsigned)(dm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)dm, 0u));
-                        active[w] = uu < total;
-                        if (active[w]) C[w] = tstart(uu);
+                        active[w] = uu < wend;
+                        if (active[w]) C[w] = tstart(tok_at(uu));
                         node[w] = 0; nb[w] = tv.root_base; ok[w] = true;
                     }
                     nxt += (unsigned)__builtin_popcountll(dm);
@@ -1635,6 +1791,8 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
         STAMP(4);
         PRIO_PHASE(4);
     }
+    if constexpr (G == 16 && !BIG)
+        if (n_pend) walk_pending(n_pend);
     STAMP_FLUSH;
 }
 
@@ -1925,6 +2083,7 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     a.work_next = p.retry_count + 1;
     a.part_ctr = p.retry_count + PART_CTR_OFFSET / 4;
     a.wsl_scratch = p.wsl_scratch;
+    a.pend = p.pend; a.ws_node = p.ws_node; a.ws_base = p.ws_base; a.ws_id = p.ws_id;
     a.long_span = p.long_span;
     TrieView tv{p.slots, p.slot_ids, p.slots4, p.root_base, p.n_slots};
     const bool wide = (p.mode & DPT_MODE_MASK) == DPT_MODE_ATOMS;   // atoms of up to 8 bytes
@@ -2000,6 +2159,8 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     else hipLaunchKernelGGL(finish_kernel<int32_t>, dim3((unsigned)fb), dim3(FIN_THREADS), 0, stream, f);
     return hipGetLastError();
 }
+
+size_t pend_scratch_bytes(unsigned max_blocks) { return (size_t)max_blocks * 64 * sizeof(uint4); }
 
 size_t wsl_scratch_bytes(unsigned max_blocks) {
     return (size_t)max_blocks * 4 * GroupLDS<SMALL_CH, 16>::WSL_STRIDE;   // NG x stride covers both G at CH = 256
