@@ -1573,6 +1573,10 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
             // the stored bytes once a round would overflow it (walk_pending); a longer one is walked
             // below by the refill walker.
             constexpr bool BULK = G == 16 && !BIG;
+#ifndef PEND_CAP
+#define PEND_CAP 64   // residual tokens a wave's pending row holds (A/B knob; the scratch row has 64 entries)
+#endif
+            static_assert(PEND_CAP >= 1 && PEND_CAP <= 64, "pending row");
             unsigned wbeg = 0, wend = total;
             auto list_ref = [&](unsigned i) -> uint16_t & {
                 return *reinterpret_cast<uint16_t *>(smem + (i >> 8) * (unsigned)group_lds_bytes<CH, G>() + (i & 255u) * 4u);
@@ -1631,7 +1635,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                 }
                 wave_sync();
                 wend = r;
-                if (r > 0 && r < 64u) {
+                if (r > 0 && r < (unsigned)PEND_CAP) {
                     uint4 ent = make_uint4(0u, 0u, 0u, 0u);
                     bool lng = false;
                     if (lane < r) {
@@ -1654,7 +1658,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                         ent = make_uint4((uint32_t)out, ((uint32_t)(out >> 32) & 0xFFFFu) | (len << 16) | (fi << 24), (uint32_t)by, (uint32_t)(by >> 32));
                     }
                     if (!ballot(lng)) {
-                        if (n_pend + r > 64u) {
+                        if (n_pend + r > (unsigned)PEND_CAP) {
                             walk_pending(n_pend);
                             n_pend = 0;
                         }
