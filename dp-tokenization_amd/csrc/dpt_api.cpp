@@ -41,9 +41,8 @@ struct dpt_ctx {
                                       // counter at byte 32, ..., the first pass's partition counters at byte 256
     uint8_t *wsl_scratch = nullptr;   // word lists of the 256-byte pass (dpt::wsl_scratch_bytes)
     uint4 *pend = nullptr;            // pending residual tokens of the 256-byte pass (dpt::pend_scratch_bytes)
-    unsigned long long *flags = nullptr;   // finish kernel's look-back flags (one per 64 strings)
+    unsigned long long *flags = nullptr;   // batch sums, then (from cap_flags / 2) batch prefixes: one each per 256 strings
     uint64_t cap_flags = 0;
-    unsigned epoch = 0;               // call counter for the flags (1..65535; the array is cleared on wrap)
     unsigned max_blocks = 0;
     // host path: one device buffer in (text | offsets | cut) and one out (id_off | status | capped |
     // counters | ids | edges), each mirrored by a pinned host buffer so every copy is one async DMA
@@ -141,10 +140,12 @@ int ensure_workspace(dpt_ctx *c, const dpt_vocab *v, uint64_t n_bytes, uint64_t 
         cap2 /= 2;
         c->cap_str = cap < cap2 ? cap : cap2;
     }
-    if ((n_str + 63) / 64 > c->cap_flags || !c->flags) {
-        if ((e = grow(&c->flags, &c->cap_flags, (n_str + 63) / 64)) != hipSuccess) return hip_fail(e, "hipMalloc(flags)");
+    if (2 * ((n_str + dpt::FIN_BATCH - 1) / dpt::FIN_BATCH) > c->cap_flags || !c->flags) {
+        // two arrays of one entry per batch (sums | prefixes at cap_flags / 2), at one per 64 strings
+        const uint64_t want = 2 * ((n_str + 63) / 64 > 1 ? (n_str + 63) / 64 : 1);
+        if ((e = grow(&c->flags, &c->cap_flags, want)) != hipSuccess) return hip_fail(e, "hipMalloc(flags)");
+        // the batch sums start at zero; every call's batch_scan_kernel zeroes them again
         if ((e = hipMemset(c->flags, 0, c->cap_flags * sizeof(unsigned long long))) != hipSuccess) return hip_fail(e, "hipMemset(flags)");
-        c->epoch = 0;
     }
     if (!c->wsl_scratch) {
         e = hipMalloc((void **)&c->wsl_scratch, dpt::wsl_scratch_bytes(c->max_blocks));
@@ -400,12 +401,7 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
     p.long_span = v->stats.max_cp > 64 ? 1 : 0;
     p.max_tok_bytes = v->stats.max_bytes;
     p.flags = c->flags;
-    if (++c->epoch > 0xFFFFu) {   // the flags' epoch wraps: clear them so no stale flag can match
-        hipError_t e0 = hipMemsetAsync(c->flags, 0, c->cap_flags * sizeof(unsigned long long), (hipStream_t)hip_stream);
-        if (e0 != hipSuccess) return hip_fail(e0, "hipMemsetAsync(flags)");
-        c->epoch = 1;
-    }
-    p.epoch = c->epoch;
+    p.bpre = c->flags + c->cap_flags / 2;
     p.max_blocks = c->max_blocks;
     p.arena = c->arena;
     p.arena_cap = c->arena_cap;
@@ -438,7 +434,8 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
     }
     hipError_t e = dpt::launch_encode(p, st, evp);
     if (e != hipSuccess) {
-        (void)hipMemsetAsync(c->retry_count, 0, dpt::CTR_ALLOC_BYTES, st);   // the finish kernel did not reset them
+        (void)hipMemsetAsync(c->retry_count, 0, dpt::CTR_ALLOC_BYTES, st);   // the scan kernel did not reset them
+        (void)hipMemsetAsync(c->flags, 0, c->cap_flags * sizeof(unsigned long long), st);   // nor zero the batch sums
         return hip_fail(e, "encode launch");
     }
     return DPT_OK;

@@ -30,8 +30,9 @@ struct EncodeLaunch {
     uint8_t *wsl_scratch;    // max_blocks x wsl_scratch_bytes(1) bytes
     int long_span;           // vocabulary tokens longer than 64 code points: words over 64 atoms -> unbounded pass
     uint32_t max_tok_bytes;  // longest vocabulary token, bytes
-    unsigned long long *flags;   // finish kernel's look-back flags (sized one per 64 strings; one per FIN_BATCH used)
-    unsigned epoch;              // the ctx's call counter (1..65535)
+    unsigned long long *flags;   // per FIN_BATCH-string batch: the sum of its counts, added by the tokenize passes as
+                                 //   strings finish; batch_scan_kernel zeroes it for the next call
+    unsigned long long *bpre;    // per batch: its exclusive id prefix (batch_scan_kernel)
     unsigned max_blocks;
     int variant;             // KERNEL_* below
     bool padded;             // dpt_encode_padded: staging = the caller's ids, counts = the caller's; no finish pass
@@ -51,6 +52,8 @@ struct EncodeLaunch {
 // PART_STRIDE uint32 (a 256-byte line each), from byte PART_CTR_OFFSET of the counter block, then the
 // used-up mask; the counter block is CTR_ALLOC_BYTES long (the host path copies its first 64 bytes)
 constexpr unsigned NPART_MAX = 32;
+// strings per finish batch (the batch arrays are sized one per 64 strings, two arrays)
+constexpr unsigned FIN_BATCH = 256;
 constexpr unsigned PART_STRIDE = 64;
 constexpr size_t PART_CTR_OFFSET = 256;
 constexpr size_t CTR_ALLOC_BYTES = PART_CTR_OFFSET + (NPART_MAX + 1) * PART_STRIDE * 4;
@@ -81,6 +84,7 @@ struct LongLaunch {
     uint64_t *far;                    // as EncodeLaunch
     uint64_t far_cap;
     unsigned long long *far_count;    // pairs found (all of them; > far_cap: the host grows and reruns)
+    unsigned long long *bsum;         // nullable: per FIN_BATCH strings, the sum of their counts (EncodeLaunch::flags)
     const uint32_t *list;
     const uint32_t *list_count;
     uint32_t *work_next;

@@ -281,6 +281,7 @@ struct EncodeArgs {
     int32_t *staging;           // ids staged at (str_off[s]-str_off[0]) + k
     int16_t *staging16;         // non-null: the ids are staged here as int16 instead (half the bytes)
     uint64_t *counts;           // per string
+    unsigned long long *bsum;   // nullable: per FIN_BATCH strings, the sum of their counts (atomics as strings finish)
     int32_t *status;
     int32_t *capped;            // nullable
     uint32_t *retry_list;       // strings for the 2048-byte pass
@@ -1786,6 +1787,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                     const uint64_t s = S.s;
                     a.status[s] = (int32_t)S.status;
                     a.counts[s] = S.status == 0 ? (uint64_t)S.ntok : 0ull;
+                    if (a.bsum && S.status == 0 && S.ntok) atomicAdd(&a.bsum[s / FIN_BATCH], (unsigned long long)S.ntok);
                     if (a.capped) a.capped[s] = S.status == 3 ? -1 : (int32_t)S.capsum;
                     S.active = 0;
                 }
@@ -1805,31 +1807,25 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
 // ------------------------------------------------------------------ finish: offsets + CSR ids in one pass
 
 // Counter block (EncodeLaunch::retry_count, CTR_ALLOC_BYTES; zeroed once at allocation, then reset for
-// the next call by the finish kernel's last block): uint32 [0] retry count, [1] unused, [2]
-// 2048-byte pass work, [3] long count, [4] long work, [5] finish ticket, [6] finish blocks done;
-// uint64 [4] (byte 32) the unbounded pass's claimed bytes, [5] (byte 40) the last call's claimed
-// bytes (dpt_ctx_long_need), [6] (byte 48) far edge pairs found, [7] (byte 56) the last call's
-// far edge pairs (dpt_dp_host_far); from byte PART_CTR_OFFSET the first pass's partition counters
-// and their used-up mask (dpt_internal.h).
-constexpr unsigned CTR_TICKET = 5, CTR_DONE = 6;
+// the next call by batch_scan_kernel, which runs after every tokenize pass): uint32 [0] retry count,
+// [1] unused, [2] 2048-byte pass work, [3] long count, [4] long work, [5], [6] unused; uint64 [4] (byte
+// 32) the unbounded pass's claimed bytes, [5] (byte 40) the last call's claimed bytes
+// (dpt_ctx_long_need), [6] (byte 48) far edge pairs found, [7] (byte 56) the last call's far edge pairs
+// (dpt_dp_host_far); from byte PART_CTR_OFFSET the first pass's partition counters and their used-up
+// mask (dpt_internal.h).
 constexpr unsigned CTR_ARENA64 = 4, CTR_LASTNEED64 = 5, CTR_FAR64 = 6, CTR_LASTFAR64 = 7;
 #ifndef FIN_THREADS
 #define FIN_THREADS 512   // threads per finish block (>= FIN_BATCH): all of them copy
 #endif
-#ifndef FIN_BATCH
-#define FIN_BATCH 256   // strings per finish batch = threads per finish block (>= 64: the flags are sized per 64 strings)
+#ifndef SCAN_THREADS
+#define SCAN_THREADS 1024   // threads of the batch-scan block
 #endif
-
-// Look-back flags, one uint64 per FIN_BATCH-string batch: epoch (16 bits, the ctx's call counter; 0
-// never used, the host clears the array when it wraps) | state (2 bits: 1 = batch aggregate, 2 =
-// inclusive prefix) | value (46 bits of ids).
-__device__ __forceinline__ uint64_t flag_pack(unsigned epoch, unsigned st, uint64_t v) {
-    return ((uint64_t)epoch << 48) | ((uint64_t)st << 46) | v;
-}
-
-__device__ __forceinline__ uint64_t readlane64(uint64_t v, unsigned l) {
-    return uni64(((uint64_t)__builtin_amdgcn_readlane((unsigned)(v >> 32), l) << 32) | __builtin_amdgcn_readlane((unsigned)v, l));
-}
+#ifndef FIN_TARGET_BLOCKS
+#define FIN_TARGET_BLOCKS 2048   // small batches: each batch's copy is split over slices until the grid has this many blocks
+#endif
+#ifndef FIN_MAX_SLICES
+#define FIN_MAX_SLICES 8
+#endif
 
 // 64-bit inclusive add-scan over the wave (ds_bpermute shifts)
 __device__ __forceinline__ uint64_t wave_incl_scan_add64(uint64_t v, unsigned lane) {
@@ -1843,57 +1839,26 @@ __device__ __forceinline__ uint64_t wave_incl_scan_add64(uint64_t v, unsigned la
     return v;
 }
 
-struct FinishArgs {
-    const void *staging;          // int16_t or int32_t (ST)
-    const uint64_t *str_off;
-    const uint64_t *counts;
-    uint64_t n_str;
-    uint64_t *id_off;
-    int32_t *ids;
-    unsigned long long *flags;
-    uint32_t *ctr;
-    unsigned epoch;
-};
-
-// Exclusive id offset of batch t (t > 0) by decoupled look-back, one wave: lane l reads batch
-// jb - l's flag; once every batch from jb down to the nearest inclusive prefix in the window has
-// published, their values are summed (no prefix in the window: all 64 aggregates, then the next
-// window).  Batches before t hold tickets taken before t's, by blocks already running, so every
-// flag it waits for is published without t's help.
-__device__ __forceinline__ uint64_t finish_lookback(const FinishArgs &f, uint64_t t, unsigned lane) {
-    uint64_t excl = 0, jb = t - 1;
-    for (unsigned spin = 0;;) {
-        const bool in = lane <= jb;
-        const uint64_t fl = in ? __hip_atomic_load(&f.flags[jb - lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                               : flag_pack(f.epoch, 2, 0);
-        const unsigned st = (fl >> 48) == f.epoch ? (unsigned)(fl >> 46) & 3u : 0u;
-        const uint64_t pm = ballot(st == 2), ready = ballot(st != 0);
-        const unsigned p = pm ? (unsigned)__builtin_ctzll(pm) : 64u;   // nearest prefix in the window
-        const uint64_t need = p < 63 ? ((2ull << p) - 1) : ~0ull;      // lanes 0..p
-        if ((ready & need) != need) {                                  // not all published yet
-            __builtin_amdgcn_s_sleep(1);
-            if (++spin > (1u << 24)) return excl;   // never expected: bounded, so a broken protocol cannot hang the GPU
-            continue;
-        }
-        const uint64_t v = wave_incl_scan_add64((lane <= p && in) ? (fl & ((1ull << 46) - 1)) : 0ull, lane);
-        excl += readlane64(v, 63);
-        if (p < 64) return excl;
-        jb -= 64;
-        spin = 0;
+// inclusive add-scan over a block of NT threads; *total = the block's sum.  Uses s_w[NT / 64] and
+// ends with the block synchronised (s_w reusable after it).
+template <unsigned NT>
+__device__ __forceinline__ uint64_t block_incl_scan_add64(uint64_t v, uint64_t *s_w, uint64_t *total) {
+    const unsigned tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+    uint64_t incl = wave_incl_scan_add64(v, lane);
+    if (lane == 63) s_w[w] = incl;
+    __syncthreads();
+    uint64_t agg = 0;
+#pragma unroll
+    for (unsigned k = 0; k < NT / 64; k++) {
+        const uint64_t ws = s_w[k];
+        if (k < w) incl += ws;
+        agg += ws;
     }
+    *total = agg;
+    __syncthreads();
+    return incl;
 }
 
-// Offsets and CSR ids in one launch: a persistent grid (32 waves per CU) of FIN_THREADS-thread blocks
-// takes FIN_BATCH-string batches in ticket order.  Per batch: one count per thread of the first
-// FIN_BATCH, a block scan (wave scans + the wave sums in LDS); wave 0 publishes the batch aggregate,
-// finds the batch's first id by look-back and publishes the inclusive prefix; every string's end
-// offset is written; then ALL the block's threads copy the batch's staged ids -- threads over the
-// batch's OUTPUT ids, so every store is a coalesced row -- FIN_U independent loads in flight per
-// thread.  The last block out resets the counter block for the next call.  Replaces round 1's counter
-// reset, offset scan and compaction (three launches, two more passes over the counts).  512 threads
-// for 256-string batches: 0.345 vs 0.361 ms per 1M strings and 0.067 vs 0.092 ms per 125k than 256
-// (a quarter of the copy parallelism at small batches); smaller batches lengthen the look-back
-// chains (64-string batches: 1.85 ms per 1M) (profiles/r02_ab_issue_model.log).
 // Reset the counter block for the next call (the claimed arena bytes and far pairs stay readable as
 // the call's "last need" / "last far").
 __device__ __forceinline__ void reset_counters(uint32_t *ctr) {
@@ -1902,92 +1867,118 @@ __device__ __forceinline__ void reset_counters(uint32_t *ctr) {
     c64[CTR_ARENA64] = 0;
     c64[CTR_LASTFAR64] = c64[CTR_FAR64];
     c64[CTR_FAR64] = 0;
-    ctr[0] = 0; ctr[1] = 0; ctr[2] = 0; ctr[3] = 0; ctr[4] = 0;
+    ctr[0] = 0; ctr[1] = 0; ctr[2] = 0; ctr[3] = 0; ctr[4] = 0; ctr[5] = 0; ctr[6] = 0;
     uint32_t *pc = ctr + PART_CTR_OFFSET / 4;
     for (unsigned q = 0; q <= NPART; q++) pc[q * PART_STRIDE] = 0;   // the partition counters and the mask
-    ctr[CTR_TICKET] = 0;
-    ctr[CTR_DONE] = 0;
 }
 
+// Batch prefixes: the tokenize passes add every string's count to its FIN_BATCH-string batch's sum
+// as the string finishes (one no-return atomic per string, dpt_kernels.hip / dpt_long.hip); this ONE
+// block turns bsum[0..nb) into exclusive prefixes bpre[0..nb) (thread i over a contiguous chunk:
+// chunk sums, one block scan, the chunk again), zeroes bsum for the next call and resets the counter
+// block -- every tokenize pass has finished when it runs.  It replaces round 2's decoupled look-back
+// inside a persistent finish kernel, which chained the batches: a finish block could not start its
+// copy before its look-back, so each block took its batches one after another.
+__global__ void __launch_bounds__(SCAN_THREADS) batch_scan_kernel(uint64_t n_str, unsigned long long *bsum,
+                                                                  unsigned long long *bpre, uint32_t *ctr) {
+    __shared__ uint64_t s_w[SCAN_THREADS / 64];
+    const unsigned tid = threadIdx.x;
+    const uint64_t nb = (n_str + FIN_BATCH - 1) / FIN_BATCH;
+    const uint64_t per = (nb + SCAN_THREADS - 1) / SCAN_THREADS;
+    const uint64_t c0 = (uint64_t)tid * per < nb ? (uint64_t)tid * per : nb, c1 = c0 + per < nb ? c0 + per : nb;
+    uint64_t sum = 0;
+    for (uint64_t k = c0; k < c1; k++) sum += bsum[k];
+    uint64_t total;
+    uint64_t run = block_incl_scan_add64<SCAN_THREADS>(sum, s_w, &total) - sum;
+    for (uint64_t k = c0; k < c1; k++) {
+        const uint64_t b = bsum[k];
+        bpre[k] = run;
+        bsum[k] = 0;
+        run += b;
+    }
+    if (tid == 0) reset_counters(ctr);
+}
+
+struct FinishArgs {
+    const void *staging;          // int16_t or int32_t (ST)
+    const uint64_t *str_off;
+    const uint64_t *counts;
+    uint64_t n_str;
+    uint64_t *id_off;
+    int32_t *ids;
+    const unsigned long long *bpre;   // per batch: its first id (batch_scan_kernel)
+    unsigned slices;                  // blocks per batch
+};
+
+// CSR offsets and ids: block b takes slice b % slices of batch b / slices.  One count per thread of
+// the first FIN_BATCH, a block scan (the batch's relative offsets), the batch's first id from bpre;
+// slice 0 writes every string's end offset; then ALL the block's threads copy the slice's staged ids --
+// threads over the OUTPUT ids, so every store is a coalesced row -- FIN_U independent loads in flight
+// per thread.  At 1M strings a batch is one block (3 907 blocks); small calls split each batch's copy
+// so the grid still has ~FIN_TARGET_BLOCKS blocks (a block's copy is a chain of dependent load rounds:
+// 125k strings were 489 blocks of 7 rounds each).
 template <typename ST>
 __global__ void __launch_bounds__(FIN_THREADS) finish_kernel(FinishArgs f) {
     __shared__ uint64_t s_rel[FIN_BATCH + 1];   // ids of the batch's strings before string k, + the batch total
     __shared__ uint64_t s_src[FIN_BATCH];       // staging element of each string's first id
-    __shared__ uint64_t s_wsum[FIN_BATCH / 64];
-    __shared__ uint64_t s_base;                 // the batch's first id
-    __shared__ unsigned s_ticket;
-    const unsigned tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
-    const uint64_t n_batches = (f.n_str + FIN_BATCH - 1) / FIN_BATCH;
+    __shared__ uint64_t s_w[FIN_THREADS / 64];
+    const unsigned tid = threadIdx.x;
+    const uint64_t t = blockIdx.x / f.slices;
+    const unsigned sl = blockIdx.x % f.slices;
     const uint64_t base_off = f.str_off[0];
     const ST *__restrict__ staging = reinterpret_cast<const ST *>(f.staging);
-    for (;;) {
-        if (tid == 0) s_ticket = atomicAdd(&f.ctr[CTR_TICKET], 1u);
-        __syncthreads();
-        const uint64_t t = s_ticket;
-        if (t >= n_batches) break;
-        const uint64_t s0 = t * FIN_BATCH;
-        // the first FIN_BATCH threads hold one string each; every thread copies
-        const bool has = tid < FIN_BATCH && tid < f.n_str - s0;
-        const uint64_t c = has ? f.counts[s0 + tid] : 0ull;
-        const uint64_t src = has ? f.str_off[s0 + tid] - base_off : 0ull;
-        uint64_t incl = wave_incl_scan_add64(c, lane);
-        if (lane == 63 && w < FIN_BATCH / 64) s_wsum[w] = incl;
-        __syncthreads();
-        uint64_t agg = 0;
-#pragma unroll
-        for (unsigned k = 0; k < FIN_BATCH / 64; k++) {
-            const uint64_t ws = s_wsum[k];
-            if (k < w) incl += ws;
-            agg += ws;
-        }
-        if (w == 0) {
-            uint64_t excl = 0;
-            if (t == 0) {
-                if (lane == 0) __hip_atomic_store(&f.flags[0], flag_pack(f.epoch, 2, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            } else {
-                if (lane == 0) __hip_atomic_store(&f.flags[t], flag_pack(f.epoch, 1, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                excl = finish_lookback(f, t, lane);
-                if (lane == 0) __hip_atomic_store(&f.flags[t], flag_pack(f.epoch, 2, excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            if (lane == 0) s_base = excl;
-        }
-        if (tid < FIN_BATCH) {
-            s_rel[tid] = incl - c;
-            s_src[tid] = src;
-        }
-        if (tid == FIN_BATCH - 1) s_rel[FIN_BATCH] = incl;
-        __syncthreads();
-        const uint64_t o0 = s_base, total = agg;
+    const uint64_t s0 = t * FIN_BATCH;
+    const uint64_t o0 = f.bpre[t];
+    // the first FIN_BATCH threads hold one string each; every thread copies
+    const bool has = tid < FIN_BATCH && tid < f.n_str - s0;
+    const uint64_t c = has ? f.counts[s0 + tid] : 0ull;
+    const uint64_t src = has ? f.str_off[s0 + tid] - base_off : 0ull;
+    uint64_t total;
+    const uint64_t incl = block_incl_scan_add64<FIN_THREADS>(c, s_w, &total);
+    if (tid < FIN_BATCH) {
+        s_rel[tid] = incl - c;
+        s_src[tid] = src;
+    }
+    if (tid == FIN_BATCH - 1) s_rel[FIN_BATCH] = incl;
+    __syncthreads();
+    if (sl == 0) {
         if (has) f.id_off[s0 + tid + 1] = o0 + incl;
         if (t == 0 && tid == 0) f.id_off[0] = 0;
+    }
+    const uint64_t k_beg = total * sl / f.slices, k_end = total * (sl + 1) / f.slices;
 #ifndef FIN_U
 #define FIN_U 16
 #endif
-        constexpr unsigned U = FIN_U;
-        unsigned j = 0;   // the string of this thread's current id (monotone in k)
-        for (uint64_t k0 = 0; k0 < total; k0 += FIN_THREADS * U) {
-            int32_t v[U];
+    constexpr unsigned U = FIN_U;
+    // the string of this thread's first id: the last string whose start is <= it (binary search;
+    // then monotone in k)
+    unsigned j = 0;
+    if (k_beg + tid < k_end) {
+        const uint64_t k = k_beg + tid;
+        unsigned lo = 0, hi = FIN_BATCH;   // s_rel[lo] <= k < s_rel[hi]
+        while (hi - lo > 1) {
+            const unsigned mid = (lo + hi) >> 1;
+            if (s_rel[mid] <= k) lo = mid;
+            else hi = mid;
+        }
+        j = lo;
+    }
+    for (uint64_t k0 = k_beg; k0 < k_end; k0 += FIN_THREADS * U) {
+        int32_t v[U];
 #pragma unroll
-            for (unsigned u = 0; u < U; u++) {
-                const uint64_t k = k0 + (uint64_t)u * FIN_THREADS + tid;
-                v[u] = 0;
-                if (k < total) {
-                    while (s_rel[j + 1] <= k) j++;
-                    v[u] = (int32_t)staging[s_src[j] + (k - s_rel[j])];
-                }
-            }
-#pragma unroll
-            for (unsigned u = 0; u < U; u++) {
-                const uint64_t k = k0 + (uint64_t)u * FIN_THREADS + tid;
-                if (k < total) f.ids[o0 + k] = v[u];
+        for (unsigned u = 0; u < U; u++) {
+            const uint64_t k = k0 + (uint64_t)u * FIN_THREADS + tid;
+            v[u] = 0;
+            if (k < k_end) {
+                while (s_rel[j + 1] <= k) j++;
+                v[u] = (int32_t)staging[s_src[j] + (k - s_rel[j])];
             }
         }
-        __syncthreads();   // s_rel / s_src / s_ticket are rewritten for the next batch
-    }
-    if (tid == 0) {
-        const unsigned d = atomicAdd(&f.ctr[CTR_DONE], 1u);
-        // the last block out: every ticket is taken and every tokenize pass is done
-        if (d + 1 == gridDim.x) reset_counters(f.ctr);
+#pragma unroll
+        for (unsigned u = 0; u < U; u++) {
+            const uint64_t k = k0 + (uint64_t)u * FIN_THREADS + tid;
+            if (k < k_end) f.ids[o0 + k] = v[u];
+        }
     }
 }
 
@@ -2079,7 +2070,7 @@ static void launch_tok(const EncodeArgs &a, const TrieView &tv, uint64_t n_units
 hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t ev[2]) {
     EncodeArgs a;
     a.text = p.text; a.str_off = p.str_off; a.cut_mask = p.cut_mask; a.n_str = p.n_str;
-    a.staging = p.staging; a.staging16 = p.staging16; a.counts = p.counts; a.status = p.status; a.capped = p.capped;
+    a.staging = p.staging; a.staging16 = p.staging16; a.counts = p.counts; a.bsum = p.padded ? nullptr : p.flags; a.status = p.status; a.capped = p.capped;
     a.retry_list = p.retry_list; a.retry_count = p.retry_count; a.work_list = nullptr; a.work_count = nullptr;
     a.long_list = p.retry_list + p.n_str; a.long_count = p.retry_count + 3;
     a.mode = p.mode;
@@ -2133,7 +2124,7 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
         // its waves read a zero count and exit)
         LongLaunch l;
         l.mode = p.mode; l.text = p.text; l.str_off = p.str_off; l.cut_mask = p.cut_mask;
-        l.staging = p.staging; l.staging16 = p.staging16; l.counts = p.counts; l.status = p.status; l.capped = p.capped;
+        l.staging = p.staging; l.staging16 = p.staging16; l.counts = p.counts; l.bsum = p.padded ? nullptr : p.flags; l.status = p.status; l.capped = p.capped;
         l.arena = p.arena; l.arena_cap = p.arena_cap;
         l.arena_used = reinterpret_cast<unsigned long long *>(p.retry_count + 8);
         l.edges = p.edges; l.far = p.far; l.far_cap = p.far_cap;
@@ -2153,12 +2144,16 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
         hipLaunchKernelGGL(reset_kernel, dim3(1), dim3(64), 0, stream, p.retry_count);
         return hipGetLastError();
     }
+    // batch prefixes (and the counter block's reset), then the CSR pass
+    hipLaunchKernelGGL(batch_scan_kernel, dim3(1), dim3(SCAN_THREADS), 0, stream, p.n_str, p.flags, p.bpre, p.retry_count);
     FinishArgs f;
     f.staging = p.staging16 ? (const void *)p.staging16 : (const void *)p.staging;
     f.str_off = p.str_off; f.counts = p.counts; f.n_str = p.n_str; f.id_off = p.id_off; f.ids = p.ids;
-    f.flags = p.flags; f.ctr = p.retry_count; f.epoch = p.epoch;
-    uint64_t fb = (p.n_str + FIN_BATCH - 1) / FIN_BATCH;
-    if (fb > (uint64_t)p.max_blocks * 32u / FIN_THREADS) fb = (uint64_t)p.max_blocks * 32u / FIN_THREADS;   // max_blocks = CUs x 64: 32 waves per CU
+    f.bpre = p.bpre;
+    const uint64_t nb = (p.n_str + FIN_BATCH - 1) / FIN_BATCH;
+    uint64_t sls = (FIN_TARGET_BLOCKS + nb - 1) / nb;
+    f.slices = (unsigned)(sls < 1 ? 1 : (sls > FIN_MAX_SLICES ? FIN_MAX_SLICES : sls));
+    const uint64_t fb = nb * f.slices;
     if (p.staging16) hipLaunchKernelGGL(finish_kernel<int16_t>, dim3((unsigned)fb), dim3(FIN_THREADS), 0, stream, f);
     else hipLaunchKernelGGL(finish_kernel<int32_t>, dim3((unsigned)fb), dim3(FIN_THREADS), 0, stream, f);
     return hipGetLastError();

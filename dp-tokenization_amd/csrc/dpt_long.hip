@@ -112,6 +112,7 @@ struct Args {
     uint64_t arena_cap;
     unsigned long long *arena_used;
     uint64_t *counts;
+    unsigned long long *bsum;   // nullable: per FIN_BATCH strings, the sum of their counts
     int32_t *status;
     int32_t *capped;
     uint64_t *edges;
@@ -545,6 +546,7 @@ __global__ void __launch_bounds__(64) long_kernel(Args a) {
         if (lane == 0) {
             a.status[s] = (int32_t)status;
             a.counts[s] = (status == 0 && !len_only) ? (uint64_t)total : 0ull;
+            if (a.bsum && status == 0 && !len_only && total) atomicAdd(&a.bsum[s / FIN_BATCH], (unsigned long long)total);
             if (a.capped) a.capped[s] = status == 3 ? -1 : (int32_t)capsum;
         }
         phase_sync();
@@ -556,7 +558,7 @@ __global__ void __launch_bounds__(64) long_kernel(Args a) {
 void launch_long(const LongLaunch &p, hipStream_t stream) {
     lng::Args a;
     a.text = p.text; a.str_off = p.str_off; a.cut_mask = p.cut_mask;
-    a.staging = p.staging; a.staging16 = p.staging16; a.counts = p.counts; a.status = p.status; a.capped = p.capped;
+    a.staging = p.staging; a.staging16 = p.staging16; a.counts = p.counts; a.bsum = p.bsum; a.status = p.status; a.capped = p.capped;
     a.rec = reinterpret_cast<uint4 *>(p.arena);
     a.stg = reinterpret_cast<int32_t *>(p.arena + 16 * p.arena_cap);
     a.arena_cap = p.arena_cap;

@@ -399,10 +399,11 @@ def test_histogram_statuses_and_overflow(engines, oracles):
     assert h[nb + 4] > 0   # empty strings were counted under status 2
 
 
-def test_finish_lookback_sizes_and_repeats(engines, oracles):
-    """The finish kernel (decoupled look-back over 64-string batches, ticket order, epoch-tagged
-    flags, counters reset by the last batch) on one ctx across calls of changing sizes -- flags a
-    larger earlier call left behind must never be read as this call's -- against the C oracle."""
+def test_finish_sizes_and_repeats(engines, oracles):
+    """The finish pass (batch sums added by the tokenize passes, one-block scan that zeroes them and
+    resets the counter block, batches split over 1..8 slices by call size) on one ctx across calls
+    of changing sizes -- sums a larger earlier call left behind must never leak into this call's --
+    against the C oracle."""
     torch = pytest.importorskip("torch")
     from dptok import synth
     enc = engines["llama32k"]
@@ -435,9 +436,9 @@ def test_finish_lookback_sizes_and_repeats(engines, oracles):
         assert np.array_equal(ids[: int(roff[-1])].cpu().numpy(), rids)
 
 
-def test_finish_epoch_wrap(engines, oracles):
-    """65 540 calls on one ctx: the 16-bit flag epoch wraps (the host clears the flags) and the
-    results stay exact."""
+def test_finish_repeated_calls(engines, oracles):
+    """4 100 calls on one ctx, with dpt_encode_padded calls (which add no batch sums) between them:
+    every call's batch sums start from zero and the results stay exact."""
     torch = pytest.importorskip("torch")
     from dptok import synth
     enc = engines["toy1k"]
@@ -451,9 +452,14 @@ def test_finish_epoch_wrap(engines, oracles):
     st = torch.empty(n, dtype=torch.int32, device="cuda")
     s = torch.cuda.current_stream().cuda_stream
     rids, roff, rst, _ = oracles["toy1k"].encode_csr(text, offs)
-    for k in range(65540):
+    pids = torch.empty(nb, dtype=torch.int32, device="cuda")
+    cnt = torch.empty(n, dtype=torch.int64, device="cuda")
+    pst = torch.empty(n, dtype=torch.int32, device="cuda")
+    for k in range(4100):
         enc.encode_device(dt.data_ptr(), nb, do.data_ptr(), n, ids.data_ptr(), nb, io.data_ptr(), st.data_ptr(), stream=s)
-        if k % 8192 == 0 or k >= 65530:
+        if k % 7 == 3:
+            enc.encode_device_padded(dt.data_ptr(), nb, do.data_ptr(), n, pids.data_ptr(), nb, cnt.data_ptr(), pst.data_ptr(), stream=s)
+        if k % 512 == 0 or k >= 4090:
             torch.cuda.synchronize()
             assert np.array_equal(io.cpu().numpy().view(np.uint64), roff), k
             assert np.array_equal(ids[: int(roff[-1])].cpu().numpy(), rids), k
