@@ -18,6 +18,7 @@ struct dpt_vocab {
     int device = 0;
     int2 *d_slots = nullptr;
     int32_t *d_ids = nullptr;
+    int16_t *d_pair16 = nullptr;      // int16 vocabularies: ids of the two-byte tokens (b0 << 8 | b1), then the one-byte ones
     int4 *d_slots4 = nullptr;         // {base | TERM, check, id, 0} for the lane kernel
     int32_t root_base = 0;
     int32_t ws_node = -1, ws_base = 0, ws_id = -1;   // the trie node after U+2581 (-1: no such path)
@@ -216,6 +217,11 @@ int dpt_vocab_create(const uint8_t *utf8_blob, const uint64_t *tok_off, const in
     std::vector<int2> slots((size_t)da.n_slots + 65536);
     std::vector<int4> slots4((size_t)da.n_slots + 65536);
     std::vector<uint32_t> filt(da.n_slots, 0u);
+    // C2's one-lookup tokens (int16 vocabularies): pair16[b0 << 8 | b1] = id of the two-byte token
+    // b0 b1, pair16[65536 + b0] = id of the one-byte token b0, -1 where none -- the ids the root table
+    // and the root children give (slots4), in a 128-KB int16 table whose printable-ASCII part (24 KB
+    // of lines) stays in a CU's L1 where the 16-B root-table entries (144 KB) do not
+    std::vector<int16_t> pair16(65536 + 256, (int16_t)-1);
     for (uint32_t t = 0; t < da.n_slots; t++) {
         const int32_t p = da.check[t];
         if (p >= 0 && (uint32_t)p < da.n_slots) {
@@ -240,7 +246,9 @@ int dpt_vocab_create(const uint8_t *utf8_blob, const uint64_t *tok_off, const in
             slots[(size_t)da.n_slots + (b0 << 8) + b1] = make_int2(e2 ? da.base[s2] : 0, (int32_t)y);
             slots4[(size_t)da.n_slots + (b0 << 8) + b1] = make_int4(e2 ? da.base[s2] : 0, (int32_t)y, e2 ? da.id[s2] : -1,
                                                                     e2 ? (int32_t)filt[s2] : 0);
+            pair16[(b0 << 8) + b1] = (int16_t)(e2 ? da.id[s2] : -1);
         }
+        pair16[65536 + b0] = (int16_t)(e1 ? da.id[s1] : -1);
     }
     e = hipMalloc((void **)&v->d_slots, sizeof(int2) * slots.size());
     if (e == hipSuccess) e = hipMalloc((void **)&v->d_slots4, sizeof(int4) * slots4.size());
@@ -248,11 +256,14 @@ int dpt_vocab_create(const uint8_t *utf8_blob, const uint64_t *tok_off, const in
     if (e == hipSuccess) e = hipMalloc((void **)&v->d_ids, sizeof(int32_t) * da.n_slots);
     if (e == hipSuccess) e = hipMemcpy(v->d_slots, slots.data(), sizeof(int2) * slots.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(v->d_ids, da.id, sizeof(int32_t) * da.n_slots, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc((void **)&v->d_pair16, sizeof(int16_t) * pair16.size());
+    if (e == hipSuccess) e = hipMemcpy(v->d_pair16, pair16.data(), sizeof(int16_t) * pair16.size(), hipMemcpyHostToDevice);
     if (e != hipSuccess) {
         dpt::free_double_array(&da);
         if (v->d_slots) (void)hipFree(v->d_slots);
         if (v->d_ids) (void)hipFree(v->d_ids);
         if (v->d_slots4) (void)hipFree(v->d_slots4);
+        if (v->d_pair16) (void)hipFree(v->d_pair16);
         delete v;
         return hip_fail(e, "vocab upload");
     }
@@ -276,7 +287,7 @@ int dpt_vocab_create(const uint8_t *utf8_blob, const uint64_t *tok_off, const in
     v->stats.n_slots = da.n_slots;
     v->stats.max_bytes = da.max_bytes;
     v->stats.max_cp = da.max_cp;
-    v->stats.device_bytes = (uint64_t)da.n_slots * (sizeof(int2) + sizeof(int32_t) + sizeof(int4)) + 65536 * (sizeof(int2) + sizeof(int4));
+    v->stats.device_bytes = (uint64_t)da.n_slots * (sizeof(int2) + sizeof(int32_t) + sizeof(int4)) + 65536 * (sizeof(int2) + sizeof(int4)) + (65536 + 256) * sizeof(int16_t);
     dpt::free_double_array(&da);
     *out = v;
     return DPT_OK;
@@ -288,6 +299,7 @@ int dpt_vocab_destroy(dpt_vocab *v) {
     (void)hipFree(v->d_slots);
     (void)hipFree(v->d_ids);
     (void)hipFree(v->d_slots4);
+    (void)hipFree(v->d_pair16);
     delete v;
     return DPT_OK;
 }
@@ -417,6 +429,7 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
     }
     p.slots = v->d_slots;
     p.slot_ids = v->d_ids;
+    p.pair16 = v->d_pair16;
     p.n_slots = v->stats.n_slots;
     p.slots4 = v->d_slots4;
     p.root_base = v->root_base;

@@ -42,6 +42,7 @@ struct EncodeLaunch {
     // vocabulary
     const int2 *slots;
     const int32_t *slot_ids;
+    const int16_t *pair16;   // ids of the one- and two-byte tokens (dpt_api.cpp dpt_vocab_create; int16 staging only)
     const int4 *slots4;      // {base | TERM<<31 | LEAF<<30, check, id, child filter}
     uint32_t n_slots;
     int32_t root_base;

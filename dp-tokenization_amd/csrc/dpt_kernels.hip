@@ -247,6 +247,7 @@ struct TrieView {
     const int4 *__restrict__ slots4;  // {base, check, id, 0}: C2's walks get the id with the last node
     int32_t root_base;
     uint32_t n_slots;
+    const int16_t *__restrict__ pair16;   // [b0 << 8 | b1]: id of the two-byte token, [65536 + b0]: of the one-byte one (-1: none)
 };
 
 // Trie reads through buffer resources: 32-bit slot offsets (no 64-bit address arithmetic) and a
@@ -1574,6 +1575,9 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
             // the stored bytes once a round would overflow it (walk_pending); a longer one is walked
             // below by the refill walker.
             constexpr bool BULK = G == 16 && !BIG;
+#ifndef C2_PAIR16
+#define C2_PAIR16 1   // A/B knob: 0 = the bulk pass reads the root children / root table (slots4)
+#endif
 #ifndef PEND_CAP
 #define PEND_CAP 64   // residual tokens a wave's pending row holds (A/B knob; the scratch row has 64 entries)
 #endif
@@ -1612,13 +1616,25 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                                               ((unsigned)(b0 == ' ') | (unsigned)(b0 == '\n') | (q.fw & (unsigned)(jj == 0)) |
                                                ((unsigned)(nbytes == 2u) & ((unsigned)(b1 == ' ') | (unsigned)(b1 == '\n'))));
                         const unsigned bulk = (unsigned)in & (unsigned)(nbytes - 1u <= 1u) & (expd ^ 1u);
-                        ix[u] = bulk ? (nbytes == 1u ? tv.root_base + (int32_t)b0 : (int32_t)(tv.n_slots + (b0 << 8) + b1)) : 0;
+                        if constexpr (SW == 1 && C2_PAIR16)   // int16 ids: the 128-KB pair table (L1-resident for ASCII)
+                            ix[u] = bulk ? (int32_t)(nbytes == 1u ? 65536u + b0 : (b0 << 8) + b1) : 0;
+                        else
+                            ix[u] = bulk ? (nbytes == 1u ? tv.root_base + (int32_t)b0 : (int32_t)(tv.n_slots + (b0 << 8) + b1)) : 0;
                         kind[u] = bulk ? nbytes : 0u;
                         oq[u] = q.ob + k;
                         const bool res = in && !bulk;
                         const uint64_t m = ballot(res);
                         if (res) list_ref(r + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u))) = (uint16_t)t;
                         r += (unsigned)__builtin_popcountll(m);
+                    }
+                    if constexpr (SW == 1 && C2_PAIR16) {
+                        int16_t pv[4];
+#pragma unroll
+                        for (int u = 0; u < 4; u++) pv[u] = tv.pair16[ix[u]];
+#pragma unroll
+                        for (int u = 0; u < 4; u++)
+                            if (kind[u]) a.staging16[oq[u]] = pv[u];
+                        continue;
                     }
                     int4 ent[4];
 #pragma unroll
@@ -2080,7 +2096,7 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     a.wsl_scratch = p.wsl_scratch;
     a.pend = p.pend; a.ws_node = p.ws_node; a.ws_base = p.ws_base; a.ws_id = p.ws_id;
     a.long_span = p.long_span;
-    TrieView tv{p.slots, p.slot_ids, p.slots4, p.root_base, p.n_slots};
+    TrieView tv{p.slots, p.slot_ids, p.slots4, p.root_base, p.n_slots, p.pair16};
     const bool wide = (p.mode & DPT_MODE_MASK) == DPT_MODE_ATOMS;   // atoms of up to 8 bytes
 
     if (p.n_str == 0) {
