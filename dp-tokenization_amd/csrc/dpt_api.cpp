@@ -18,7 +18,7 @@ struct dpt_vocab {
     int device = 0;
     int2 *d_slots = nullptr;
     int32_t *d_ids = nullptr;
-    int16_t *d_pair16 = nullptr;      // int16 vocabularies: ids of the two-byte tokens (b0 << 8 | b1), then the one-byte ones
+    int16_t *d_pair16 = nullptr;      // C2's pair-id table (dpt::PAIR16_N int16), then phase A0's byte-pair table (65536 uint2)
     int4 *d_slots4 = nullptr;         // {base | TERM, check, id, 0} for the lane kernel
     int32_t root_base = 0;
     int32_t ws_node = -1, ws_base = 0, ws_id = -1;   // the trie node after U+2581 (-1: no such path)
@@ -222,6 +222,11 @@ int dpt_vocab_create(const uint8_t *utf8_blob, const uint64_t *tok_off, const in
     // and the root children give (slots4), in a 128-KB int16 table whose printable-ASCII part (24 KB
     // of lines) stays in a CU's L1 where the 16-B root-table entries (144 KB) do not
     std::vector<int16_t> pair16(65536 + 256, (int16_t)-1);
+    // phase A0 (byte-parallel first lookups of pure-ASCII windows) needs only flags and the child
+    // filter of the root-table entry: a0[b0 << 8 | b1] = {b0 is a root child | b0 is a token << 1 |
+    // node b0 b1 exists << 2 | it ends a token << 3 | it is a leaf << 4, its child filter} -- 8 B
+    // instead of the 16-B slots4 entry, so twice the entries per L1/L2 line
+    std::vector<uint2> a0((size_t)65536, make_uint2(0u, 0u));
     for (uint32_t t = 0; t < da.n_slots; t++) {
         const int32_t p = da.check[t];
         if (p >= 0 && (uint32_t)p < da.n_slots) {
@@ -247,6 +252,10 @@ int dpt_vocab_create(const uint8_t *utf8_blob, const uint64_t *tok_off, const in
             slots4[(size_t)da.n_slots + (b0 << 8) + b1] = make_int4(e2 ? da.base[s2] : 0, (int32_t)y, e2 ? da.id[s2] : -1,
                                                                     e2 ? (int32_t)filt[s2] : 0);
             pair16[(b0 << 8) + b1] = (int16_t)(e2 ? da.id[s2] : -1);
+            a0[(b0 << 8) + b1] = make_uint2((e1 ? 1u : 0u) | (term1 ? 2u : 0u) | (e2 ? 4u : 0u) |
+                                                (e2 && (da.base[s2] & (int32_t)0x80000000) ? 8u : 0u) |
+                                                (e2 && (da.base[s2] & 0x40000000) ? 16u : 0u),
+                                            e2 ? filt[s2] : 0u);
         }
         pair16[65536 + b0] = (int16_t)(e1 ? da.id[s1] : -1);
     }
@@ -256,8 +265,10 @@ int dpt_vocab_create(const uint8_t *utf8_blob, const uint64_t *tok_off, const in
     if (e == hipSuccess) e = hipMalloc((void **)&v->d_ids, sizeof(int32_t) * da.n_slots);
     if (e == hipSuccess) e = hipMemcpy(v->d_slots, slots.data(), sizeof(int2) * slots.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(v->d_ids, da.id, sizeof(int32_t) * da.n_slots, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMalloc((void **)&v->d_pair16, sizeof(int16_t) * pair16.size());
+    // one allocation, one kernel pointer (SGPRs are what the hot kernel spills): pair16, then a0
+    if (e == hipSuccess) e = hipMalloc((void **)&v->d_pair16, sizeof(int16_t) * dpt::PAIR16_N + sizeof(uint2) * a0.size());
     if (e == hipSuccess) e = hipMemcpy(v->d_pair16, pair16.data(), sizeof(int16_t) * pair16.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(v->d_pair16 + dpt::PAIR16_N, a0.data(), sizeof(uint2) * a0.size(), hipMemcpyHostToDevice);
     if (e != hipSuccess) {
         dpt::free_double_array(&da);
         if (v->d_slots) (void)hipFree(v->d_slots);
@@ -287,7 +298,7 @@ int dpt_vocab_create(const uint8_t *utf8_blob, const uint64_t *tok_off, const in
     v->stats.n_slots = da.n_slots;
     v->stats.max_bytes = da.max_bytes;
     v->stats.max_cp = da.max_cp;
-    v->stats.device_bytes = (uint64_t)da.n_slots * (sizeof(int2) + sizeof(int32_t) + sizeof(int4)) + 65536 * (sizeof(int2) + sizeof(int4)) + (65536 + 256) * sizeof(int16_t);
+    v->stats.device_bytes = (uint64_t)da.n_slots * (sizeof(int2) + sizeof(int32_t) + sizeof(int4)) + 65536 * (sizeof(int2) + sizeof(int4)) + (65536 + 256) * sizeof(int16_t) + 65536 * sizeof(uint2);
     dpt::free_double_array(&da);
     *out = v;
     return DPT_OK;

@@ -42,7 +42,8 @@ struct EncodeLaunch {
     // vocabulary
     const int2 *slots;
     const int32_t *slot_ids;
-    const int16_t *pair16;   // ids of the one- and two-byte tokens (dpt_api.cpp dpt_vocab_create; int16 staging only)
+    const int16_t *pair16;   // ids of the one- and two-byte tokens (PAIR16_N int16), then phase A0's byte-pair flags
+                             //   + child filters (65536 uint2) -- dpt_api.cpp dpt_vocab_create
     const int4 *slots4;      // {base | TERM<<31 | LEAF<<30, check, id, child filter}
     uint32_t n_slots;
     int32_t root_base;
@@ -53,6 +54,9 @@ struct EncodeLaunch {
 // PART_STRIDE uint32 (a 256-byte line each), from byte PART_CTR_OFFSET of the counter block, then the
 // used-up mask; the counter block is CTR_ALLOC_BYTES long (the host path copies its first 64 bytes)
 constexpr unsigned NPART_MAX = 32;
+// entries of the pair-id table (65536 byte pairs + 256 single bytes, int16; a multiple of 4 so the
+// A0 table after it is 8-byte aligned)
+constexpr unsigned PAIR16_N = 65536 + 256;
 // strings per finish batch (the batch arrays are sized one per 64 strings, two arrays)
 constexpr unsigned FIN_BATCH = 256;
 constexpr unsigned PART_STRIDE = 64;

@@ -247,7 +247,10 @@ struct TrieView {
     const int4 *__restrict__ slots4;  // {base, check, id, 0}: C2's walks get the id with the last node
     int32_t root_base;
     uint32_t n_slots;
-    const int16_t *__restrict__ pair16;   // [b0 << 8 | b1]: id of the two-byte token, [65536 + b0]: of the one-byte one (-1: none)
+    // [b0 << 8 | b1]: id of the two-byte token, [65536 + b0]: of the one-byte one (-1: none); then, from
+    // element PAIR16_N, A0's uint2 table [b0 << 8 | b1]: flags (root child b0, b0 a token, node b0 b1, its
+    // TERM, LEAF) + that node's child filter
+    const int16_t *__restrict__ pair16;
 };
 
 // Trie reads through buffer resources: 32-bit slot offsets (no 64-bit address arithmetic) and a
@@ -870,6 +873,9 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                         auto byte_at = [&](unsigned q) -> unsigned {   // byte k0+q, END past the window
                             return k0 + q < wl ? (unsigned)((w >> (8u * q)) & 0xFFu) : END;
                         };
+#ifndef A0_PACK
+#define A0_PACK 1   // A/B knob: 0 = A0 reads the 16-B root-table / root-child entries (slots4)
+#endif
 #ifndef A0_INFLIGHT
 #define A0_INFLIGHT 4
 #endif
@@ -888,13 +894,25 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                             const unsigned stop = (unsigned)(n1 == END) | (unsigned)(n1 == ' ');
                             const unsigned e1 = n1 == '\n' ? (unsigned)'<' : n1;
                             // a one-byte atom at the word's end: its own slot; else the two-byte root entry
+#if A0_PACK
+                            // the packed byte-pair table: the flags of b0 do not depend on the second byte
+                            (void)stop;
+                            idx[uq] = (int32_t)(((b & 0xFFu) << 8) | (e1 & 0xFFu));
+#else
                             const int32_t i1 = tv.root_base + (int32_t)(b & 0xFFu);
                             const int32_t i2 = (int32_t)(tv.n_slots + ((b & 0xFFu) << 8) + (e1 & 0xFFu));
                             idx[uq] = stop ? i1 : i2;
+#endif
                         }
+#if A0_PACK
+                        uint2 ent[A0_INFLIGHT];
+#pragma unroll
+                        for (int uq = 0; uq < A0_INFLIGHT; uq++) ent[uq] = reinterpret_cast<const uint2 *>(tv.pair16 + PAIR16_N)[idx[uq]];
+#else
                         int4 ent[A0_INFLIGHT];
 #pragma unroll
                         for (int uq = 0; uq < A0_INFLIGHT; uq++) ent[uq] = trie_slotA(tv, idx[uq]);
+#endif
                         // Per byte: tk1 bit u = a one-atom token ends at k0+1+u, tk2 bit u = a two-atom
                         // token ends at k0+2+u (the end masks are written once below)
 #pragma unroll
@@ -902,23 +920,32 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                             const int u = u0 + uq;
                             const unsigned k = k0 + (unsigned)u;
                             const unsigned b = byte_at(u), n1 = byte_at(u + 1), n2 = byte_at(u + 2);
-                            const int4 e = ent[uq];
+                            const auto e = ent[uq];
                             const unsigned valid = (unsigned)(b != END);
                             const unsigned special = (unsigned)(b == ' ') | (unsigned)(b == '\n') | ((unsigned)first & (unsigned)(k == 0));   // the walker's
                             const unsigned norm = valid & (special ^ 1u);
                             // n1 ends the word: the lookup was the atom's own root slot
                             const unsigned wend = (unsigned)(n1 == END) | (unsigned)(n1 == ' ');
+#if A0_PACK
+                            const unsigned xterm = ((unsigned)e.x >> 3) & 1u, xleaf = ((unsigned)e.x >> 4) & 1u;
+                            const unsigned tok1 = (unsigned)e.x & ((unsigned)e.x >> 1) & 1u;
+                            const unsigned node2 = ((unsigned)e.x >> 2) & 1u;
+                            const unsigned filt = (unsigned)e.y;
+#else
                             const unsigned y30 = ((unsigned)e.y >> 30) & 1u, y31 = (unsigned)e.y >> 31;
                             const unsigned xterm = (unsigned)e.x >> 31, xleaf = ((unsigned)e.x >> 30) & 1u;
                             const unsigned tok1 = wend ? ((unsigned)(e.y == 0) & xterm) : (y30 & y31);
+                            const unsigned node2 = y30 & (unsigned)((e.y & 0x3FFFFFFF) != 0);
+                            const unsigned filt = (unsigned)e.w;
+#endif
                             nocap |= (norm & (tok1 ^ 1u)) != 0;
                             // a node after two bytes: n1 = '\n' leaves the walk inside "<0x0A>" after
                             // its '<'; otherwise atom k+1 is consumed (the span k .. k+2)
-                            const unsigned has2 = norm & (wend ^ 1u) & y30 & (unsigned)((e.y & 0x3FFFFFFF) != 0);
+                            const unsigned has2 = norm & (wend ^ 1u) & node2;
                             const unsigned nl1 = (unsigned)(n1 == '\n');
                             const unsigned e2 = nl1 ? (unsigned)'0' : (n2 == '\n' ? (unsigned)'<' : n2);
                             const unsigned more = has2 & (xleaf ^ 1u) & (nl1 | ((unsigned)(n2 != END) & (unsigned)(n2 != ' '))) &
-                                                  (((unsigned)e.w >> child_bit(e2)) & 1u);
+                                                  ((filt >> child_bit(e2)) & 1u);
                             tk1 |= (norm & tok1) << u;
                             tk2 |= (has2 & (nl1 ^ 1u) & xterm) << u;
                             mark |= ((valid & special) | more) << (4 * g + u);
