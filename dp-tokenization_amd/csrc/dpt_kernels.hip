@@ -2104,7 +2104,16 @@ static unsigned resident_per_cu() {
 template <int CH, int G, bool BIG, bool WIDE, int SW = 0>
 static void launch_tok(const EncodeArgs &a, const TrieView &tv, uint64_t n_units, unsigned n_cu, hipStream_t stream) {
     constexpr int lds = block_lds_bytes<CH, G>();
-    uint64_t blocks = (uint64_t)n_cu * resident_per_cu<CH, G, BIG, WIDE, SW>();
+    uint64_t wpc = resident_per_cu<CH, G, BIG, WIDE, SW>();
+    if constexpr (G == 16 && !BIG) {
+        // small calls: no more resident waves than give every slot ~7 strings (rounds of 4 strings per
+        // wave; a wave's last round is the tail): 125k strings run 3 % faster at 18 waves per CU than
+        // at the occupancy limit of 22, 250k and more are fastest at 22 (profiles/r02_ab_issue_model.log)
+        const uint64_t want = (n_units + 7ull * n_cu - 1) / (7ull * n_cu);   // n_units = strings / 4
+        const uint64_t lo = wpc < 16u ? wpc : 16u;
+        if (want < wpc) wpc = want > lo ? want : lo;
+    }
+    uint64_t blocks = (uint64_t)n_cu * wpc;
     if (blocks > (uint64_t)n_cu * 64u) blocks = (uint64_t)n_cu * 64u;   // the scratch is sized for 64 per CU
     if (blocks > n_units) blocks = n_units ? n_units : 1;
     hipLaunchKernelGGL((tokenize_kernel<CH, G, BIG, WIDE, SW>), dim3((unsigned)blocks), dim3(64), lds, stream, a, tv);
