@@ -1951,6 +1951,8 @@ struct FinishArgs {
     int32_t *ids;
     const unsigned long long *bpre;   // per batch: its first id (batch_scan_kernel)
     unsigned slices;                  // blocks per batch
+    unsigned long long *bsum;         // one-batch calls (no scan kernel): zeroed here ...
+    uint32_t *ctr;                    // ... and the counter block reset here (both null otherwise)
 };
 
 // CSR offsets and ids: block b takes slice b % slices of batch b / slices.  One count per thread of
@@ -1971,7 +1973,7 @@ __global__ void __launch_bounds__(FIN_THREADS) finish_kernel(FinishArgs f) {
     const uint64_t base_off = f.str_off[0];
     const ST *__restrict__ staging = reinterpret_cast<const ST *>(f.staging);
     const uint64_t s0 = t * FIN_BATCH;
-    const uint64_t o0 = f.bpre[t];
+    const uint64_t o0 = f.bsum ? 0ull : f.bpre[t];   // one batch: its first id is 0
     // the first FIN_BATCH threads hold one string each; every thread copies
     const bool has = tid < FIN_BATCH && tid < f.n_str - s0;
     const uint64_t c = has ? f.counts[s0 + tid] : 0ull;
@@ -1986,7 +1988,13 @@ __global__ void __launch_bounds__(FIN_THREADS) finish_kernel(FinishArgs f) {
     __syncthreads();
     if (sl == 0) {
         if (has) f.id_off[s0 + tid + 1] = o0 + incl;
-        if (t == 0 && tid == 0) f.id_off[0] = 0;
+        if (t == 0 && tid == 0) {
+            f.id_off[0] = 0;
+            if (f.bsum) {   // one-batch call: the scan kernel's other duties (every tokenize pass is done)
+                f.bsum[0] = 0;
+                reset_counters(f.ctr);
+            }
+        }
     }
     const uint64_t k_beg = total * sl / f.slices, k_end = total * (sl + 1) / f.slices;
 #ifndef FIN_U
@@ -2196,13 +2204,16 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
         hipLaunchKernelGGL(reset_kernel, dim3(1), dim3(64), 0, stream, p.retry_count);
         return hipGetLastError();
     }
-    // batch prefixes (and the counter block's reset), then the CSR pass
-    hipLaunchKernelGGL(batch_scan_kernel, dim3(1), dim3(SCAN_THREADS), 0, stream, p.n_str, p.flags, p.bpre, p.retry_count);
+    // batch prefixes (and the counter block's reset), then the CSR pass; a one-batch call (<= 256
+    // strings: the drop-in's per-string calls) needs no prefix, and its finish block does the rest
+    const uint64_t nb = (p.n_str + FIN_BATCH - 1) / FIN_BATCH;
     FinishArgs f;
+    f.bsum = nullptr; f.ctr = nullptr;
+    if (nb > 1) hipLaunchKernelGGL(batch_scan_kernel, dim3(1), dim3(SCAN_THREADS), 0, stream, p.n_str, p.flags, p.bpre, p.retry_count);
+    else { f.bsum = p.flags; f.ctr = p.retry_count; }
     f.staging = p.staging16 ? (const void *)p.staging16 : (const void *)p.staging;
     f.str_off = p.str_off; f.counts = p.counts; f.n_str = p.n_str; f.id_off = p.id_off; f.ids = p.ids;
     f.bpre = p.bpre;
-    const uint64_t nb = (p.n_str + FIN_BATCH - 1) / FIN_BATCH;
     uint64_t sls = (FIN_TARGET_BLOCKS + nb - 1) / nb;
     f.slices = (unsigned)(sls < 1 ? 1 : (sls > FIN_MAX_SLICES ? FIN_MAX_SLICES : sls));
     const uint64_t fb = nb * f.slices;
