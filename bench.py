@@ -19,6 +19,7 @@ Launch: python bench.py --gpus 1 --steps K --warmup W
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import multiprocessing as mp
 import os
@@ -41,15 +42,17 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=["cfg2", "cfg4", "cfg5", "bloom"], default="cfg2",
-                    help="cfg2 (the metric's config): 256-byte random ASCII; cfg4: S2ORC-shaped; cfg5: Arabic-shaped; "
+    ap.add_argument("--workload", choices=["cfg1", "cfg2", "cfg4", "cfg5", "bloom"], default="cfg2",
+                    help="cfg2 (the metric's config): 256-byte random ASCII; cfg1: BASELINE configs[0], 1k x 64-byte "
+                         "random ASCII with the toy 1k vocabulary (the reference's CPU plumbing case); "
+                         "cfg4: S2ORC-shaped; cfg5: Arabic-shaped; "
                          "bloom: row f3 at BLOOM scale (250,680-entry byte-level BPE, atoms mode, <= 256-byte strings)")
     ap.add_argument("--strings", type=int, default=None,
                     help="strings of the global corpus (strong) or per GPU (weak); default 1M (cfg4: 200k)")
     ap.add_argument("--scaling", choices=["strong", "weak"], default=None,
                     help="strong (default for N > 1; identical at N = 1): the global corpus is sharded over the "
                          "ranks by dptok.dist.shard_range; weak: every rank owns --strings strings")
-    ap.add_argument("--length", type=int, default=256)
+    ap.add_argument("--length", type=int, default=None, help="bytes per string (default 256; cfg1: 64)")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--exact-sample", type=int, default=None,
                     help="strings checked against the C oracle (rank 0; default: every string of the rank's shard)")
@@ -99,16 +102,16 @@ def exact_matches(ids_h, off_h, st_h, rids, roff, rst, S: int) -> int:
 _PORT = {}
 
 
-def _port_init(bloom: bool = False):
+def _port_init(kind: str = "llama"):
     from dptok import synth
     from oracle import ref_port
-    if bloom:
+    if kind == "bloom":
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         from bloom_fixture import big_vocab
         _PORT["t2i"] = big_vocab()
         _PORT["f"] = ref_port.dp_tokenize_word_atoms
     else:
-        _PORT["t2i"] = synth.llama_shaped_vocab()
+        _PORT["t2i"] = synth.toy_vocab() if kind == "toy" else synth.llama_shaped_vocab()
         _PORT["f"] = ref_port.dp_tokenize_raw
 
     def _alarm(signum, frame):
@@ -150,12 +153,12 @@ def words_of_atoms(text: np.ndarray, offs: np.ndarray, cut: np.ndarray) -> list:
     return out
 
 
-def cpu_baseline(items, budget, cores, bloom=False):
+def cpu_baseline(items, budget, cores, kind="llama"):
     """The reference's enumerate-then-select DP (oracle/ref_port.py) on `cores` processes; items =
     (input, bytes) pairs."""
     done_bytes, n_done, n_to = 0, 0, 0
     ctx = mp.get_context("fork")
-    with ctx.Pool(cores, initializer=_port_init, initargs=(bloom,)) as pool:
+    with ctx.Pool(cores, initializer=_port_init, initargs=(kind,)) as pool:
         t0 = time.perf_counter()
         it = pool.imap_unordered(_port_one, items, chunksize=4)
         for nb, ok in it:
@@ -271,14 +274,16 @@ def main():
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         from bloom_fixture import big_vocab
         t2i = big_vocab()
+    elif args.workload == "cfg1":
+        t2i = synth.toy_vocab()
     else:
         t2i = synth.llama_shaped_vocab()
-    Lb = args.length
+    Lb = args.length or (64 if args.workload == "cfg1" else 256)
     cores, cpus_visible = cpu_share()
     gen_procs = args.gen_procs or max(1, min(16, cores))
     if args.cpu_sample is None:
         args.cpu_sample = 262144 if bloom else 2048
-    default_n = {"cfg4": 200_000, "bloom": 500_000}.get(args.workload, 1_000_000)
+    default_n = {"cfg1": 1000, "cfg4": 200_000, "bloom": 500_000}.get(args.workload, 1_000_000)
     N = args.strings or default_n
     lo, hi = rank_strings(N, rank, world, scaling)
     M = hi - lo
@@ -290,6 +295,11 @@ def main():
               "BLOOM-scale vocabulary")
         data = ("synthetic byte-level words (dptok.synth.bloom_like_corpus: 15% tokens > 16 code points); synthetic "
                 "250,680-entry byte-level BPE (tests/golden/bloom_big_tokenizer.json.xz)")
+    elif args.workload == "cfg1":
+        text, offs = synth.random_ascii_corpus(M, Lb, seed=args.seed, start=lo)
+        wl = f"cfg1: {N} x {Lb}-byte random ASCII strings {per}, raw pre-tokenization, toy 1k vocabulary"
+        data = ("synthetic random printable ASCII (Philox keyed by seed+global index; tests/golden/cfg1_toy1k holds the "
+                "reference's outputs for seed 1); synthetic toy 1000-entry vocab")
     elif args.workload == "cfg2":
         text, offs = synth.random_ascii_corpus(M, Lb, seed=args.seed, start=lo)
         wl = f"cfg2: {N // 1000}k x {Lb}-byte random ASCII strings {per}, raw pre-tokenization"
@@ -315,11 +325,19 @@ def main():
         else:
             inputs = synth.unpack(text[: int(offs[args.cpu_sample])], sub)
         items = list(zip(inputs, np.diff(sub).astype(int).tolist()))
-        v, nd, nto, cdt = cpu_baseline(items, args.cpu_budget, cores, bloom)
+        v, nd, nto, cdt = cpu_baseline(items, args.cpu_budget, cores,
+                                       "bloom" if bloom else ("toy" if args.workload == "cfg1" else "llama"))
         cpu = {"value": v, "unit": "bytes/s", "cores": cores, "host_cpus_visible": cpus_visible, "kind": "port",
                "sample": f"{nd} of the first {args.cpu_sample} {args.workload} strings in {cdt:.1f}s "
                          f"(enumerate-then-select, oracle/ref_port.py, {cores} processes = the box's CPU share "
                          f"OMP_NUM_THREADS of {cpus_visible} visible CPUs; {nto} hit the 10s per-string limit)"}
+        if args.workload == "cfg1":
+            # BASELINE.md quotes the reference on cfg1 on ONE core (79.2 KB/s): the port on one core too
+            _port_init("toy")
+            t0c = time.perf_counter()
+            for x, _ in items:
+                _PORT["f"](x, _PORT["t2i"])
+            cpu["port_1core_bytes_per_s"] = sum(nb for _, nb in items) / (time.perf_counter() - t0c)
 
     gpu = local % max(1, torch.cuda.device_count())
     if gpu != local and args.dist_backend == "nccl":
@@ -442,6 +460,10 @@ def main():
         dtp = float(t.item())
     padded_same = bool(torch.equal(d_cnt[:M], (d_idoff[1:] - d_idoff[:-1])[:M]) and torch.equal(d_pst[:M], d_status[:M]))
 
+    # every unbounded-pass string fitted the arena (else it has status 3 and the device path refused it)
+    need, cap = enc.long_need()
+    if need > cap:
+        raise SystemExit(f"bench: the unbounded pass needed {need} arena bytes of {cap}: reserve more")
     hist = d_hists[(n_step[0] - 1) % 2].cpu().numpy()   # the last step's reduced histogram
     n_tok_rank = int(d_idoff[-1].item())
     n_tok_all = int(hist[N_BINS])          # after the all-reduce: all ranks' ids
@@ -497,11 +519,16 @@ def main():
             "data": data,
             "config": {"workload": wl, "strings_total": strings_all,
                        "strings_per_gpu": M, "bytes_per_string": Lb,
-                       "vocab": "synthetic byte-level BPE 250680" if bloom else "synthetic llama-shaped 32000",
+                       "vocab": ("synthetic byte-level BPE 250680" if bloom else
+                                 "synthetic toy 1000" if args.workload == "cfg1" else "synthetic llama-shaped 32000"),
                        "parallelism": f"dp{world} ({scaling} scaling: corpus shards, 1 all-reduce of the histogram per step)"},
             "per_gpu_bytes_per_s": value / world,
             "tokens_per_byte": n_tok_all / max(bytes_all, 1.0),
             "ok_strings": ok_strings,
+            # the reduced histogram itself (tests/test_gpu_sharded.py compares ranks x shards runs)
+            "histogram": {"n_bins": N_BINS, "sha256": hashlib.sha256(hist.astype("<i8").tobytes()).hexdigest(),
+                          "total_ids": n_tok_all, "total_strings": int(hist[N_BINS + 1]),
+                          "status": [int(x) for x in hist[N_BINS + 2:N_BINS + 7]]},
             "exact_match": exact,
             "stage_ms_per_step": {"tokenize": ms_stage[0] / max(launches, 1)},   # finish (offsets + CSR ids): rocprof
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -35,6 +35,7 @@ struct dpt_ctx {
     uint64_t cap16 = 0;
     uint8_t *arena = nullptr;         // the unbounded pass's scratch, 20 bytes per input byte it holds
     uint64_t arena_cap = 0;           // input bytes
+    bool arena_reserved = false;      // dpt_ctx_reserve_vocab set it: the encode path does not resize it
     uint64_t *counts = nullptr;
     uint32_t *retry_list = nullptr;
     uint64_t cap_str = 0;
@@ -123,11 +124,14 @@ constexpr size_t COUNTER_BYTES = 64;
 int ensure_workspace(dpt_ctx *c, const dpt_vocab *v, uint64_t n_bytes, uint64_t n_str, uint64_t long_bytes,
                      bool staging = true) {
     hipError_t e;
+    bool fresh = false;   // zeroed buffers were (re)allocated
     const bool need16 = staging && (!v || v->ids16), need32 = staging && (!v || !v->ids16);
     if (need16 && (e = grow(&c->staging16, &c->cap16, n_bytes)) != hipSuccess) return hip_fail(e, "hipMalloc(staging16)");
     if (need32 && (e = grow(&c->staging32, &c->cap32, n_bytes)) != hipSuccess) return hip_fail(e, "hipMalloc(staging32)");
+    // long_bytes = 0 (the encode path): the default size, unless the caller reserved the arena -- a
+    // reserved arena is left alone, so a reserved call never reallocates (capture-safe, dpt.h)
     const uint64_t lb = long_bytes ? long_bytes : default_long_bytes(n_bytes);
-    if (lb > c->arena_cap || !c->arena) {
+    if (!c->arena || (lb > c->arena_cap && (long_bytes || !c->arena_reserved))) {
         uint64_t cap = c->arena_cap ? c->arena_cap * ARENA_PER_BYTE : 0;
         if ((e = grow(&c->arena, &cap, lb * ARENA_PER_BYTE)) != hipSuccess) return hip_fail(e, "hipMalloc(arena)");
         c->arena_cap = cap / ARENA_PER_BYTE;
@@ -147,6 +151,7 @@ int ensure_workspace(dpt_ctx *c, const dpt_vocab *v, uint64_t n_bytes, uint64_t 
         if ((e = grow(&c->flags, &c->cap_flags, want)) != hipSuccess) return hip_fail(e, "hipMalloc(flags)");
         // the batch sums start at zero; every call's batch_scan_kernel zeroes them again
         if ((e = hipMemset(c->flags, 0, c->cap_flags * sizeof(unsigned long long))) != hipSuccess) return hip_fail(e, "hipMemset(flags)");
+        fresh = true;
     }
     if (!c->wsl_scratch) {
         e = hipMalloc((void **)&c->wsl_scratch, dpt::wsl_scratch_bytes(c->max_blocks));
@@ -161,7 +166,11 @@ int ensure_workspace(dpt_ctx *c, const dpt_vocab *v, uint64_t n_bytes, uint64_t 
         e = hipMalloc((void **)&c->retry_count, dpt::CTR_ALLOC_BYTES);
         if (e == hipSuccess) e = hipMemset(c->retry_count, 0, dpt::CTR_ALLOC_BYTES);
         if (e != hipSuccess) return hip_fail(e, "hipMalloc(retry_count)");
+        fresh = true;
     }
+    // the zero state every later call relies on must be in place before a call on any stream (a
+    // non-blocking stream is not ordered after the null stream's memsets); allocations only
+    if (fresh && (e = hipDeviceSynchronize()) != hipSuccess) return hip_fail(e, "hipDeviceSynchronize(zeroed workspace)");
     return DPT_OK;
 }
 
@@ -359,7 +368,9 @@ int dpt_ctx_reserve_vocab(dpt_ctx *c, const dpt_vocab *v, uint64_t n_bytes, uint
     if (!c) return fail(DPT_E_ARG, "null ctx");
     if (v && v->device != c->device) return fail(DPT_E_ARG, "ctx and vocab on different devices");
     DeviceGuard g(c->device);
-    return ensure_workspace(c, v, n_bytes, n_str, long_bytes);
+    const int rc = ensure_workspace(c, v, n_bytes, n_str, long_bytes);
+    if (rc == DPT_OK && long_bytes) c->arena_reserved = true;
+    return rc;
 }
 
 int dpt_ctx_workspace_bytes(const dpt_ctx *c, uint64_t *device_path, uint64_t *host_path) {
@@ -482,10 +493,15 @@ int dpt_encode_padded(dpt_ctx *c, const dpt_vocab *v, int mode, const uint8_t *t
                        nullptr, hip_stream, nullptr, 0, counts);
 }
 
+static int rerun_too_long(dpt_ctx *c, const dpt_vocab *v, int mode, const uint8_t *text, const uint64_t *str_off,
+                          const uint8_t *cut_mask, uint64_t n_str, int32_t *ids, uint64_t ids_cap, uint64_t *id_off,
+                          int32_t *status, int32_t *capped_len);
+
 static int encode_host_impl(dpt_ctx *c, const dpt_vocab *v, int mode, const uint8_t *text, uint64_t n_bytes,
                             const uint64_t *str_off, const uint8_t *cut_mask, uint64_t n_str, int32_t *ids,
                             uint64_t ids_cap, uint64_t *id_off, int32_t *status, int32_t *capped_len,
-                            uint64_t *edges, uint64_t *far = nullptr, uint64_t far_cap = 0, uint64_t *n_far = nullptr) {
+                            uint64_t *edges, uint64_t *far = nullptr, uint64_t far_cap = 0, uint64_t *n_far = nullptr,
+                            int depth = 0) {
     // host arguments first (checkable without a device)
     if (!str_off || !id_off || (n_str && !status)) return fail(DPT_E_ARG, "null output/offsets");
     if (n_bytes && (!text || !ids)) return fail(DPT_E_ARG, "null text/ids");
@@ -530,6 +546,7 @@ static int encode_host_impl(dpt_ctx *c, const dpt_vocab *v, int mode, const uint
     const uint64_t *p_idoff = reinterpret_cast<const uint64_t *>(c->p_out);
     // small batches: everything in one copy (ids up to the n_bytes bound); large: the head, then the ids
     const bool one_copy = 4 * n_bytes <= (4ull << 20);
+    bool overflow = false;   // some strings got status 3 (arena full): they alone run again below
     for (int attempt = 0;; attempt++) {
         int rc = encode_impl(c, v, mode, c->d_in, n_bytes, reinterpret_cast<const uint64_t *>(c->d_in + o_off),
                              cut ? c->d_in + o_cut : nullptr, n_str, d_ids, n_bytes ? n_bytes : 1, d_idoff, d_status,
@@ -547,8 +564,14 @@ static int encode_host_impl(dpt_ctx *c, const dpt_vocab *v, int mode, const uint
         if (used <= c->arena_cap) break;
         // the unbounded pass's arena was too small for the strings routed to it (those strings got
         // status 3): grow it to what the pass claimed and run the call again
-        if (attempt > 0) return fail(DPT_E_ARG, "unbounded pass arena overflow after growth");
+        if (attempt > 0 || depth > 0) return fail(DPT_E_ARG, "unbounded pass arena overflow after growth");
         if ((rc = ensure_workspace(c, v, n_bytes, n_str, used))) return rc;
+        // without edge outputs only the strings the arena could not hold run again (a sub-batch,
+        // spliced in below); edge-recording calls (one string each from the drop-ins) rerun whole
+        if (!edges) {
+            overflow = true;
+            break;
+        }
     }
     const uint64_t total = p_idoff[n_str];
     if (total > ids_cap) return fail(DPT_E_CAP, "ids overflow");
@@ -574,6 +597,59 @@ static int encode_host_impl(dpt_ctx *c, const dpt_vocab *v, int mode, const uint
     if (total) memcpy(ids, c->p_out + o_ids, 4 * total);
     if (edges && n_bytes) memcpy(edges, c->p_out + o_edges, 8 * n_bytes);
     if (nf) memcpy(far, c->p_out + o_far, 16 * nf);
+    if (overflow) return rerun_too_long(c, v, mode, text, str_off, cut_mask, n_str, ids, ids_cap, id_off, status, capped_len);
+    return DPT_OK;
+}
+
+// After an arena overflow (the arena has since grown to what the pass claimed): the strings with
+// status DPT_STATUS_TOO_LONG -- exactly those the unbounded pass could not hold -- as one sub-batch,
+// their results spliced into the caller's CSR arrays.
+static int rerun_too_long(dpt_ctx *c, const dpt_vocab *v, int mode, const uint8_t *text, const uint64_t *str_off,
+                          const uint8_t *cut_mask, uint64_t n_str, int32_t *ids, uint64_t ids_cap, uint64_t *id_off,
+                          int32_t *status, int32_t *capped_len) {
+    std::vector<uint64_t> sel;
+    for (uint64_t i = 0; i < n_str; i++)
+        if (status[i] == DPT_STATUS_TOO_LONG) sel.push_back(i);
+    if (sel.empty()) return DPT_OK;
+    const uint64_t k = sel.size();
+    std::vector<uint64_t> soff(k + 1, 0);
+    for (uint64_t q = 0; q < k; q++) soff[q + 1] = soff[q] + (str_off[sel[q] + 1] - str_off[sel[q]]);
+    const uint64_t sb = soff[k];
+    const bool cut = (mode & DPT_MODE_MASK) != DPT_MODE_RAW;
+    std::vector<uint8_t> stext(sb ? sb : 1), scut(cut && sb ? sb : 1);
+    for (uint64_t q = 0; q < k; q++) {
+        const uint64_t a = str_off[sel[q]] - str_off[0], n = soff[q + 1] - soff[q];
+        if (n) memcpy(stext.data() + soff[q], text + a, n);
+        if (cut && n) memcpy(scut.data() + soff[q], cut_mask + a, n);
+    }
+    std::vector<int32_t> sids(sb ? sb : 1), sst(k), scap(k);
+    std::vector<uint64_t> sidoff(k + 1);
+    int rc = encode_host_impl(c, v, mode, stext.data(), sb, soff.data(), cut ? scut.data() : nullptr, k, sids.data(),
+                              sb ? sb : 1, sidoff.data(), sst.data(), capped_len ? scap.data() : nullptr, nullptr,
+                              nullptr, 0, nullptr, 1);
+    if (rc) return rc;
+    // splice: the overflowed strings had no ids; rebuild the CSR arrays around their new ones
+    const uint64_t total = id_off[n_str] + sidoff[k];
+    if (total > ids_cap) return fail(DPT_E_CAP, "ids overflow");
+    std::vector<int32_t> old(ids, ids + id_off[n_str]);
+    std::vector<uint64_t> old_off(id_off, id_off + n_str + 1);
+    uint64_t o = 0, q = 0;
+    for (uint64_t i = 0; i < n_str; i++) {
+        id_off[i] = o;
+        if (q < k && sel[q] == i) {
+            const uint64_t n = sidoff[q + 1] - sidoff[q];
+            if (n) memcpy(ids + o, sids.data() + sidoff[q], 4 * n);
+            o += n;
+            status[i] = sst[q];
+            if (capped_len) capped_len[i] = scap[q];
+            q++;
+        } else {
+            const uint64_t n = old_off[i + 1] - old_off[i];
+            if (n) memcpy(ids + o, old.data() + old_off[i], 4 * n);
+            o += n;
+        }
+    }
+    id_off[n_str] = o;
     return DPT_OK;
 }
 

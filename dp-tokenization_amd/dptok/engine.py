@@ -127,6 +127,98 @@ def pack_word_atoms(strings: Sequence[Sequence[Sequence[str]]]) -> Tuple[np.ndar
     return text, np.array(offs, dtype=np.uint64), cut
 
 
+def pack_presplit_words(strings: Sequence[Sequence[str]]):
+    """Strings given as lists of words -> DPT_MODE_PRESPLIT buffers (text u8, offsets u64[n+1], cut
+    mask u8 = 1 at every word's first byte) + per string its word count and the index of its first
+    empty word (-1: none; the string is cut there, see ``Encoder.encode_presplit``)."""
+    enc_words, n_words, cut_at = [], [], []
+    for words in strings:
+        k = next((i for i, w in enumerate(words) if not w), -1)
+        ws = words if k < 0 else words[:k]
+        enc_words.extend(encode_utf8(w) for w in ws)
+        n_words.append(len(ws))
+        cut_at.append(k)
+    wl = np.fromiter((len(e) for e in enc_words), dtype=np.uint64, count=len(enc_words))
+    wend = np.concatenate([np.zeros(1, np.uint64), np.cumsum(wl, dtype=np.uint64)])   # bytes of the first k words
+    offs = np.concatenate([np.zeros(1, np.uint64), wend[np.cumsum(np.asarray(n_words, dtype=np.int64))]]) \
+        if len(strings) else np.zeros(1, np.uint64)
+    raw = b"".join(enc_words)
+    cut = np.zeros(len(raw) + 1, dtype=np.uint8)
+    if len(wl):
+        cut[wend[:-1].astype(np.int64)] = 1   # every word's first byte
+    text = np.frombuffer(raw + b"\0", dtype=np.uint8)
+    return text, offs, cut, n_words, cut_at
+
+
+_WS_BYTES = "\u2581".encode("utf-8")
+
+
+class PieceTable:
+    """Per vocabulary id: the piece's UTF-8 bytes and whether it starts with '\u2581' -- llama mode's
+    host pre-tokenization (reference packages/tokenizer_utils.py:24-31: ids -> pieces through the
+    inverted vocabulary, then ``merge_tokens(sep='\u2581')`` :7-22) as array gathers over a whole
+    batch.  merge_tokens starts a word at the first piece and at every piece that starts with the
+    separator and appends every other piece to the current word, so a string's pre-split text is
+    the concatenation of its pieces' bytes, with a word start at the first piece and at each '\u2581'
+    piece -- the bytes and cut mask ``Encoder.encode_presplit`` builds from the merged words."""
+
+    def __init__(self, t2i: Dict[str, int]):
+        ids = np.fromiter(t2i.values(), dtype=np.int64, count=len(t2i))
+        n = int(ids.max()) + 1 if len(ids) else 0
+        # a dense table only (ids of get_vocab() are 0..|V|-1); negative or very sparse ids: unusable
+        self.ok = len(ids) > 0 and int(ids.min()) >= 0 and n <= 4 * len(ids) + 1024
+        if not self.ok:
+            return
+        inv = {}
+        for tok, i in t2i.items():   # the last token of a duplicated id wins, like {v: k for k, v in items}
+            inv[i] = tok
+        enc = [encode_utf8(inv[i]) if i in inv else b"" for i in range(n)]
+        self.present = np.zeros(n, dtype=bool)
+        self.present[list(inv.keys())] = True
+        self.plen = np.fromiter((len(e) for e in enc), dtype=np.int64, count=n)
+        self.poff = np.zeros(n, dtype=np.int64)
+        if n > 1:
+            self.poff[1:] = np.cumsum(self.plen[:-1])
+        self.blob = np.frombuffer(b"".join(enc) + b"\0", dtype=np.uint8)
+        self.ws = np.fromiter((e.startswith(_WS_BYTES) for e in enc), dtype=bool, count=n)
+        # merge_tokens of a list with an empty piece can yield an empty word (IndexError in the
+        # reference's DP): such a vocabulary takes the word-list path
+        self.empty_piece = bool((self.plen[self.present] == 0).any())
+
+    def pack(self, id_lists: Sequence[Sequence[int]]):
+        """Token ids per string -> (text u8, offsets u64[n+1], cut mask u8, pieces per string) for
+        DPT_MODE_PRESPLIT.  KeyError for an id outside the vocabulary (the reference's
+        ``vocab_bidict.inverse[token]``)."""
+        import itertools
+        n_str = len(id_lists)
+        cnt = np.fromiter((len(x) for x in id_lists), dtype=np.int64, count=n_str)
+        total = int(cnt.sum())
+        flat = np.fromiter(itertools.chain.from_iterable(id_lists), dtype=np.int64, count=total)
+        if total:
+            bad = (flat < 0) | (flat >= len(self.present))
+            bad[~bad] = ~self.present[flat[~bad]]
+            if bad.any():
+                raise KeyError(int(flat[np.argmax(bad)]))
+        plen = self.plen[flat]
+        pend = np.cumsum(plen)
+        pstart = pend - plen
+        nb = int(pend[-1]) if total else 0
+        # byte k of the batch comes from blob[poff[id] + (k - pstart)]
+        src = np.repeat(self.poff[flat] - pstart, plen) + np.arange(nb, dtype=np.int64)
+        text = np.empty(nb + 1, dtype=np.uint8)
+        text[:nb] = self.blob[src]
+        text[nb] = 0
+        first = np.zeros(total, dtype=bool)
+        send = np.cumsum(cnt)
+        first[(send - cnt)[cnt > 0]] = True   # every string's first piece opens its first word
+        cut = np.zeros(nb + 1, dtype=np.uint8)
+        cut[pstart[first | self.ws[flat]]] = 1
+        offs = np.zeros(n_str + 1, dtype=np.uint64)
+        if n_str:
+            offs[1:] = np.concatenate([[0], pend])[send]
+        return text, offs, cut, cnt
+
+
 class Encoder:
     """Batch shortest-tokenization on one GPU (one workspace; use from one stream at a time)."""
 
@@ -178,23 +270,8 @@ class Encoder:
         (tokenizer_utils.py:70-75): an empty word raises IndexError there (dp_tokenize.py:49)
         unless an earlier word already failed (no tokenization -> ValueError), so a string is cut
         at its first empty word and that word's status is decided by the prefix before it."""
-        enc_words, n_words, cut_at = [], [], []
-        for words in strings:
-            k = next((i for i, w in enumerate(words) if not w), -1)
-            ws = words if k < 0 else words[:k]
-            enc_words.extend(encode_utf8(w) for w in ws)
-            n_words.append(len(ws))
-            cut_at.append(k)
-        wl = np.fromiter((len(e) for e in enc_words), dtype=np.uint64, count=len(enc_words))
-        wend = np.concatenate([np.zeros(1, np.uint64), np.cumsum(wl, dtype=np.uint64)])   # bytes of the first k words
+        text, offs, cut, n_words, cut_at = pack_presplit_words(strings)
         n_str = len(strings)
-        offs = np.concatenate([np.zeros(1, np.uint64), wend[np.cumsum(np.asarray(n_words, dtype=np.int64))]]) \
-            if n_str else np.zeros(1, np.uint64)
-        raw = b"".join(enc_words)
-        cut = np.zeros(len(raw) + 1, dtype=np.uint8)
-        if len(wl):
-            cut[wend[:-1].astype(np.int64)] = 1   # every word's first byte
-        text = np.frombuffer(raw + b"\0", dtype=np.uint8)
         ids, id_off, st, _ = self.encode_csr(text, offs, mode="presplit", cut_mask=cut)
         flat = ids.tolist()
         o = id_off.tolist()
@@ -208,6 +285,17 @@ class Encoder:
             else:
                 out.append((flat[o[i]:o[i + 1]] if s == _lib.STATUS_OK else [], s))
         return out
+
+    def encode_packed_presplit(self, text: np.ndarray, offs: np.ndarray, cut: np.ndarray,
+                               n_pieces: np.ndarray) -> List[Tuple[List[int], int]]:
+        """``PieceTable.pack`` output in ONE launch: per string (ids, status); a string of no pieces
+        has no words (the reference's loop emits nothing, status 0).  Pieces are never empty here,
+        so no word is."""
+        ids, id_off, st, _ = self.encode_csr(text, offs, mode="presplit", cut_mask=cut)
+        flat, o, sl = ids.tolist(), id_off.tolist(), st.tolist()
+        none = (np.asarray(n_pieces) == 0).tolist()
+        return [([], _lib.STATUS_OK) if none[i] else ((flat[o[i]:o[i + 1]] if sl[i] == _lib.STATUS_OK else []), sl[i])
+                for i in range(len(offs) - 1)]
 
     def encode_words(self, words: Sequence[str]) -> Tuple[List[int], int]:
         """One string pre-split into words (llama mode, DPT_MODE_PRESPLIT): ids and status."""

@@ -211,6 +211,8 @@ def generate_parallel(kind: str, n: int, start: int = 0, procs: int = 8, **kw) -
     jobs = [(kind, min(step, n - s), start + s, kw) for s in range(0, n, step)]
     with mp.get_context("fork").Pool(len(jobs)) as pool:
         res = pool.map(_gen_chunk, jobs)
+        pool.close()   # workers exit on their own (leaving the block would terminate them)
+        pool.join()
     texts = [t for t, _ in res]
     lens = np.concatenate([np.diff(o) for _, o in res])
     offs = np.zeros(n + 1, dtype=np.uint64)
@@ -289,6 +291,8 @@ def bloom_like_parallel(n: int, vocab: Dict[str, int], start: int = 0, procs: in
     jobs = [(min(step, n - s), start + s, pool, kw) for s in range(0, n, step)]
     with mp.get_context("fork").Pool(len(jobs)) as p:
         res = p.map(_bloom_chunk, jobs)
+        p.close()
+        p.join()
     lens = np.concatenate([np.diff(o) for _, o, _ in res])
     offs = np.zeros(n + 1, dtype=np.uint64)
     offs[1:] = np.cumsum(lens, dtype=np.uint64)

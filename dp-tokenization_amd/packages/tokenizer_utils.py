@@ -29,6 +29,8 @@ if _HERE not in sys.path:
     sys.path.insert(0, _HERE)
 
 from dptok import Encoder, Vocab, raise_for_status  # noqa: E402
+from dptok.engine import PieceTable  # noqa: E402
+from dptok.hostpool import PretokenizePool  # noqa: E402
 
 SPACE_TOKEN = "▁"
 
@@ -96,6 +98,39 @@ def _device() -> int:
     return int(os.environ.get("LOCAL_RANK", "0"))
 
 
+def batch_encoder(tokenizer):
+    """``texts -> [tokenizer.encode(t) for t in texts]``, in one call of the Rust backend when the
+    tokenizer is a ``transformers`` tokenizers-backed class whose ``encode`` is the library's own:
+    that ``encode`` is ``_encode_plus`` over a one-text batch -- ``set_truncation_and_padding`` with
+    the default strategies, ``encode_special_tokens = split_special_tokens``, then
+    ``_tokenizer.encode_batch([text], add_special_tokens=True)`` -- so one ``encode_batch_fast``
+    over every text returns the same ids per text (tests/test_llama_sp.py checks it on every
+    fixture), with the backend's threads.  Any other tokenizer object: its ``encode``, per text."""
+    try:
+        from transformers.tokenization_utils_base import PreTrainedTokenizerBase
+        from transformers.tokenization_utils_tokenizers import TokenizersBackend
+        from transformers.utils import PaddingStrategy
+        from transformers.tokenization_utils_base import TruncationStrategy
+    except ImportError:
+        TokenizersBackend = None
+    if (TokenizersBackend is not None and isinstance(tokenizer, TokenizersBackend)
+            and type(tokenizer).encode is PreTrainedTokenizerBase.encode
+            and type(tokenizer)._encode_plus is TokenizersBackend._encode_plus
+            and hasattr(tokenizer._tokenizer, "encode_batch_fast")):
+        def encode_batch(texts):
+            pad, trunc, max_len, _ = tokenizer._get_padding_truncation_strategies(padding=False, truncation=None,
+                                                                                  max_length=None)
+            if pad != PaddingStrategy.DO_NOT_PAD or trunc != TruncationStrategy.DO_NOT_TRUNCATE:
+                return [tokenizer.encode(t) for t in texts]
+            tokenizer.set_truncation_and_padding(padding_strategy=pad, truncation_strategy=trunc, max_length=max_len,
+                                                 stride=0, pad_to_multiple_of=None, padding_side=None)
+            if tokenizer._tokenizer.encode_special_tokens != tokenizer.split_special_tokens:
+                tokenizer._tokenizer.encode_special_tokens = tokenizer.split_special_tokens
+            return [e.ids for e in tokenizer._tokenizer.encode_batch_fast(list(texts), add_special_tokens=True)]
+        return encode_batch
+    return lambda texts: [tokenizer.encode(t) for t in texts]
+
+
 def dp_tokenize_llama(llama_tokenizer, pretokenize_option="llama"):
     t2i: Dict[str, int] = dict(llama_tokenizer.get_vocab())
     vocab_bidict = _InverseDict(t2i)
@@ -113,13 +148,21 @@ def dp_tokenize_llama(llama_tokenizer, pretokenize_option="llama"):
             return out
     elif pretokenize_option == "llama":
         pretokenize = pretokenize_with_llama(llama_tokenizer, vocab_bidict)
+        pieces = PieceTable(t2i)
+        encode_ids = batch_encoder(llama_tokenizer)
+        host = PretokenizePool(llama_tokenizer, pieces, encode_ids)   # worker processes for large batches
 
         def encode_many(texts: Sequence[str]) -> List[List[int]]:
-            # SentencePiece runs on the host (third-party); the DP of every word of every text is
+            # SentencePiece runs on the host (third-party); the pieces -> words merge is array
+            # gathers over the whole batch (PieceTable), and the DP of every word of every text is
             # ONE pre-split launch
             texts = list(texts)
+            if pieces.ok and not pieces.empty_piece:
+                res = engine.encode_packed_presplit(*host.pack(texts))
+            else:
+                res = engine.encode_presplit([pretokenize(t) for t in texts])
             out = []
-            for t, (ids, st) in zip(texts, engine.encode_presplit([pretokenize(t) for t in texts])):
+            for t, (ids, st) in zip(texts, res):
                 raise_for_status(st, t)
                 out.append(ids)
             return out
@@ -136,6 +179,8 @@ def dp_tokenize_llama(llama_tokenizer, pretokenize_option="llama"):
 
     dp_tokenize.batch = encode_many
     dp_tokenize.engine = engine
+    if pretokenize_option == "llama":
+        dp_tokenize.host_pool = host
     return dp_tokenize, decode_dp_tokenization
 
 

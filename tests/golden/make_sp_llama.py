@@ -13,7 +13,7 @@
    with the stubs of make_golden.py.  Writes tests/golden/sp_llama_cases.json.gz: text, the
    tokenizer's ids, the merged words, the reference's ids / status (data only).
 
-Usage: python tests/golden/make_sp_llama.py [train] [cases]
+Usage: python tests/golden/make_sp_llama.py [train] [cases] [decode]
 """
 from __future__ import annotations
 
@@ -135,9 +135,37 @@ def cases():
     print(path, len(rows), "cases, statuses", st)
 
 
+def decode():
+    """Adds to every case the reference's own ``decode_dp_tokenization(ids)`` (the second closure of
+    ``dp_tokenize_llama``, packages/tokenizer_utils.py:82-84: ``llama_tokenizer.decode(ids)[4:]``),
+    over the recorded ids -- the round-trip surface of main_analyze_s2orc.py:84-87."""
+    sys.path.insert(0, HERE)
+    import make_golden  # noqa: F401  (stubs; the reference read-only)
+    from packages.tokenizer_utils import dp_tokenize_llama
+    import packages
+    assert packages.__file__.startswith("/root/reference"), packages.__file__
+    toks = {"hf": hf_llama(), "sp": SPLlama()}
+    dec = {k: dp_tokenize_llama(t, "llama")[1] for k, t in toks.items()}
+    path = os.path.join(HERE, "sp_llama_cases.json.gz")
+    with gzip.open(path, "rt", encoding="utf-8") as f:
+        out = json.load(f)
+    n = 0
+    for c in out["cases"]:
+        if c.get("skipped") or c["status"] != 0:
+            continue
+        c["decoded"] = dec[c["tokenizer"]](c["ids"])
+        n += 1
+    out["decode_source"] = "reference dp_tokenize_llama(tokenizer)[1] (packages/tokenizer_utils.py:82-84) over the ids"
+    with gzip.GzipFile(path, "wb", mtime=0) as f:
+        f.write(json.dumps(out, ensure_ascii=False).encode("utf-8"))
+    print(path, "decoded", n, "cases")
+
+
 if __name__ == "__main__":
-    steps = sys.argv[1:] or ["train", "cases"]
+    steps = sys.argv[1:] or ["train", "cases", "decode"]
     if "train" in steps:
         train()
     if "cases" in steps:
         cases()
+    if "decode" in steps:
+        decode()

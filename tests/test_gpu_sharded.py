@@ -1,0 +1,58 @@
+"""BASELINE configs[2] (cfg3) as the GPU suite runs it: bench.py's sharded path -- one corpus split
+across ranks by dptok.dist.shard_range, each rank tokenizing its shard on the GPU and checking it
+against the C oracle, ONE all-reduce of the token-count histogram per step.
+
+The box has one GPU, so the two-rank run shares it over gloo (the all-reduce then runs on the host;
+rank r uses device r mod 1); the RCCL all-reduce itself runs in a second child at world size 1 with
+DPT_BENCH_COLL=1 (bench.py's async nccl path: two histogram buffers, work.wait() on the encode
+stream).  Both are fresh child processes started with subprocess (never exec from a process that
+touched the GPU).  The reduced histograms must equal each other: the shards tile the corpus and the
+collective sums them.  Reference: words are independent DP problems,
+/root/reference/packages/tokenizer_utils.py:70.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+N = 20000
+
+
+def _bench_line(cmd, env, timeout=240):
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+    assert out.returncode == 0, (out.returncode, out.stderr[-4000:])
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]   # rank 0 prints ONE JSON line
+    return json.loads(lines[0])
+
+
+def _env(**kw):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "4"))
+    env.pop("DPT_BENCH_COLL", None)
+    env.update(kw)
+    return env
+
+
+@pytest.mark.timeout(600)
+def test_cfg3_two_gloo_ranks_match_one_rccl_rank():
+    args = ["--strings", str(N), "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
+    two = _bench_line([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                       "--master-addr=127.0.0.1", "--master-port=29561", "bench.py", "--gpus", "2",
+                       "--dist-backend", "gloo"] + args, _env())
+    one = _bench_line([sys.executable, "bench.py", "--gpus", "1"] + args,
+                      _env(DPT_BENCH_COLL="1", MASTER_PORT="29563"))
+    for line, world in ((two, 2), (one, 1)):
+        assert line["n_gpus"] == world and line["scaling"] == "strong"
+        assert line["config"]["strings_total"] == N
+        assert line["exact_match"]["rate"] == 1.0 and line["exact_match"]["sample"] == N
+        h = line["histogram"]
+        assert h["total_strings"] == N and h["status"][0] == N   # cfg2 strings all tokenize (status 0)
+    assert two["config"]["strings_per_gpu"] == N // 2
+    # the two-rank reduced histogram is the one-rank histogram of the whole corpus
+    assert two["histogram"] == one["histogram"]

@@ -41,6 +41,7 @@ def test_fixture_coverage(sp_cases):
     for kind in ("hf", "sp"):
         cs = _by_kind(sp_cases, kind)
         assert len(cs) >= 500
+        assert all(isinstance(c["decoded"], str) for c in cs)    # reference decode outputs (make_sp_llama.py decode)
         words = [w for c in cs for w in c["words"]]
         assert any("<0x" in w for w in words)                      # byte-fallback pieces
         assert any(w.strip("▁") == "" for w in words)             # '▁'-only pieces (whitespace runs)
@@ -68,15 +69,18 @@ def test_dp_tokenize_llama_real_sentencepiece(kind, sp_cases, tokenizers_):
     dp_tokenize, decode = dp_tokenize_llama(tokenizers_[kind])   # default pretokenize_option='llama'
     cs = _by_kind(sp_cases, kind)
     for c in cs[:120]:                                            # the unchanged callers' per-string call
-        assert dp_tokenize(c["text"]) == c["ids"], c["text"]
-    assert isinstance(decode(cs[30]["ids"]), str)
+        ids = dp_tokenize(c["text"])
+        assert ids == c["ids"], c["text"]
+        # the round trip of main_analyze_s2orc.py:84-87: the reference's own decode output
+        assert decode(ids) == c["decoded"], c["text"]
     eng = dp_tokenize.engine
     eng.profile(True)
-    got = dp_tokenize.batch([c["text"] for c in cs])
+    got = dp_tokenize.batch([c["text"] for c in cs] * 4)          # >= 2048 strings: the worker pool's path
     _, launches = eng.profile_read()
     eng.profile(False)
     assert launches == 1                                          # one pre-split launch for the batch
-    bad = [c["text"] for c, g in zip(cs, got) if g != c["ids"]]
+    assert dp_tokenize.host_pool._workers or dp_tokenize.host_pool._broken
+    bad = [c["text"] for c, g in zip(cs * 4, got) if g != c["ids"]]
     assert not bad, bad[:3]
 
 
@@ -93,3 +97,55 @@ def test_encode_presplit_empty_word_order():
     assert res[3] == ([0], STATUS_OK)
     assert res[4] == ([], STATUS_EMPTY_WORD)
     assert res[5] == ([0, 1, 2], STATUS_OK)
+
+
+@pytest.mark.parametrize("kind", ["hf", "sp"])
+def test_batched_host_pretokenization_equals_per_string(kind, sp_cases, tokenizers_):
+    """The drop-in's batched llama-mode host side (packages/tokenizer_utils.batch_encoder + the
+    array-gather PieceTable) gives, for every fixture text and a random ASCII / S2ORC-shaped sample,
+    the ids of per-string ``tokenizer.encode`` and the exact pre-split buffers the word lists of
+    ``pretokenize_with_llama`` + ``merge_tokens`` (reference tokenizer_utils.py:7-31) pack into."""
+    import numpy as np
+    from dptok import synth
+    from dptok.engine import PieceTable, pack_presplit_words
+    from packages.tokenizer_utils import _InverseDict, batch_encoder, pretokenize_with_llama
+    tok = tokenizers_[kind]
+    t2i = dict(tok.get_vocab())
+    texts = [c["text"] for c in _by_kind(sp_cases, kind)]
+    texts += synth.unpack(*synth.random_ascii_corpus(300, 256, seed=11))
+    texts += synth.unpack(*synth.s2orc_like_corpus(30, seed=12))
+    ids = batch_encoder(tok)(texts)
+    assert ids == [list(tok.encode(t)) for t in texts]
+    table = PieceTable(t2i)
+    assert table.ok and not table.empty_piece
+    text, offs, cut, cnt = table.pack(ids)
+    pre = pretokenize_with_llama(tok, _InverseDict(t2i))
+    words = [pre(t) for t in texts]
+    t2, o2, c2, nw, cut_at = pack_presplit_words(words)
+    assert all(k < 0 for k in cut_at)                   # no empty words
+    assert np.array_equal(offs, o2) and np.array_equal(text, t2) and np.array_equal(cut, c2)
+    assert np.array_equal(cnt > 0, np.asarray(nw) > 0)
+    with pytest.raises(KeyError):
+        table.pack([[1, 2], [len(table.present) + 5]])   # reference: vocab_bidict.inverse[token]
+
+
+@pytest.mark.parametrize("kind", ["hf", "sp"])
+def test_pretokenize_pool_equals_in_process(kind, tokenizers_):
+    """dptok.hostpool.PretokenizePool (worker processes, python -m dptok._pretok_worker) returns the
+    in-process buffers for a batch split into chunks, in order."""
+    import numpy as np
+    from dptok import synth
+    from dptok.engine import PieceTable
+    from dptok.hostpool import PretokenizePool
+    from packages.tokenizer_utils import batch_encoder
+    tok = tokenizers_[kind]
+    texts = synth.unpack(*synth.random_ascii_corpus(1500, 128, seed=13)) + ["", " ", "a\nb"] * 20
+    table, enc = PieceTable(dict(tok.get_vocab())), batch_encoder(tok)
+    ref = table.pack(enc(texts))
+    pool = PretokenizePool(tok, table, enc, procs=2, min_batch=1)
+    try:
+        got = pool.pack(texts)
+        assert pool._workers and not pool._broken          # the workers ran it
+        assert all(np.array_equal(a, b) for a, b in zip(got, ref))
+    finally:
+        pool.close()

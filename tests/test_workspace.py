@@ -63,7 +63,11 @@ def test_arena_overflow_host_path_reruns(vocabs):
     from dptok import Encoder, Vocab, pack_strings
     from oracle import oracle
     rng = np.random.default_rng(4)
-    texts = _long_batch(rng, n=30) + ["x y z"] * 5
+    # long strings interleaved with short ones: only the long ones overflow and run again, and
+    # their ids are spliced between the short strings' (dpt_api.cpp rerun_too_long)
+    texts = []
+    for k, t in enumerate(_long_batch(rng, n=30)):
+        texts += [t, "x y z" if k % 2 else "", " ab\ncd"]
     text, offs = pack_strings(texts)
     enc = Encoder(Vocab(vocabs["llama32k"], 0))
     got = enc.encode_csr(text, offs)
@@ -71,4 +75,28 @@ def test_arena_overflow_host_path_reruns(vocabs):
     for a, b in zip(got[:3], ref[:3]):
         assert np.array_equal(a, b)
     need, cap = enc.long_need()
-    assert need == 30 * 200_000 <= cap                   # grown to what the pass claimed
+    # the last call reran only the strings the default 4 MiB arena could not hold (20 of 30 fitted)
+    assert need == 10 * 200_000 <= cap
+
+
+def test_reserved_arena_is_not_resized_by_encode(vocabs):
+    """An explicitly reserved arena stays as reserved on the device path (no reallocation inside a
+    reserved call: capture-safe), even when the call's default would be larger."""
+    torch = pytest.importorskip("torch")
+    from dptok import Encoder, Vocab, synth
+    enc = Encoder(Vocab(vocabs["llama32k"], 0))
+    text, offs = synth.random_ascii_corpus(200_000, 256, seed=2)   # default arena: max(4 MiB, n_bytes/32) > 1 MiB
+    n, nb = len(offs) - 1, int(offs[-1])
+    enc.reserve(nb, n, long_bytes=1 << 20)
+    _, cap0 = enc.long_need()
+    dt = torch.from_numpy(text).cuda()
+    do = torch.from_numpy(offs.view(np.int64)).cuda()
+    ids = torch.empty(nb, dtype=torch.int32, device="cuda")
+    io = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    st = torch.empty(n, dtype=torch.int32, device="cuda")
+    enc.encode_device(dt.data_ptr(), nb, do.data_ptr(), n, ids.data_ptr(), nb, io.data_ptr(), st.data_ptr(),
+                      stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    need, cap1 = enc.long_need()
+    assert cap1 == cap0 and need == 0
+    assert (st.cpu().numpy() == 0).all()
