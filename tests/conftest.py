@@ -28,7 +28,7 @@ def load_golden(name):
 
 
 CORPUS_FIXTURES = ["edge_llama32k.json.gz", "edge_toy1k.json.gz", "cfg1_toy1k.json.gz",
-                   "cfg2_llama32k.json.gz", "cfg4_s2orc.json.gz", "cfg5_arabic.json.gz"]
+                   "cfg2_llama32k.json.gz", "cfg4_s2orc.json.gz", "cfg5_arabic.json.gz", "oov_llama32k.json.gz"]
 
 
 @pytest.fixture(scope="session")

@@ -3,6 +3,7 @@ fixtures produced by the reference itself (tests/golden/make_golden.py).
 
 CPU tests cover the host-side string utilities; ``gpu`` tests cover every DP-backed name."""
 import math
+import os
 
 import numpy as np
 import pytest
@@ -54,6 +55,29 @@ def test_inspect_obtain_token_compositions():
     merges = ["a b", "b c", "ab c"]
     assert it.obtain_token_compositions("abc", vocab, merges) == [["ab", "c"], ["a", "b", "c"]]
     assert it.obtain_token_compositions("a", vocab, merges) == [["a"]]
+
+
+def test_obtain_token_compositions_matches_reference():
+    """tests/golden/compositions.json.gz: the reference's own obtain_token_compositions
+    (inspect_tokenizer.py:17-42) over the synthetic BPEs' merges (make_compositions.py) -- every
+    token of the 1,800-entry BPE with its merges as a list, and tokens of 2..41 code points (and
+    non-tokens) of the 250,680-entry BPE with its merges as a set."""
+    import gzip
+    import json
+    import lzma
+    import inspect_tokenizer as it
+    from conftest import GOLDEN
+    g = load_golden("compositions.json.gz")
+    small = json.load(gzip.open(os.path.join(GOLDEN, "bloom_synth_tokenizer.json.gz"), "rt", encoding="utf-8"))
+    with lzma.open(os.path.join(GOLDEN, "bloom_big_tokenizer.json.xz"), "rt", encoding="utf-8") as fh:
+        big = json.load(fh)
+    merges = lambda m: [x if isinstance(x, str) else " ".join(x) for x in m]   # noqa: E731
+    src = {"small": (small["model"]["vocab"], merges(small["model"]["merges"])),
+           "big": (big["model"]["vocab"], set(merges(big["model"]["merges"])))}
+    assert len(g["cases"]) > 2000 and any(len(c["token"]) > 30 for c in g["cases"])
+    for c in g["cases"]:
+        v, m = src[c["source"]]
+        assert it.obtain_token_compositions(c["token"], v, m) == c["compositions"], c["token"]
 
 
 # ------------------------------------------------------------------ DP-backed names (GPU)
