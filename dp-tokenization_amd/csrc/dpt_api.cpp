@@ -23,6 +23,7 @@ struct dpt_vocab {
     int32_t root_base = 0;
     int32_t ws_node = -1, ws_base = 0, ws_id = -1;   // the trie node after U+2581 (-1: no such path)
     bool ids16 = false;               // every id in 0..32767: ids are staged as int16 (half the staging traffic)
+    uint32_t hash_buckets = 0, hash_probe = 0;   // C2's token hash table (0: none)
     dpt_vocab_stats stats{};
 };
 
@@ -176,6 +177,64 @@ int ensure_workspace(dpt_ctx *c, const dpt_vocab *v, uint64_t n_bytes, uint64_t 
 
 // First-pass kernel: 16-lane rows (4 strings per wave) when every token has <= 16 code points,
 // else 64-lane rows.  DPT_KERNEL=rows64 forces the 64-lane kernel (tests run it on the 32k vocab).
+// C2's token hash table (dpt_internal.h TokHashHeader + buckets of two {fp, id}) over the tokens of at
+// most TOKHASH_MAX_BYTES bytes, as uint32 words; {0, 0, 0, 0} (max_probe 0: no table) if no seed gives
+// every token an unambiguous lookup.  For a token of the last vocabulary entry of equal bytes wins,
+// like the trie (dpt_vocab.cpp).
+std::vector<uint32_t> build_token_hash(const uint8_t *blob, const uint64_t *off, const int32_t *ids, uint32_t n) {
+    struct Key { uint32_t w[4]; uint32_t len; int32_t id; };
+    std::vector<Key> keys;
+    keys.reserve(n);
+    for (uint32_t t = 0; t < n; t++) {
+        const uint64_t len = off[t + 1] - off[t];
+        if (len == 0 || len > dpt::TOKHASH_MAX_BYTES) continue;
+        Key k{{0, 0, 0, 0}, (uint32_t)len, ids ? ids[t] : (int32_t)t};
+        memcpy(k.w, blob + off[t], len);   // little-endian dwords, zero past the token
+        keys.push_back(k);
+    }
+    std::vector<uint32_t> none(4, 0u);
+    if (keys.empty()) return none;
+    uint32_t nb = 1;
+    while (nb < keys.size()) nb <<= 1;   // buckets of two entries: load <= 1/2
+    for (uint32_t seed = 0x2545F491u, tries = 0; tries < 8; tries++, seed = seed * 0x9E3779B9u + 0x7F4A7C15u) {
+        std::vector<uint32_t> tab(4 + (size_t)nb * 4, 0u);
+        uint32_t *bk = tab.data() + 4;
+        uint32_t max_probe = 0;
+        std::vector<std::pair<uint32_t, uint32_t>> where(keys.size());   // (bucket, slot) per key
+        bool bad = false;
+        for (size_t q = 0; q < keys.size() && !bad; q++) {
+            uint32_t h, fp;
+            dpt::tokhash(keys[q].w[0], keys[q].w[1], keys[q].w[2], keys[q].w[3], keys[q].len, seed, h, fp);
+            uint32_t b = h & (nb - 1), p = 1;
+            for (;; b = (b + 1) & (nb - 1), p++) {
+                uint32_t *e = bk + 4 * (size_t)b;
+                if (e[0] == fp || e[2] == fp) { bad = true; break; }   // an earlier key would answer for this one
+                if (!e[0]) { e[0] = fp; e[1] = (uint32_t)keys[q].id; where[q] = {b, 0}; break; }
+                if (!e[2]) { e[2] = fp; e[3] = (uint32_t)keys[q].id; where[q] = {b, 1}; break; }
+            }
+            max_probe = p > max_probe ? p : max_probe;
+        }
+        if (bad) continue;
+        // every key's lookup (the first entry of its fingerprint from its home bucket) is its own entry
+        for (size_t q = 0; q < keys.size() && !bad; q++) {
+            uint32_t h, fp;
+            dpt::tokhash(keys[q].w[0], keys[q].w[1], keys[q].w[2], keys[q].w[3], keys[q].len, seed, h, fp);
+            uint32_t b = h & (nb - 1);
+            for (uint32_t p = 0; p < max_probe; p++, b = (b + 1) & (nb - 1)) {
+                const uint32_t *e = bk + 4 * (size_t)b;
+                if (e[0] == fp) { bad = !(where[q].first == b && where[q].second == 0); break; }
+                if (e[2] == fp) { bad = !(where[q].first == b && where[q].second == 1); break; }
+            }
+        }
+        if (bad) continue;
+        tab[0] = nb - 1;
+        tab[1] = max_probe;
+        tab[2] = seed;
+        return tab;
+    }
+    return none;
+}
+
 int kernel_variant(uint32_t max_cp) {
     int v = max_cp <= 16 ? dpt::KERNEL_ROWS16 : dpt::KERNEL_ROWS64;
     if (const char *e = getenv("DPT_KERNEL"))
@@ -274,10 +333,15 @@ int dpt_vocab_create(const uint8_t *utf8_blob, const uint64_t *tok_off, const in
     if (e == hipSuccess) e = hipMalloc((void **)&v->d_ids, sizeof(int32_t) * da.n_slots);
     if (e == hipSuccess) e = hipMemcpy(v->d_slots, slots.data(), sizeof(int2) * slots.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(v->d_ids, da.id, sizeof(int32_t) * da.n_slots, hipMemcpyHostToDevice);
-    // one allocation, one kernel pointer (SGPRs are what the hot kernel spills): pair16, then a0
-    if (e == hipSuccess) e = hipMalloc((void **)&v->d_pair16, sizeof(int16_t) * dpt::PAIR16_N + sizeof(uint2) * a0.size());
+    // C2's token hash table (dpt_internal.h): header + buckets, after a0
+    std::vector<uint32_t> th = build_token_hash(utf8_blob, tok_off, ids, n_tok);
+    // one allocation, one kernel pointer (SGPRs are what the hot kernel spills): pair16, then a0, then the hash
+    if (e == hipSuccess) e = hipMalloc((void **)&v->d_pair16, dpt::TOKHASH_OFFSET + sizeof(uint32_t) * th.size());
     if (e == hipSuccess) e = hipMemcpy(v->d_pair16, pair16.data(), sizeof(int16_t) * pair16.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(v->d_pair16 + dpt::PAIR16_N, a0.data(), sizeof(uint2) * a0.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(reinterpret_cast<uint8_t *>(v->d_pair16) + dpt::TOKHASH_OFFSET, th.data(), sizeof(uint32_t) * th.size(), hipMemcpyHostToDevice);
+    v->hash_buckets = th[1] ? th[0] + 1 : 0;
+    v->hash_probe = th[1];
     if (e != hipSuccess) {
         dpt::free_double_array(&da);
         if (v->d_slots) (void)hipFree(v->d_slots);

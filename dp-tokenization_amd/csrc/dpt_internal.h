@@ -67,6 +67,41 @@ constexpr size_t CTR_ALLOC_BYTES = PART_CTR_OFFSET + (NPART_MAX + 1) * PART_STRI
 // low five bits inside each 32-byte block, so the 26 lowercase letters get distinct bits
 __host__ __device__ inline unsigned child_bit(unsigned b) { return (b ^ (b >> 5)) & 31u; }
 
+// Token hash table (C2's one-lookup ids for tokens of 3..16 expanded bytes; dpt_vocab_create builds
+// it after the A0 table in the pair16 allocation).  Key: the token's bytes as four little-endian
+// dwords, zero past its length, plus the length; bucket = h & mask, buckets of two {fp, id} entries
+// probed linearly; fp != 0 (0 marks a free entry).  The builder checks that every token's lookup
+// finds its own entry within `max_probe` buckets (else it re-seeds): a span the DP selected is a
+// vocabulary token by construction (phase A matched it), so the lookup needs no key compare.
+constexpr unsigned TOKHASH_MAX_BYTES = 16;
+constexpr size_t TOKHASH_OFFSET = PAIR16_N * sizeof(int16_t) + 65536 * 8;   // bytes into the pair16 allocation
+struct TokHashHeader {
+    uint32_t mask;        // buckets - 1 (a power of two)
+    uint32_t max_probe;   // buckets a lookup may visit (0: no table -- the walkers resolve every token)
+    uint32_t seed;
+    uint32_t pad;
+};
+__host__ __device__ inline uint32_t tokhash_rotl(uint32_t x, unsigned r) { return (x << r) | (x >> (32u - r)); }
+__host__ __device__ inline uint32_t tokhash_fmix(uint32_t h) {
+    h ^= h >> 16;
+    h *= 0x85EBCA6Bu;
+    h ^= h >> 13;
+    h *= 0xC2B2AE35u;
+    h ^= h >> 16;
+    return h;
+}
+// (h: the bucket hash, fp: the entry's fingerprint)
+__host__ __device__ inline void tokhash(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t len, uint32_t seed,
+                                        uint32_t &h, uint32_t &fp) {
+    uint32_t a = seed ^ (len * 0x9E3779B9u);
+    a = tokhash_rotl((a ^ w0) * 0xCC9E2D51u, 15);
+    a = tokhash_rotl((a ^ w1) * 0x1B873593u, 13);
+    a = tokhash_rotl((a ^ w2) * 0xCC9E2D51u, 15);
+    a = (a ^ w3) * 0x1B873593u;
+    h = tokhash_fmix(a);
+    fp = tokhash_fmix(h ^ 0x5BD1E995u) | 1u;
+}
+
 // kernel variants for the first pass (the 2048-byte window pass always follows for retries)
 constexpr int KERNEL_ROWS16 = 1;  // 4 strings per wave in 16-lane DPP rows, LDS windows (max_cp <= 16)
 constexpr int KERNEL_ROWS64 = 2;  // 1 string per wave, 64-lane DPP (max_cp <= 64)

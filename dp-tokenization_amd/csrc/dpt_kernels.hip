@@ -392,6 +392,56 @@ __device__ __forceinline__ uint64_t atom_from_info(const uint8_t *bytes, uint32_
     return seq;
 }
 
+// C2's hash key of the token of `nbytes` window bytes from p0 (dpt_internal.h tokhash): its expanded
+// bytes -- raw mode: the string's first atom is '\u2581' + its bytes, a leading ' ' is '\u2581' -- as
+// four little-endian dwords, zero past the expanded length E.  False (the walkers take the token) when
+// E > TOKHASH_MAX_BYTES or, in raw mode, a newline atom (expanded to "<0x0A>") is in the token.
+template <int CH>
+__device__ __forceinline__ bool token_key(const uint8_t *bytes, unsigned p0, unsigned nbytes, bool raw, unsigned first,
+                                          uint32_t (&w)[4], unsigned &E) {
+    const uint32_t *wp = reinterpret_cast<const uint32_t *>(bytes) + (p0 >> 2);
+    const unsigned sh = p0 & 3u;
+    // (reads up to 20 bytes past p0's dword: within the group's bytes, the next group or the slot states)
+    const uint32_t d0 = wp[0], d1 = wp[1], d2 = wp[2], d3 = wp[3], d4 = wp[4];
+    uint32_t r0 = __builtin_amdgcn_alignbyte(d1, d0, sh), r1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+    uint32_t r2 = __builtin_amdgcn_alignbyte(d3, d2, sh), r3 = __builtin_amdgcn_alignbyte(d4, d3, sh);
+    const unsigned b0 = r0 & 0xFFu;
+    const unsigned fi = raw ? first : 0u;
+    const unsigned sp = (raw ? 1u : 0u) & (fi ^ 1u) & (unsigned)(b0 == ' ');
+    E = nbytes + 3u * fi + 2u * sp;
+    if (E > TOKHASH_MAX_BYTES || nbytes == 0) return false;
+    // bytes [fi, nbytes) of the raw token must hold no '\n' (a non-first '\n' atom expands to 6 bytes)
+    auto keep = [](unsigned n, unsigned k) -> uint32_t {   // bytes of dword k below n
+        return n >= 4u * k + 4u ? 0xFFFFFFFFu : (n <= 4u * k ? 0u : (1u << (8u * (n - 4u * k))) - 1u);
+    };
+    if (raw) {
+        uint32_t nl = 0;
+        const uint32_t x[4] = {r0, r1, r2, r3};
+#pragma unroll
+        for (unsigned k = 0; k < 4; k++) {
+            // bytes outside [fi, nbytes) read as 0xFF (never '\n'); haszero over x ^ '\n'
+            uint32_t v = x[k] | ~keep(nbytes, k);
+            if (k == 0) v |= fi ? 0xFFu : 0u;
+            v ^= 0x0A0A0A0Au;
+            nl |= (v - 0x01010101u) & ~v & 0x80808080u;
+        }
+        if (nl) return false;
+        if (fi | sp) {
+            // '\u2581' (E2 96 81) in front: a first atom keeps its bytes (shift 3), a leading space
+            // becomes the 81 of the prefix (shift 2)
+            const uint32_t s0 = sp ? ((r0 & 0xFFFFFF00u) | 0x81u) : r0;
+            const uint32_t pm = fi ? 0x8196E200u : 0x96E20000u;
+            const unsigned as = fi ? 1u : 2u;
+            r3 = __builtin_amdgcn_alignbyte(r3, r2, as);
+            r2 = __builtin_amdgcn_alignbyte(r2, r1, as);
+            r1 = __builtin_amdgcn_alignbyte(r1, s0, as);
+            r0 = __builtin_amdgcn_alignbyte(s0, pm, as);
+        }
+    }
+    w[0] = r0 & keep(E, 0); w[1] = r1 & keep(E, 1); w[2] = r2 & keep(E, 2); w[3] = r3 & keep(E, 3);
+    return true;
+}
+
 // ------------------------------------------------------------------ prep: one slot's window
 
 // The bytes (and cut-mask bytes) of a window, in registers: lane l holds bytes
@@ -574,9 +624,38 @@ static_assert(NPART >= 1 && NPART <= NPART_MAX, "NPART");
 #ifndef WPE16
 #define WPE16 6
 #endif
+// The kernel's arguments, as one struct at the start of the kernarg segment
+struct KernArgs {
+    EncodeArgs ea;
+    TrieView tv;
+};
+typedef __attribute__((address_space(4))) const KernArgs ConstKernArgs;
+// Arguments are read through the kernarg segment pointer, which KREFRESH makes opaque at every phase
+// boundary: each phase then loads (s_load, scalar-cache hits) the few arguments it uses instead of
+// the compiler keeping all ~30 of them in SGPRs across the whole loop -- the hot kernel sits at the
+// SGPR limit and spills.
+#ifndef KARG_REFRESH
+#define KARG_REFRESH 1
+#endif
+// (a field-wise copy: only the fields a use reads are loaded)
+__device__ __forceinline__ TrieView tv_of(ConstKernArgs *kp) {
+    TrieView t;
+    t.slots = kp->tv.slots; t.ids = kp->tv.ids; t.slots4 = kp->tv.slots4;
+    t.root_base = kp->tv.root_base; t.n_slots = kp->tv.n_slots; t.pair16 = kp->tv.pair16;
+    return t;
+}
+#if KARG_REFRESH
+#define KREFRESH() asm volatile("" : "+s"(kp))
+#else
+#define KREFRESH() do { } while (0)
+#endif
+
 template <int CH, int G, bool BIG, bool WIDE, int SW = 0>   // SW: staged id width 0 = by a.staging16, 1 = int16, 2 = int32
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CH == 256 && G == 16) ? WPE16 : 1)))
-tokenize_kernel(EncodeArgs a, TrieView tv) {
+tokenize_kernel(KernArgs ka) {
+    ConstKernArgs *kp = (ConstKernArgs *)__builtin_amdgcn_kernarg_segment_ptr();
+#define a (kp->ea)
+#define tv (tv_of(kp))
     constexpr int NG = 64 / G;
     using GL = GroupLDS<CH, G>;
     using GR = Group<G>;
@@ -692,6 +771,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
     wave_sync();
 
     for (;;) {
+        KREFRESH();
         // ---------------------------------------------------------- slots: fetch strings, find windows, prep
         // Inactive slots are refilled together (one counter atomic, offsets loaded by one lane
         // per slot), and every slot's window bytes are loaded before any is atomised, so the
@@ -783,6 +863,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
         PRIO_PHASE(0);
 
         // ---------------------------------------------------------- A: match discovery (all slots)
+        KREFRESH();
 #if DPT_DOUBLE == 1
         for (int rep_ = 0; rep_ < 2; rep_++) {
             if (rep_) wave_sync();
@@ -829,6 +910,13 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
             auto end_token = [&](unsigned e, unsigned ln) {
                 uint32_t *r32 = reinterpret_cast<uint32_t *>(smem + lbase);
                 __hip_atomic_fetch_and(&r32[e], ~(1u << (15u + ln)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            };
+            auto end_token_at = [&](unsigned lb, unsigned e, unsigned ln) {   // (the group at LDS byte lb)
+                uint32_t *r32 = reinterpret_cast<uint32_t *>(smem + lb);
+                __hip_atomic_fetch_and(&r32[e], ~(1u << (15u + ln)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            };
+            auto grp_bytes_at = [&](unsigned lb, unsigned p) -> unsigned {   // window byte p (p < CH + 16) of that group
+                return reinterpret_cast<const GL *>(smem + lb)->bytes[p];
             };
             auto start_gj = [&](unsigned gs, unsigned jj) {
                 j = jj;
@@ -973,6 +1061,141 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                     }
                 }
             }
+#ifndef A_FAST
+#define A_FAST 1   // A/B knob: 0 = the generic walker takes A0's marked starts too
+#endif
+            // ASCII walker: the marked starts of A0 slots (pure-ASCII raw windows: an atom is one byte, a
+            // word start ' ' is '\u2581' = the trie node ws_node, '\n' is "<0x0A>", the string's first
+            // atom '\u2581' + its byte) walked byte by byte without the generic walker's atom
+            // descriptors.  A "more" start (a plain byte whose walk goes past A0's two-byte lookup, its one-
+            // and two-atom tokens already recorded by A0) repeats that lookup in the root table and goes on
+            // from the node after two bytes.  The generic walker below takes the other slots.
+            if constexpr (G == 16 && !BIG) {
+                if (A_FAST && a0mask) {
+                    unsigned fpre[NG + 1];
+                    fpre[0] = 0;
+#pragma unroll
+                    for (int g = 0; g < NG; g++) {
+                        fpre[g + 1] = fpre[g] + (((a0mask >> g) & 1u) ? nstart[g] : 0u);
+                        if ((a0mask >> g) & 1u) nstart[g] = 0;
+                    }
+                    const unsigned ftotal = fpre[NG];
+                    const int32_t wsn = a.ws_node, wsb = a.ws_base;
+                    const unsigned wst = a.ws_id >= 0 ? 1u : 0u;   // '\u2581' alone is a token
+                    const int32_t rb = tv.root_base;
+                    const unsigned nsl = tv.n_slots;
+                    constexpr uint64_t NL5 = 0x3E41307830ull;   // "0x0A>" after the '<'
+                    unsigned fj = 0, flen = 0, fp = 0, fwl = 0, cur = 0, pc = 0, fgs = 0, fl = 0, isr = 0, one = 0;
+                    uint64_t pend = 0;
+                    int32_t fnode = 0, fnb = 0, ft2 = 0;
+                    bool act = false;
+                    // a start: (walk state, or over at once -- the '\u2581' node missing / the word ends)
+                    auto fstart = [&](unsigned uu) -> bool {
+                        unsigned gs = 0;
+#pragma unroll
+                        for (int g = 1; g < NG; g++) gs += uu >= fpre[g] ? 1u : 0u;
+                        unsigned base = 0;
+#pragma unroll
+                        for (int g = 0; g < NG; g++) base = (gs == (unsigned)g) ? fpre[g] : base;
+                        fgs = gs;
+                        fl = gs * (unsigned)group_lds_bytes<CH, G>();
+                        const GL &L = *reinterpret_cast<const GL *>(smem + fl);
+                        const unsigned jj = L.fin[uu - base].v;
+                        fj = jj;
+                        fwl = SS[gs].wlen;
+                        const unsigned b0 = L.bytes[jj];
+                        isr = 0; one = 0; pc = 0; pend = 0;
+                        if (((fwmask >> gs) & 1u) && jj == 0) {   // '\u2581' + b0: one atom
+                            fnode = wsn; fnb = wsb; cur = b0; fp = 1; flen = 0;
+                            return wsn >= 0;
+                        }
+                        if (b0 == '\n') {
+                            fnode = 0; fnb = rb; cur = '<'; pend = NL5; pc = 5; fp = jj + 1; flen = 0;
+                            return true;
+                        }
+                        if (b0 != ' ') {   // a "more" start: the root table over (b0, next byte)
+                            const unsigned n1 = L.bytes[jj + 1];
+                            isr = 1; one = 1;
+                            if (n1 == '\n') {   // inside atom jj+1's "<0x0A>" after its '<'
+                                ft2 = (int32_t)(nsl + (b0 << 8) + (unsigned)'<');
+                                flen = 1; cur = '0'; pend = NL5 >> 8; pc = 4; fp = jj + 2;
+                            } else {             // two atoms; A0 saw a third that is no word start
+                                ft2 = (int32_t)(nsl + (b0 << 8) + n1);
+                                const unsigned n2 = L.bytes[jj + 2];
+                                flen = 2; fp = jj + 3;
+                                if (n2 == '\n') { cur = '<'; pend = NL5; pc = 5; }
+                                else cur = n2;
+                            }
+                            return true;
+                        }
+                        // a word start: the atom '\u2581' is the node ws_node
+                        if (wsn < 0) return false;
+                        fnode = wsn; fnb = wsb; flen = 1; one = wst;
+                        if (wst) end_token_at(fl, jj + 1, 1);
+                        if (jj + 1 >= fwl) return false;
+                        const unsigned n1 = L.bytes[jj + 1];
+                        if (n1 == ' ') return false;
+                        fp = jj + 2;
+                        if (n1 == '\n') { cur = '<'; pend = NL5; pc = 5; }
+                        else cur = n1;
+                        return true;
+                    };
+                    unsigned nxt = DPT_STOP == 21 ? ftotal : 0u;   // diagnostic: A0 only
+                    for (;;) {
+                        {
+                            const uint64_t im = ballot(!act);
+                            const unsigned nidle = (unsigned)__builtin_popcountll(im);
+                            if (nxt < ftotal && (nidle >= A_REFILL || ftotal - nxt <= nidle)) {
+                                if (!act) {
+                                    const unsigned uu = nxt + __builtin_amdgcn_mbcnt_hi((unsigned)(im >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)im, 0u));
+                                    if (uu < ftotal) {
+                                        act = fstart(uu);
+                                        if (!act && !one) SS[fgs].capb = 1;   // the start atom is no token
+                                    }
+                                }
+                                nxt += nidle;
+                            }
+                        }
+                        if (!ballot(act)) break;
+                        // the next raw byte, read before the trie load returns (masked off past the window)
+                        const unsigned nbv = grp_bytes_at(fl, fp);
+                        const int32_t t = isr ? ft2 : fnb + (int32_t)cur;
+                        const int4 ent = trie_slotA(tv, t);
+                        const unsigned y = (unsigned)ent.y;
+                        const unsigned av = act ? 1u : 0u;
+                        const unsigned ok = av & (isr ? (((y >> 30) & 1u) & (unsigned)((y & 0x3FFFFFFFu) != 0)) : (unsigned)(ent.y == fnode));
+                        fnode = isr ? (int32_t)(y & 0x3FFFFFFFu) : t;
+                        fnb = ent.x & BASE_MASK;
+                        const unsigned leaf = ((unsigned)ent.x >> 30) & 1u;
+                        // plain step: cur consumed; the atom ends unless its expansion has bytes left
+                        const unsigned aend = ok & (isr ^ 1u) & (unsigned)(pc == 0);
+                        const unsigned inexp = (isr ^ 1u) & (unsigned)(pc != 0);
+                        cur = inexp ? (unsigned)(pend & 0xFFu) : cur;
+                        pend = inexp ? pend >> 8 : pend;
+                        pc = inexp ? pc - 1u : pc;
+                        isr = 0;
+                        flen += aend;
+                        const unsigned term = aend & ((unsigned)ent.x >> 31);
+                        one |= term & (unsigned)(flen == 1);
+                        if (term) end_token_at(fl, fj + flen, flen);
+                        // the next atom (after an atom end): a byte of the word, "<0x0A>", or the end
+                        const unsigned past = (unsigned)(fp >= fwl) | (unsigned)(flen == 16u) | (unsigned)(nbv == ' ');
+                        const unsigned stop = aend & past;
+                        const unsigned nxa = aend & (past ^ 1u);
+                        const unsigned isnl = (unsigned)(nbv == '\n');
+                        cur = nxa ? (isnl ? (unsigned)'<' : nbv) : cur;
+                        pend = (nxa & isnl) ? NL5 : pend;
+                        pc = (nxa & isnl) ? 5u : pc;
+                        fp += nxa;
+                        const unsigned nochild = (((unsigned)ent.w >> child_bit(cur)) & 1u) ^ 1u;
+                        const unsigned done = av & ((ok ^ 1u) | leaf | stop | nochild);
+                        if (done) {
+                            if (!one) SS[fgs].capb = 1;
+                            act = false;
+                        }
+                    }
+                }
+            }
             unsigned pre[NG + 1];
             pre[0] = 0;
 #pragma unroll
@@ -1070,6 +1293,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
         PRIO_PHASE(1);
 
         // ---------------------------------------------------------- B: forward recurrence
+        KREFRESH();
         bool lane_mode = false;   // B ran per chunk and did C0 and C1 itself (G = 16, capless, no edges)
         if (DPT_RUN_B) {
             GL &L = grp(mg);
@@ -1450,6 +1674,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
         PRIO_PHASE(2);
 
         // ---------------------------------------------------------- C0: per-window token counts and validity
+        KREFRESH();
         // (word w ends at atom word_end(w); its final state is in fin[word_end(w)])
         if (DPT_RUN_B && !lane_mode) {
             unsigned pre[NG + 1];
@@ -1492,6 +1717,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
         wave_sync();
 
         // ---------------------------------------------------------- C1: selection, one lane per word
+        KREFRESH();
 #if DPT_DOUBLE == 3
         for (int rep_ = 0; rep_ < 2; rep_++) {
             if (rep_) wave_sync();
@@ -1555,6 +1781,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
         PRIO_PHASE(3);
 
         // ---------------------------------------------------------- C2: ids (lanes over all slots' tokens)
+        KREFRESH();
 #if DPT_DOUBLE == 4
         for (int rep_ = 0; rep_ < 2; rep_++) {
             if (rep_) wave_sync();
@@ -1610,8 +1837,70 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
 #endif
             static_assert(PEND_CAP >= 1 && PEND_CAP <= 64, "pending row");
             unsigned wbeg = 0, wend = total;
+            // the list of tokens left for the walkers: in the rec[].cpos halves (dead in C2) -- G = 16:
+            // entry i in group i / 256's rec[i % 256]; G = 64 (one slot): rec[i]
             auto list_ref = [&](unsigned i) -> uint16_t & {
-                return *reinterpret_cast<uint16_t *>(smem + (i >> 8) * (unsigned)group_lds_bytes<CH, G>() + (i & 255u) * 4u);
+                if constexpr (G == 16)
+                    return *reinterpret_cast<uint16_t *>(smem + (i >> 8) * (unsigned)group_lds_bytes<CH, G>() + (i & 255u) * 4u);
+                else
+                    return grp(0).rec[i].cpos;
+            };
+#ifndef C2_HASH
+#define C2_HASH 1   // A/B knob: 0 = every token the bulk pass leaves goes to the walkers
+#endif
+            // hash pass over n tokens (token number of entry i: src(i)): a token of at most
+            // TOKHASH_MAX_BYTES expanded bytes without a newline atom gets its id from ONE bucket load
+            // of the token hash table (dpt_internal.h); the others are listed, in order, at the front of
+            // the list for the walkers.  Returns their number (n without a table).
+            auto hash_pass = [&](unsigned n, auto src) -> unsigned {
+                const uint8_t *hbase = reinterpret_cast<const uint8_t *>(tv.pair16) + TOKHASH_OFFSET;
+                const TokHashHeader hh = *reinterpret_cast<const TokHashHeader *>(hbase);
+                if (!C2_HASH || !hh.max_probe) {
+                    for (unsigned i = lane; i < n; i += 64u) list_ref(i) = (uint16_t)src(i);
+                    return n;
+                }
+                const __amdgpu_buffer_rsrc_t hr = __builtin_amdgcn_make_buffer_rsrc(
+                    (void *)(hbase + sizeof(TokHashHeader)), (short)0, (int)((hh.mask + 1u) * 16u), 0x00020000);
+                unsigned r2 = 0;
+                for (unsigned i0 = 0; i0 < n; i0 += 64u) {
+                    const unsigned i = i0 + lane;
+                    const bool in = i < n;
+                    const unsigned t = in ? src(i) : 0u;
+                    unsigned g = 0;
+#pragma unroll
+                    for (int k = 1; k < NG; k++) g += t >= pre[k] ? 1u : 0u;
+                    const GL &L = *reinterpret_cast<const GL *>(smem + g * (unsigned)group_lds_bytes<CH, G>());
+                    const C2Slot q = *reinterpret_cast<const C2Slot *>(&L.fin[0]);
+                    const unsigned k = in ? t - q.base : 0u;
+                    const unsigned jj = (unsigned)L.rec[k].smask;
+                    const unsigned nx = (unsigned)L.rec[k + 1].smask;   // k + 1 <= ntk < NA
+                    const unsigned j1 = k + 1 < q.ntk ? nx : q.na;
+                    const unsigned p0 = L.aoff[jj];
+                    const unsigned nbytes = (typename GL::Idx)(L.aoff[j1] - p0);
+                    uint32_t w[4];
+                    unsigned E = 0;
+                    const bool hashed = in && token_key<CH>(L.bytes, p0, nbytes, raw, (raw ? 1u : 0u) & q.fw & (unsigned)(jj == 0), w, E);
+                    if (hashed) {
+                        uint32_t h, fp;
+                        tokhash(w[0], w[1], w[2], w[3], E, hh.seed, h, fp);
+                        int32_t idv = -1;
+                        unsigned b = h & hh.mask;
+                        for (unsigned pr = 0; pr < hh.max_probe; pr++) {
+                            const auto e = __builtin_amdgcn_raw_buffer_load_b128(hr, b * 16u, 0, 0);
+                            if (e[0] == fp) { idv = (int32_t)e[1]; break; }
+                            if (e[2] == fp) { idv = (int32_t)e[3]; break; }
+                            b = (b + 1u) & hh.mask;
+                        }
+                        if (n16) a.staging16[q.ob + k] = (int16_t)idv;
+                        else a.staging[q.ob + k] = idv;
+                    }
+                    // every lane read its entry above (a list source): the compacted rest lands below i0 + 64
+                    const bool rest = in && !hashed;
+                    const uint64_t m = ballot(rest);
+                    if (rest) list_ref(r2 + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u))) = (uint16_t)t;
+                    r2 += (unsigned)__builtin_popcountll(m);
+                }
+                return r2;
             };
             if constexpr (BULK) {
                 const bool i16 = n16;
@@ -1678,6 +1967,10 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                     }
                 }
                 wave_sync();
+                if (r > 0) {
+                    r = hash_pass(r, [&](unsigned i) -> unsigned { return list_ref(i); });
+                    wave_sync();
+                }
                 wend = r;
                 if (r > 0 && r < (unsigned)PEND_CAP) {
                     uint4 ent = make_uint4(0u, 0u, 0u, 0u);
@@ -1712,10 +2005,13 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
                     }
                 }
             }
-            auto tok_at = [&](unsigned i) -> unsigned {
-                if constexpr (BULK) return list_ref(i);
-                else return i;
-            };
+            if constexpr (!BULK) {   // the walkers take what the hash pass leaves
+                if (total > 0) {
+                    wend = hash_pass(total, [](unsigned i) -> unsigned { return i; });
+                    wave_sync();
+                }
+            }
+            auto tok_at = [&](unsigned i) -> unsigned { return list_ref(i); };
             // One token walk per lane; a lane whose token is resolved writes the id and takes the
             // next token (ballot + mbcnt), so each iteration is one trie step for 64 tokens.  A
             // token's bytes do not depend on the trie, so each iteration issues the trie load
@@ -1813,6 +2109,7 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
         wave_sync();
 
         // ---------------------------------------------------------- advance slots, finish strings
+        KREFRESH();
         if (lane < (unsigned)NG) {
             SlotState &S = SS[lane];
             if (S.active && S.n_atoms > 0 && S.status == 0 && (S.inval & 2)) {
@@ -1843,6 +2140,8 @@ tokenize_kernel(EncodeArgs a, TrieView tv) {
     if constexpr (G == 16 && !BIG)
         if (n_pend) walk_pending(n_pend);
     STAMP_FLUSH;
+#undef a
+#undef tv
 }
 
 // ------------------------------------------------------------------ compaction
@@ -2124,7 +2423,7 @@ static void launch_tok(const EncodeArgs &a, const TrieView &tv, uint64_t n_units
     uint64_t blocks = (uint64_t)n_cu * wpc;
     if (blocks > (uint64_t)n_cu * 64u) blocks = (uint64_t)n_cu * 64u;   // the scratch is sized for 64 per CU
     if (blocks > n_units) blocks = n_units ? n_units : 1;
-    hipLaunchKernelGGL((tokenize_kernel<CH, G, BIG, WIDE, SW>), dim3((unsigned)blocks), dim3(64), lds, stream, a, tv);
+    hipLaunchKernelGGL((tokenize_kernel<CH, G, BIG, WIDE, SW>), dim3((unsigned)blocks), dim3(64), lds, stream, KernArgs{a, tv});
 }
 
 hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t ev[2]) {

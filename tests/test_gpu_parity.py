@@ -343,6 +343,46 @@ def test_ascii_windows_phase_a0(engines, oracles):
         assert np.array_equal(got[3], ref[3])
 
 
+@pytest.mark.parametrize("seed", [31, 32])
+def test_ascii_walker_and_token_hash(seed):
+    """Phase A's ASCII walker (A0 slots: word starts from the '\u2581' node, the string's first atom,
+    "<0x0A>" expansions at a walk's start and inside it, walks going on past A0's two-byte lookup) and
+    C2's token hash (tokens of 3..16 expanded bytes with a '\u2581' prefix from a space or from the
+    first atom; tokens with a newline atom and longer ones left to the walkers) on a vocabulary of
+    long letter tokens and newline-bearing tokens, over multi-window strings, against the C oracle.
+    Seed 32 leaves '\u2581' itself out of the vocabulary (a word start is then no token)."""
+    from dptok import Encoder, Vocab, pack_strings
+    from oracle import oracle
+    rng = np.random.default_rng(seed)
+    letters = "etaoinsh"
+    vocab = set(letters) | {"\u2581" + c for c in letters} | {"<0x0A>", "\n"}
+    if seed == 31:
+        vocab.add("\u2581")
+    for _ in range(3000):
+        L = int(rng.integers(2, 17))
+        w = "".join(rng.choice(list(letters), size=L))
+        r = rng.random()
+        if r < 0.3:
+            w = "\u2581" + w[:15]
+        elif r < 0.4:
+            k = int(rng.integers(0, len(w)))
+            w = (w[:k] + "<0x0A>" + w[k:])[:16]
+        vocab.add(w)
+    vocab = sorted(vocab)
+    t2i = {t: i for i, t in enumerate(vocab)}
+    texts = []
+    for k in range(2500):
+        n = int(rng.integers(1, 700))
+        ch = rng.choice(list(letters) + [" "] * 2 + ["\n"] * (1 if k % 3 else 0), size=n)
+        texts.append("".join(ch))
+    texts += ["\n" + "etao" * 50, " " + "e" * 300, "\n\n\n", "e\ne\ne", " \nabc"]
+    text, offs = pack_strings(texts)
+    got = Encoder(Vocab(t2i, 0)).encode_csr(text, offs)
+    ref = oracle.OracleVocab(t2i).encode_csr(text, offs)
+    _cmp_csr(got, ref)
+    assert np.array_equal(got[3], ref[3])
+
+
 @pytest.mark.parametrize("shift", [40000, "edge"])
 def test_staging_width_by_id_range(shift, vocabs):
     """Ids are staged as int16 when every id is in 0..32767 (the llama-shaped vocabularies) and as

@@ -6,6 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 tag=$1; N=${2:-1000000}; GEN=${3:-ascii}
 out=gpurun_out/pmc_$tag; mkdir -p $out
+[ "$GEN" != ascii ] && { timeout -k 10 300 python3 tools/prof_driver.py $N 1 $GEN gen-only || exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace -o run --output-format csv -- python3 tools/prof_driver.py $N 3 $GEN > $out/trace.log 2>&1 || exit 1
 i=0
 for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \

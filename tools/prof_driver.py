@@ -3,18 +3,28 @@ import os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "dp-tokenization_amd")]
 import numpy as np
-import torch
-from dptok import Encoder, Vocab, synth
+from dptok import synth
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 gen = sys.argv[3] if len(sys.argv) > 3 else "ascii"
-enc = Encoder(Vocab(synth.llama_shaped_vocab(), 0))
-if gen == "ascii":
+# generated corpora are cached in /tmp (one GPU call runs this driver many times)
+cache = "/tmp/dpt_corpus_%s_%d.npz" % (gen, n)
+if gen != "ascii" and os.path.exists(cache):
+    z = np.load(cache)
+    text, offs = z["text"], z["offs"]
+elif gen == "ascii":
     text, offs = synth.random_ascii_corpus(n, 256, seed=1)
-elif gen == "s2orc":
-    text, offs = synth.s2orc_like_corpus(n, seed=4)
 else:
-    text, offs = synth.arabic_corpus(n, 256, seed=5)
+    # (forks: only in the gen-only run, which no profiler wraps)
+    procs = 16 if (len(sys.argv) > 4 and sys.argv[4] == "gen-only") else 1
+    text, offs = synth.generate_parallel("s2orc" if gen == "s2orc" else "arabic", n, procs=procs,
+                                         **({"seed": 4} if gen == "s2orc" else {"length": 256, "seed": 5}))
+    np.savez(cache, text=text, offs=offs)
+if len(sys.argv) > 4 and sys.argv[4] == "gen-only":   # run without a profiler first: the forks happen here
+    sys.exit(0)
+import torch  # noqa: E402
+from dptok import Encoder, Vocab  # noqa: E402
+enc = Encoder(Vocab(synth.llama_shaped_vocab(), 0))
 dev = torch.device("cuda", 0)
 dt = torch.from_numpy(text).to(dev); do = torch.from_numpy(offs.view(np.int64)).to(dev)
 nb = len(text)
