@@ -376,14 +376,15 @@ def main():
         b = n_step[0] % 2
         n_step[0] += 1
         h = d_hists[b]
-        enc.encode_device(d_text.data_ptr(), n_bytes, d_off.data_ptr(), M, d_ids.data_ptr(), max(n_bytes, 1),
-                          d_idoff.data_ptr(), d_status.data_ptr(), stream=stream,
-                          cut_ptr=d_cut.data_ptr() if bloom else 0, mode="atoms" if bloom else "raw")
         if pending[b] is not None:   # the stream waits for this buffer's previous all-reduce
             pending[b].wait()
             pending[b] = None
         h.zero_()
-        enc.histogram_device(d_idoff.data_ptr(), d_status.data_ptr(), M, h.data_ptr(), N_BINS, stream=stream)
+        # the histogram is folded into the encode's finish pass (dpt_ctx_set_histogram)
+        enc.set_histogram(h.data_ptr(), N_BINS)
+        enc.encode_device(d_text.data_ptr(), n_bytes, d_off.data_ptr(), M, d_ids.data_ptr(), max(n_bytes, 1),
+                          d_idoff.data_ptr(), d_status.data_ptr(), stream=stream,
+                          cut_ptr=d_cut.data_ptr() if bloom else 0, mode="atoms" if bloom else "raw")
         if coll:   # the single collective: RCCL over xGMI with nccl, gloo in rehearsals
             if red_dev.type == "cpu":
                 hc = h.cpu()

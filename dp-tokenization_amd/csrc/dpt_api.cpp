@@ -51,6 +51,9 @@ struct dpt_ctx {
     // counters | ids | edges), each mirrored by a pinned host buffer so every copy is one async DMA
     uint8_t *d_in = nullptr, *p_in = nullptr, *d_out = nullptr, *p_out = nullptr;
     uint64_t cap_in = 0, cap_pin_in = 0, cap_out = 0, cap_pin_out = 0;
+    // dpt_ctx_set_histogram: folded into the next encode's finish pass
+    int64_t *hist = nullptr;
+    uint32_t hist_bins = 0;
     // profiling
     bool profile = false;
     std::vector<hipEvent_t> events;   // groups of 4 per call
@@ -508,6 +511,9 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
     p.staging16 = v->ids16 ? c->staging16 : nullptr;
     p.padded = padded;
     p.pend = c->pend;
+    p.hist = padded ? nullptr : c->hist;   // (dpt_encode_padded has no offsets to count)
+    p.hist_bins = c->hist_bins;
+    c->hist = nullptr;                     // one call only
     if (padded) {   // the ids go straight to their final place (int32), the counts to the caller's array
         p.staging = ids;
         p.staging16 = nullptr;
@@ -757,6 +763,14 @@ int dpt_token_histogram(const uint64_t *id_off, const int32_t *status, uint64_t 
     if (!id_off || !hist || (n_str && !status) || n_bins < 2) return fail(DPT_E_ARG, "bad histogram arguments");
     hipError_t e = dpt::launch_histogram(id_off, status, n_str, hist, n_bins, (hipStream_t)hip_stream);
     if (e != hipSuccess) return hip_fail(e, "histogram launch");
+    return DPT_OK;
+}
+
+int dpt_ctx_set_histogram(dpt_ctx *c, int64_t *hist, uint32_t n_bins) {
+    if (!c) return fail(DPT_E_ARG, "null ctx");
+    if (hist && n_bins < 2) return fail(DPT_E_ARG, "n_bins < 2");
+    c->hist = hist;
+    c->hist_bins = hist ? n_bins : 0;
     return DPT_OK;
 }
 

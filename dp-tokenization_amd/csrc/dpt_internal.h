@@ -37,6 +37,8 @@ struct EncodeLaunch {
     int variant;             // KERNEL_* below
     bool padded;             // dpt_encode_padded: staging = the caller's ids, counts = the caller's; no finish pass
     uint4 *pend;             // 16-lane first pass: each wave's pending residual tokens (pend_scratch_bytes)
+    int64_t *hist;           // nullable: the token-count histogram to add to in the finish pass (dpt_ctx_set_histogram)
+    uint32_t hist_bins;
     uint8_t *arena;          // the unbounded pass's scratch: 20 bytes per input byte of the strings it takes
     uint64_t arena_cap;      // input bytes the arena holds
     // vocabulary
@@ -60,6 +62,7 @@ constexpr unsigned PAIR16_N = 65536 + 256;
 // strings per finish batch (the batch arrays are sized one per 64 strings, two arrays)
 constexpr unsigned FIN_BATCH = 256;
 constexpr unsigned PART_STRIDE = 64;
+constexpr unsigned FIN_MAX_BINS = 1024;   // histogram bins the finish pass folds in (more: the separate pass)
 constexpr size_t PART_CTR_OFFSET = 256;
 constexpr size_t CTR_ALLOC_BYTES = PART_CTR_OFFSET + (NPART_MAX + 1) * PART_STRIDE * 4;
 

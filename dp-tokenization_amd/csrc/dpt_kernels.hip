@@ -645,7 +645,8 @@ __device__ __forceinline__ TrieView tv_of(ConstKernArgs *kp) {
     return t;
 }
 #if KARG_REFRESH
-#define KREFRESH() asm volatile("" : "+s"(kp))
+// (the 16-lane instantiations: the 64-lane ones do not spill, and measured 1.7 % slower with it)
+#define KREFRESH() do { if constexpr (G == 16) asm volatile("" : "+s"(kp)); } while (0)
 #else
 #define KREFRESH() do { } while (0)
 #endif
@@ -1156,7 +1157,11 @@ tokenize_kernel(KernArgs ka) {
                                 nxt += nidle;
                             }
                         }
-                        if (!ballot(act)) break;
+                        // (a start can be over at once, so a refill may leave every lane idle with starts left)
+                        if (!ballot(act)) {
+                            if (nxt >= ftotal) break;
+                            continue;
+                        }
                         // the next raw byte, read before the trie load returns (masked off past the window)
                         const unsigned nbv = grp_bytes_at(fl, fp);
                         const int32_t t = isr ? ft2 : fnb + (int32_t)cur;
@@ -1480,17 +1485,36 @@ tokenize_kernel(KernArgs ka) {
                         unsigned best = relax(sprev, cpi - cprev);   // j = i-1: the single atom
                         unsigned dg = 0, de = 0;
                         unsigned m = (~r >> 17) & 0x7FFFu;          // longer tokens ending at i: bit d-1
+#ifndef B_PAIR
+#define B_PAIR 0   // A/B knob: candidates per inner iteration taken two at a time (both LDS reads in flight):
+                   // cfg4 +0.9 %, cfg2 -0.9 % (profiles/r03_ab.log)
+#endif
                         while (m) {
                             const unsigned dd = ffbl(m) + 1u;
                             m &= m - 1u;
                             const unsigned j = i - 1u - dd;          // j >= ws: spans cross no cut
                             const unsigned rj = rec32[j];
+                            unsigned dd2 = dd, rj2 = 0;
+                            const bool two = B_PAIR && m != 0;
+                            if (B_PAIR) {
+                                dd2 = two ? ffbl(m) + 1u : dd;
+                                m &= two ? m - 1u : m;
+                                rj2 = rec32[i - 1u - dd2];           // (dd2 = dd when there is no second: read again, unused)
+                            }
                             const unsigned sj = j == ws ? FRESH : (rj >> 16);
                             const unsigned kk = relax(sj, cpi - (rj & 0x7FFu));
                             // ascending d = descending j: the first strict improvement is the largest j
                             if ((kk >> 5) < (best >> 5)) de = dd;
                             if (kk < best) dg = dd;
                             best = kk < best ? kk : best;
+                            if (B_PAIR) {
+                                const unsigned j2 = i - 1u - dd2;
+                                const unsigned sj2 = j2 == ws ? FRESH : (rj2 >> 16);
+                                const unsigned kk2 = two ? relax(sj2, cpi - (rj2 & 0x7FFu)) : 0xFFFFFFFFu;
+                                if ((kk2 >> 5) < (best >> 5)) de = dd2;
+                                if (kk2 < best) dg = dd2;
+                                best = kk2 < best ? kk2 : best;
+                            }
                         }
                         L.rec[i].smask = (uint16_t)best;   // this end's mask was read above
                         L.fin[i].v = (uint8_t)(dg | (de << 4));
@@ -1855,7 +1879,7 @@ tokenize_kernel(KernArgs ka) {
             auto hash_pass = [&](unsigned n, auto src) -> unsigned {
                 const uint8_t *hbase = reinterpret_cast<const uint8_t *>(tv.pair16) + TOKHASH_OFFSET;
                 const TokHashHeader hh = *reinterpret_cast<const TokHashHeader *>(hbase);
-                if (!C2_HASH || !hh.max_probe) {
+                if (!C2_HASH || !hh.max_probe || G != 16) {   // 64-lane rows: the walkers (BLOOM-scale: -3.5 % with it)
                     for (unsigned i = lane; i < n; i += 64u) list_ref(i) = (uint16_t)src(i);
                     return n;
                 }
@@ -2252,6 +2276,9 @@ struct FinishArgs {
     unsigned slices;                  // blocks per batch
     unsigned long long *bsum;         // one-batch calls (no scan kernel): zeroed here ...
     uint32_t *ctr;                    // ... and the counter block reset here (both null otherwise)
+    unsigned long long *hist;         // nullable: the token-count histogram (dpt_ctx_set_histogram) ...
+    const int32_t *status;            // ... with the statuses it counts
+    uint32_t n_bins;
 };
 
 // CSR offsets and ids: block b takes slice b % slices of batch b / slices.  One count per thread of
@@ -2285,6 +2312,33 @@ __global__ void __launch_bounds__(FIN_THREADS) finish_kernel(FinishArgs f) {
     }
     if (tid == FIN_BATCH - 1) s_rel[FIN_BATCH] = incl;
     __syncthreads();
+    if (f.hist && sl == 0) {
+        // the batch's histogram (dpt_token_histogram's layout) in LDS, added to the global one once:
+        // one LDS atomic per string for its count bin, the statuses and totals by ballots
+        __shared__ unsigned long long lh[FIN_MAX_BINS + 8];
+        const uint32_t nbh = f.n_bins + 8;
+        for (uint32_t b = tid; b < nbh; b += FIN_THREADS) lh[b] = 0;
+        __syncthreads();
+        int32_t st = -1;
+        if (has) {
+            atomicAdd(&lh[c < f.n_bins - 1 ? (uint32_t)c : f.n_bins - 1], 1ull);
+            st = f.status[s0 + tid];
+            st = st >= 0 && st <= 4 ? st : 4;
+        }
+        const unsigned lanei = tid & 63u;
+#pragma unroll
+        for (int v = 0; v < 5; v++) {
+            const uint64_t m = __ballot(st == v);
+            if (lanei == 0 && m) atomicAdd(&lh[f.n_bins + 2 + v], (unsigned long long)__builtin_popcountll(m));
+        }
+        if (tid == 0) {
+            lh[f.n_bins] += total;   // (the block scan's sum: the batch's ids)
+            lh[f.n_bins + 1] += (unsigned long long)(f.n_str - s0 < FIN_BATCH ? f.n_str - s0 : FIN_BATCH);
+        }
+        __syncthreads();
+        for (uint32_t b = tid; b < nbh; b += FIN_THREADS)
+            if (lh[b]) atomicAdd(&f.hist[b], lh[b]);
+    }
     if (sl == 0) {
         if (has) f.id_off[s0 + tid + 1] = o0 + incl;
         if (t == 0 && tid == 0) {
@@ -2477,8 +2531,14 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
         EncodeArgs b = a;
         b.work_list = p.retry_list; b.work_count = p.retry_count;
         b.work_next = p.retry_count + 2;
-        if (wide) launch_tok<BIG_CH, 64, true, true>(b, tv, p.n_str, p.max_blocks / 64, stream);
-        else launch_tok<BIG_CH, 64, true, false>(b, tv, p.n_str, p.max_blocks / 64, stream);
+#ifndef FALLBACK_DIV
+#define FALLBACK_DIV 4   // the fallback passes' grids: 1/FALLBACK_DIV of a full one (usually they find no work)
+#endif
+        // (n_units caps the grid: one block per FALLBACK_DIV CUs; the retry list is rare and short)
+        uint64_t fb_units = (uint64_t)(p.max_blocks / 64) / FALLBACK_DIV;
+        fb_units = fb_units < p.n_str ? fb_units : p.n_str;
+        if (wide) launch_tok<BIG_CH, 64, true, true>(b, tv, fb_units ? fb_units : 1, p.max_blocks / 64, stream);
+        else launch_tok<BIG_CH, 64, true, false>(b, tv, fb_units ? fb_units : 1, p.max_blocks / 64, stream);
         // the unbounded pass over whatever the windowed passes could not hold (usually nothing:
         // its waves read a zero count and exit)
         LongLaunch l;
@@ -2491,7 +2551,8 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
         l.list = a.long_list; l.list_count = a.long_count; l.work_next = p.retry_count + 4;
         l.slots = p.slots; l.slots4 = p.slots4; l.n_slots = p.n_slots; l.root_base = p.root_base;
         l.max_tok_bytes = p.max_tok_bytes; l.long_span = p.long_span;
-        const uint64_t lb = p.n_str < (uint64_t)(p.max_blocks / 16) ? p.n_str : (uint64_t)(p.max_blocks / 16);
+        const uint64_t lcap = (uint64_t)(p.max_blocks / 16) / FALLBACK_DIV;
+        const uint64_t lb = p.n_str < lcap ? p.n_str : lcap;
         l.blocks = (unsigned)(lb ? lb : 1);
         launch_long(l, stream);
     }
@@ -2508,6 +2569,10 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     const uint64_t nb = (p.n_str + FIN_BATCH - 1) / FIN_BATCH;
     FinishArgs f;
     f.bsum = nullptr; f.ctr = nullptr;
+    const bool fold_hist = p.hist && p.hist_bins >= 2 && p.hist_bins <= FIN_MAX_BINS;
+    f.hist = fold_hist ? reinterpret_cast<unsigned long long *>(p.hist) : nullptr;
+    f.status = p.status;
+    f.n_bins = p.hist_bins;
     if (nb > 1) hipLaunchKernelGGL(batch_scan_kernel, dim3(1), dim3(SCAN_THREADS), 0, stream, p.n_str, p.flags, p.bpre, p.retry_count);
     else { f.bsum = p.flags; f.ctr = p.retry_count; }
     f.staging = p.staging16 ? (const void *)p.staging16 : (const void *)p.staging;
@@ -2518,6 +2583,11 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     const uint64_t fb = nb * f.slices;
     if (p.staging16) hipLaunchKernelGGL(finish_kernel<int16_t>, dim3((unsigned)fb), dim3(FIN_THREADS), 0, stream, f);
     else hipLaunchKernelGGL(finish_kernel<int32_t>, dim3((unsigned)fb), dim3(FIN_THREADS), 0, stream, f);
+    if (p.hist && !fold_hist) {   // too many bins for the finish pass's LDS: the separate pass
+        const hipError_t eh = hipGetLastError();
+        if (eh != hipSuccess) return eh;
+        return launch_histogram(p.id_off, p.status, p.n_str, p.hist, p.hist_bins, stream);
+    }
     return hipGetLastError();
 }
 

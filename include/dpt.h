@@ -189,6 +189,15 @@ int dpt_dp_host_far(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uint8_
 int dpt_token_histogram(const uint64_t *id_off, const int32_t *status, uint64_t n_str,
                         int64_t *hist, uint32_t n_bins, void *hip_stream);
 
+/*
+ * Fold the token-count histogram of dpt_token_histogram into the NEXT dpt_encode call on this ctx
+ * (its finish pass: no separate launch, no re-read of the offsets and statuses): hist (device
+ * pointer, n_bins + 8 int64, layout and accumulate semantics of dpt_token_histogram) is added to
+ * once, stream-ordered with that call.  hist NULL cancels.  n_bins above 1024 uses the separate
+ * histogram pass after the encode.  One call only: set it again for the next.
+ */
+int dpt_ctx_set_histogram(dpt_ctx *c, int64_t *hist, uint32_t n_bins);
+
 /* Per-ctx kernel timing with HIP events on the encode stream (for bench.py's roofline): one event
  * pair per call around the tokenize passes (first pass, 2048-byte pass, unbounded pass). */
 int dpt_ctx_profile(dpt_ctx *c, int enable);

@@ -172,6 +172,37 @@ def test_device_path_and_histogram(engines, oracles):
     assert np.array_equal(h[:257], np.bincount(np.minimum(counts, 257), minlength=258)[:257])
 
 
+@pytest.mark.parametrize("n,n_bins", [(50000, 258), (257, 258), (100, 2), (3000, 1500), (1, 16)])
+def test_histogram_folded_into_encode(n, n_bins, engines):
+    """dpt_ctx_set_histogram: the finish pass's histogram (one call; n_bins > 1024 takes the separate
+    pass) equals dpt_token_histogram's, statuses included (the OOV fixture's strings fail)."""
+    torch = pytest.importorskip("torch")
+    from dptok import synth, pack_strings
+    g = load_golden("oov_llama32k.json.gz")
+    texts = [c["text"] for c in g["cases"]] + synth.unpack(*synth.random_ascii_corpus(max(n, 1), 256, seed=22))
+    text, offs = pack_strings(texts[:n] + ["", " "])
+    m = len(offs) - 1
+    enc = engines["llama32k"]
+    dt = torch.from_numpy(np.array(text)).cuda()
+    do = torch.from_numpy(offs.view(np.int64)).cuda()
+    ids = torch.empty(len(text), dtype=torch.int32, device="cuda")
+    id_off = torch.empty(m + 1, dtype=torch.int64, device="cuda")
+    st = torch.empty(m, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    folded = torch.full((n_bins + 8,), 7, dtype=torch.int64, device="cuda")   # accumulated into
+    sep = torch.full((n_bins + 8,), 7, dtype=torch.int64, device="cuda")
+    enc.set_histogram(folded.data_ptr(), n_bins)
+    enc.encode_device(dt.data_ptr(), int(offs[-1]), do.data_ptr(), m, ids.data_ptr(), len(text), id_off.data_ptr(),
+                      st.data_ptr(), stream=s)
+    enc.histogram_device(id_off.data_ptr(), st.data_ptr(), m, sep.data_ptr(), n_bins, stream=s)
+    # one call only: the next encode adds nothing to it
+    enc.encode_device(dt.data_ptr(), int(offs[-1]), do.data_ptr(), m, ids.data_ptr(), len(text), id_off.data_ptr(),
+                      st.data_ptr(), stream=s)
+    torch.cuda.synchronize()
+    assert torch.equal(folded, sep), (folded.cpu().numpy()[-8:], sep.cpu().numpy()[-8:])
+    assert int(sep[n_bins + 1]) == m + 7
+
+
 @pytest.mark.parametrize("variant", ["rows16", "rows64"])
 def test_kernel_variants_vs_oracle(variant, engines, oracles, monkeypatch):
     """Every first-pass kernel (DPT_KERNEL override) is bit-exact on cfg2 / Arabic / S2ORC samples."""

@@ -14,7 +14,7 @@ for lib in "$@"; do
   DPT_LIB=$PWD/$lib timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $out/$tag/trace -o run --output-format csv -- python3 tools/prof_driver.py $N 4 $GEN > $out/$tag.trace.log 2>&1 || { tail -5 $out/$tag.trace.log; exit 1; }
   DPT_LIB=$PWD/$lib timeout -k 10 120 rocprofv3 --kernel-trace --pmc $CTRS -d $out/$tag/p1 -o run --output-format csv -- python3 tools/prof_driver.py $N 2 $GEN > $out/$tag.pmc.log 2>&1 || { tail -5 $out/$tag.pmc.log; exit 1; }
   echo "== $tag"
-  python3 tools/pmc_summary.py $out/$tag | grep -A12 "256, 16"
+  python3 tools/pmc_summary.py $out/$tag | grep -A12 "kernel<256"
 done
 if [ -f dp-tokenization_amd/csrc/build/libdpt_stamps.so ]; then
   timeout -k 10 120 python3 tools/stamps.py $N 256 $GEN > $out/stamps.log 2>&1 || { tail -5 $out/stamps.log; exit 1; }

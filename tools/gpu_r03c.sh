@@ -4,5 +4,5 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout
 tail -2 gpurun_out/r03c/pytest.log
 L=dp-tokenization_amd/csrc/build
 for wl in cfg2 cfg4 bloom; do
-  bash tools/ab_libs_wl.sh $wl $L/var_full/libdpt.so $L/var_hashref/libdpt.so $L/var_hashonly/libdpt.so $L/var_refonly/libdpt.so $L/var_afast0/libdpt.so $L/var_wpe5/libdpt.so || exit 1
+  bash tools/ab_libs_wl.sh $wl dp-tokenization_amd/dptok/libdpt.so $L/var_hashonly/libdpt.so $L/var_refonly/libdpt.so $L/var_afast0/libdpt.so $L/var_bpair0/libdpt.so $L/var_wpe5/libdpt.so $L/var_fbdiv1/libdpt.so || exit 1
 done

@@ -9,11 +9,23 @@ reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 gen = sys.argv[3] if len(sys.argv) > 3 else "ascii"
 # generated corpora are cached in /tmp (one GPU call runs this driver many times)
 cache = "/tmp/dpt_corpus_%s_%d.npz" % (gen, n)
+cut = None
+if gen == "bloom":
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from bloom_fixture import big_vocab
+    t2i = big_vocab()
+else:
+    t2i = synth.llama_shaped_vocab()
 if gen != "ascii" and os.path.exists(cache):
     z = np.load(cache)
     text, offs = z["text"], z["offs"]
+    cut = z["cut"] if "cut" in z else None
 elif gen == "ascii":
     text, offs = synth.random_ascii_corpus(n, 256, seed=1)
+elif gen == "bloom":
+    procs = 16 if (len(sys.argv) > 4 and sys.argv[4] == "gen-only") else 1
+    text, offs, cut = synth.bloom_like_parallel(n, t2i, procs=procs, length=256)
+    np.savez(cache, text=text, offs=offs, cut=cut)
 else:
     # (forks: only in the gen-only run, which no profiler wraps)
     procs = 16 if (len(sys.argv) > 4 and sys.argv[4] == "gen-only") else 1
@@ -24,14 +36,16 @@ if len(sys.argv) > 4 and sys.argv[4] == "gen-only":   # run without a profiler f
     sys.exit(0)
 import torch  # noqa: E402
 from dptok import Encoder, Vocab  # noqa: E402
-enc = Encoder(Vocab(synth.llama_shaped_vocab(), 0))
+enc = Encoder(Vocab(t2i, 0))
 dev = torch.device("cuda", 0)
 dt = torch.from_numpy(text).to(dev); do = torch.from_numpy(offs.view(np.int64)).to(dev)
 nb = len(text)
 ids = torch.empty(nb, dtype=torch.int32, device=dev); io = torch.empty(n + 1, dtype=torch.int64, device=dev)
 st = torch.empty(n, dtype=torch.int32, device=dev)
 s = torch.cuda.current_stream().cuda_stream
+dc = torch.from_numpy(cut).to(dev) if cut is not None else None
 for _ in range(reps):
-    enc.encode_device(dt.data_ptr(), nb, do.data_ptr(), n, ids.data_ptr(), nb, io.data_ptr(), st.data_ptr(), stream=s)
+    enc.encode_device(dt.data_ptr(), nb, do.data_ptr(), n, ids.data_ptr(), nb, io.data_ptr(), st.data_ptr(), stream=s,
+                      cut_ptr=dc.data_ptr() if dc is not None else 0, mode="atoms" if dc is not None else "raw")
 torch.cuda.synchronize()
 print("tokens", int(io[-1].item()), "bytes", nb)

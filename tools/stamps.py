@@ -9,7 +9,11 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 200000
 L = int(sys.argv[2]) if len(sys.argv) > 2 else 256
 gen = sys.argv[3] if len(sys.argv) > 3 else "ascii"
 enc = Encoder(Vocab(synth.llama_shaped_vocab(), 0))
-if gen == "ascii":
+cache = "/tmp/dpt_corpus_%s_%d.npz" % (gen, n)   # tools/prof_driver.py's gen-only cache
+if gen != "ascii" and os.path.exists(cache):
+    z = np.load(cache)
+    text, offs = z["text"], z["offs"]
+elif gen == "ascii":
     text, offs = synth.random_ascii_corpus(n, L, seed=1)
 elif gen == "s2orc":
     text, offs = synth.s2orc_like_corpus(n, seed=4)
