@@ -486,6 +486,12 @@ __device__ __forceinline__ bool is_word_start(unsigned b, unsigned cm, int mode)
     return mode == 0 ? (b == ' ') : (mode == 1 ? (cm != 0 && (b & 0xC0u) != 0x80u) : (cm & 1u) != 0);
 }
 
+// 0x80 in every byte of x equal to the matching byte of c4, 0 elsewhere (exact per byte)
+__device__ __forceinline__ uint32_t eq_bytes(uint32_t x, uint32_t c4) {
+    const uint32_t y = x ^ c4;
+    return ~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y | 0x7F7F7F7Fu);
+}
+
 // Finds the window [pos, pos+wlen) (ends at a word start or at the string end).
 // Returns false when a single word does not fit in CH bytes.
 template <int CH>
@@ -496,6 +502,16 @@ __device__ bool window_bounds(const WinRegs<CH> &W, uint64_t slen, uint64_t pos,
         return true;
     }
     int best = is_word_start(W.t_end, W.c_end, mode) ? CH : -1;
+    if (CH == 256 && mode == 0) {
+        // raw mode: the last space in bytes 1..255, from a per-byte equality mask of the lane's dword
+        uint32_t sp = eq_bytes(W.t[0], 0x20202020u);
+        if (lane == 0) sp &= ~0x80u;   // byte 0 starts the window anyway
+        if (sp) best = max(best, (int)(4u * lane + ((31u - (unsigned)__builtin_clz(sp)) >> 3)));
+        const unsigned q = wave_max_u32((unsigned)(best + 1));
+        if (q == 0) return false;
+        wlen = q - 1;
+        return true;
+    }
 #pragma unroll
     for (int c = 0; c < CH / 256; c++)
 #pragma unroll
@@ -516,6 +532,63 @@ template <int CH, int G, bool WIDE>
 __device__ bool prep_window(GroupLDS<CH, G> &L, uint8_t *gw, const WinRegs<CH> &W, uint64_t pos,
                             unsigned wlen, int mode, unsigned lane, unsigned &n_atoms_o, unsigned &n_words_o) {
     const bool raw = mode == 0;
+#ifndef PREP_ASCII
+#define PREP_ASCII 1   // A/B knob: 0 = pure-ASCII raw windows take the general per-byte code below
+#endif
+    if constexpr (PREP_ASCII && G == 16 && CH == 256 && !WIDE) {
+        // Pure-ASCII raw windows: atom k is byte k, so the atom offsets are the identity and only the
+        // newlines ('\n' = "<0x0A>", 6 code points) and the string's first atom ('\u2581' + c, 2) move the
+        // code-point prefixes -- per-byte equality masks of the lane's dword (SWAR) instead of per-byte
+        // flags, one scan, the lane's four rec[] entries in one 16-byte LDS store.
+        const uint32_t w = W.t[0];
+        const unsigned k0 = 4u * lane;
+        const unsigned nv = wlen > k0 ? min(wlen - k0, 4u) : 0u;   // the lane's bytes in the window
+        const uint32_t vm = nv >= 4u ? 0xFFFFFFFFu : ((1u << (8u * nv)) - 1u);
+        if (raw && !ballot((w & vm & 0x80808080u) != 0)) {
+            const bool first0 = pos == 0;   // byte 0 is the string's first atom
+            uint32_t nl = eq_bytes(w, 0x0A0A0A0Au) & vm;
+            uint32_t ws = eq_bytes(w, 0x20202020u) & vm;
+            if (lane == 0) {
+                if (first0) nl &= ~0x80u;   // '\u2581' + '\n': two code points, no expansion
+                ws |= 0x80u;                // a window starts with a word
+            }
+            const unsigned v = (unsigned)__builtin_popcount(nl) | ((unsigned)__builtin_popcount(ws) << 9);
+            const unsigned incl = wave_incl_scan_add(v);
+            const unsigned tot = __builtin_amdgcn_readlane(incl, 63);
+            const unsigned nlb = (incl - v) & 0x1FFu;   // newlines before the lane's first byte
+            const unsigned f1 = first0 ? 1u : 0u;
+            uint32_t r[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const unsigned k = k0 + (unsigned)u;
+                const unsigned nlu = nlb + (unsigned)__builtin_popcount(nl & ((1u << (8u * (unsigned)u)) - 1u));
+                const unsigned cp = k + 5u * nlu + (k > 0 ? f1 : 0u);
+                r[u] = 0xFFFF0000u | cp | (((ws >> (8u * (unsigned)u + 7u)) & 1u) ? CP_WS : 0u);
+            }
+            uint32_t *rec32 = reinterpret_cast<uint32_t *>(L.rec);
+            if (nv == 4u) {
+                *reinterpret_cast<uint4 *>(&rec32[k0]) = make_uint4(r[0], r[1], r[2], r[3]);
+                *reinterpret_cast<uint32_t *>(&L.bytes[k0]) = w;
+            } else if (nv) {
+#pragma unroll
+                for (int u = 0; u < 4; u++)
+                    if ((unsigned)u < nv) rec32[k0 + u] = r[u];
+                *reinterpret_cast<uint32_t *>(&L.bytes[k0]) = w;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                if ((unsigned)u < nv) L.aoff[k0 + u] = (typename GroupLDS<CH, G>::Idx)(k0 + (unsigned)u);
+            const unsigned cp_tot1 = wlen + 5u * (tot & 0x1FFu) + f1;
+            if (lane == 0) {
+                L.aoff[wlen] = (typename GroupLDS<CH, G>::Idx)wlen;
+                rec32[wlen] = 0xFFFF0000u | cp_tot1 | CP_WS;
+            }
+            n_atoms_o = wlen;
+            n_words_o = tot >> 9;
+            wave_sync();
+            return true;
+        }
+    }
     unsigned n_atoms = 0, cp_tot = 0, n_words = 0;
     bool hi_byte = false;   // some byte >= 0x80: atoms may be longer than one byte
 #pragma unroll
@@ -566,7 +639,9 @@ __device__ bool prep_window(GroupLDS<CH, G> &L, uint8_t *gw, const WinRegs<CH> &
                     reinterpret_cast<uint32_t *>(L.rec)[ai] = 0xFFFF0000u | cp | (wst[u] ? CP_WS : 0u);
                 else
                     L.rec[ai].cpos = (uint16_t)(cp | (wst[u] ? CP_WS : 0));
-                if (wst[u]) { L.set_word_start(gw, wi, ai); wi++; }
+                // (the 256-byte pass's word list lives in global scratch and is needed only by row-mode
+                // windows: C0 rebuilds it there -- a store here would hold phase A's first loads back)
+                if (wst[u]) { if constexpr (!GroupLDS<CH, G>::WSLG) L.set_word_start(gw, wi, ai); wi++; }
                 ai++;
             }
             cp += cpl[u];
@@ -579,7 +654,7 @@ __device__ bool prep_window(GroupLDS<CH, G> &L, uint8_t *gw, const WinRegs<CH> &
         L.aoff[n_atoms] = (typename GroupLDS<CH, G>::Idx)wlen;
         if constexpr (G == 16) reinterpret_cast<uint32_t *>(L.rec)[n_atoms] = 0xFFFF0000u | cp_tot | CP_WS;
         else L.rec[n_atoms].cpos = (uint16_t)(cp_tot | CP_WS);
-        L.set_word_start(gw, n_words, n_atoms);
+        if constexpr (!GroupLDS<CH, G>::WSLG) L.set_word_start(gw, n_words, n_atoms);
     }
     n_atoms_o = n_atoms;
     n_words_o = n_words;
@@ -651,7 +726,10 @@ __device__ __forceinline__ TrieView tv_of(ConstKernArgs *kp) {
 #define KREFRESH() do { } while (0)
 #endif
 
-template <int CH, int G, bool BIG, bool WIDE, int SW = 0>   // SW: staged id width 0 = by a.staging16, 1 = int16, 2 = int32
+// SW: staged id width 0 = by a.staging16, 1 = int16, 2 = int32; RAW: DPT_MODE_RAW as a compile-time
+// constant (its expansions and word starts fold away in the other modes' code and vice versa -- the
+// 16-lane kernel sits at its register limit)
+template <int CH, int G, bool BIG, bool WIDE, int SW = 0, bool RAW = false>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CH == 256 && G == 16) ? WPE16 : 1)))
 tokenize_kernel(KernArgs ka) {
     ConstKernArgs *kp = (ConstKernArgs *)__builtin_amdgcn_kernarg_segment_ptr();
@@ -674,7 +752,9 @@ tokenize_kernel(KernArgs ka) {
     const uint64_t n_work = BIG ? (uint64_t)(*a.work_count) : a.n_str;
     if (BIG && n_work == 0) return;   // no retries: no counter traffic
     const uint64_t base_off = a.str_off[0];
-    const int mode = a.mode & DPT_MODE_MASK;
+    // (the other instantiations keep the mode a run-time value: folding raw = false into the atoms-mode
+    // 16-lane kernel crashes ROCm 7.2's greedy register allocator)
+    const int mode = RAW ? 0 : (a.mode & DPT_MODE_MASK);
     const bool raw = mode == 0;
     const bool uncapped = (a.mode & DPT_FLAG_UNCAPPED) != 0;   // f2: inspect_tokenizer's inf-initialised DP
     const bool len_only = (a.mode & (DPT_FLAG_UNCAPPED | DPT_FLAG_LEN_ONLY)) != 0;
@@ -1701,6 +1781,24 @@ tokenize_kernel(KernArgs ka) {
         KREFRESH();
         // (word w ends at atom word_end(w); its final state is in fin[word_end(w)])
         if (DPT_RUN_B && !lane_mode) {
+            if constexpr (GL::WSLG) {
+                // the word list (word -> first atom, then the window end) from the word-start bits
+#pragma unroll
+                for (int g = 0; g < NG; g++) {
+                    const unsigned na = uni(SS[g].n_atoms);
+                    if (na == 0) continue;
+                    const GL &L = grp(g);
+                    uint8_t *gw = wsl_of(g);
+                    unsigned wi = 0;
+                    for (unsigned j0 = 0; j0 <= na; j0 += 64u) {
+                        const unsigned j = j0 + lane;
+                        const bool ws = j <= na && (L.rec[j].cpos & CP_WS) != 0;   // atom na: the window end
+                        const uint64_t m = ballot(ws);
+                        if (ws) gw[wi + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u))] = (uint8_t)j;
+                        wi += (unsigned)__builtin_popcountll(m);
+                    }
+                }
+            }
             unsigned pre[NG + 1];
             pre[0] = 0;
 #pragma unroll
@@ -1929,10 +2027,18 @@ tokenize_kernel(KernArgs ka) {
             if constexpr (BULK) {
                 const bool i16 = n16;
                 unsigned r = 0;
-                for (unsigned t0 = 0; t0 < total; t0 += 64u * 4u) {
-                    int32_t ix[4];
-                    unsigned kind[4];   // 0: not here, 1 / 2: a token of that many bytes
-                    uint64_t oq[4];
+#ifndef C2_DEFER
+#define C2_DEFER 0   // A/B knob: the bulk pass's int16 stores after all its lookups (see below): the held ids
+                     // spill -- cfg2 -4.1 %, cfg4 +1.9 % (profiles/r03_ab.log)
+#endif
+                // The bulk pass over every selected token, 4 per lane per round of 256.  int16 ids from the
+                // pair table: all the window-set's lookups first, then all its stores -- a load waits for
+                // every OLDER vector-memory op of the wave, stores included (MI355X_MICROARCH.md: vmcnt
+                // counts loads and stores together, in issue order), so a store between two rounds of
+                // lookups put a store's full latency on every round.
+                uint32_t kmask = 0;   // bit 4 * round + u: token 256 * round + 64 * u + lane is a bulk token
+                uint32_t pvs[8];      // its id: 16-bit half (u & 1) of pvs[2 * round + u / 2]
+                auto bulk_round = [&](unsigned t0, int32_t (&ix)[4], unsigned (&kind)[4], uint64_t (&oq)[4]) {
 #pragma unroll
                     for (int u = 0; u < 4; u++) {
                         const unsigned t = t0 + 64u * (unsigned)u + lane;
@@ -1967,6 +2073,43 @@ tokenize_kernel(KernArgs ka) {
                         if (res) list_ref(r + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u))) = (uint16_t)t;
                         r += (unsigned)__builtin_popcountll(m);
                     }
+                };
+                if constexpr (SW == 1 && C2_PAIR16 && C2_DEFER) {
+                    static_assert(NG * CH <= 1024, "four rounds of 256 tokens cover a window set");
+#pragma unroll
+                    for (int rd = 0; rd < 4; rd++) {
+                        if (256u * (unsigned)rd < total) {
+                            int32_t ix[4];
+                            unsigned kind[4];
+                            uint64_t oq[4];
+                            bulk_round(256u * (unsigned)rd, ix, kind, oq);
+                            int16_t pv[4];
+#pragma unroll
+                            for (int u = 0; u < 4; u++) {
+                                pv[u] = tv.pair16[ix[u]];
+                                kmask |= (kind[u] ? 1u : 0u) << (4 * rd + u);
+                            }
+                            pvs[2 * rd] = (uint32_t)(uint16_t)pv[0] | ((uint32_t)(uint16_t)pv[1] << 16);
+                            pvs[2 * rd + 1] = (uint32_t)(uint16_t)pv[2] | ((uint32_t)(uint16_t)pv[3] << 16);
+                        }
+                    }
+                    // the stores: token t of slot g goes to staging element obase[g] + (t - pre[g])
+#pragma unroll
+                    for (int q2 = 0; q2 < 16; q2++) {
+                        if ((kmask >> q2) & 1u) {
+                            const unsigned t = 256u * (unsigned)(q2 >> 2) + 64u * (unsigned)(q2 & 3) + lane;
+                            uint64_t ob = obase[0] - pre[0];
+#pragma unroll
+                            for (int k = 1; k < NG; k++) ob = t >= pre[k] ? obase[k] - pre[k] : ob;
+                            a.staging16[ob + t] = (int16_t)(pvs[q2 >> 1] >> (16 * (q2 & 1)));
+                        }
+                    }
+                }
+                for (unsigned t0 = 0; t0 < total && !(SW == 1 && C2_PAIR16 && C2_DEFER); t0 += 64u * 4u) {
+                    int32_t ix[4];
+                    unsigned kind[4];   // 0: not here, 1 / 2: a token of that many bytes
+                    uint64_t oq[4];
+                    bulk_round(t0, ix, kind, oq);
                     if constexpr (SW == 1 && C2_PAIR16) {
                         int16_t pv[4];
 #pragma unroll
@@ -2446,12 +2589,12 @@ static_assert(block_lds_bytes<SMALL_CH, 64>() <= 64 * 1024, "small LDS");
 static_assert(block_lds_bytes<BIG_CH, 64>() <= 160 * 1024, "big LDS");
 
 // Resident waves per CU for an instantiation (LDS / VGPR limited); DPT_WAVES_PER_CU overrides.
-template <int CH, int G, bool BIG, bool WIDE, int SW = 0>
+template <int CH, int G, bool BIG, bool WIDE, int SW = 0, bool RAW = false>
 static unsigned resident_per_cu() {
     static unsigned cached = 0;
     if (cached) return cached;
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, tokenize_kernel<CH, G, BIG, WIDE, SW>, 64, block_lds_bytes<CH, G>()) != hipSuccess || nb <= 0)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, tokenize_kernel<CH, G, BIG, WIDE, SW, RAW>, 64, block_lds_bytes<CH, G>()) != hipSuccess || nb <= 0)
         nb = 8;
     if (const char *e = getenv("DPT_WAVES_PER_CU")) {
         const int v = atoi(e);
@@ -2462,10 +2605,10 @@ static unsigned resident_per_cu() {
 }
 
 // Persistent grid: every resident wave pulls strings from the work counter until it runs dry.
-template <int CH, int G, bool BIG, bool WIDE, int SW = 0>
+template <int CH, int G, bool BIG, bool WIDE, int SW = 0, bool RAW = false>
 static void launch_tok(const EncodeArgs &a, const TrieView &tv, uint64_t n_units, unsigned n_cu, hipStream_t stream) {
     constexpr int lds = block_lds_bytes<CH, G>();
-    uint64_t wpc = resident_per_cu<CH, G, BIG, WIDE, SW>();
+    uint64_t wpc = resident_per_cu<CH, G, BIG, WIDE, SW, RAW>();
     if constexpr (G == 16 && !BIG) {
         // small calls: no more resident waves than give every slot ~7 strings (rounds of 4 strings per
         // wave; a wave's last round is the tail): 125k strings run 3 % faster at 18 waves per CU than
@@ -2477,7 +2620,7 @@ static void launch_tok(const EncodeArgs &a, const TrieView &tv, uint64_t n_units
     uint64_t blocks = (uint64_t)n_cu * wpc;
     if (blocks > (uint64_t)n_cu * 64u) blocks = (uint64_t)n_cu * 64u;   // the scratch is sized for 64 per CU
     if (blocks > n_units) blocks = n_units ? n_units : 1;
-    hipLaunchKernelGGL((tokenize_kernel<CH, G, BIG, WIDE, SW>), dim3((unsigned)blocks), dim3(64), lds, stream, KernArgs{a, tv});
+    hipLaunchKernelGGL((tokenize_kernel<CH, G, BIG, WIDE, SW, RAW>), dim3((unsigned)blocks), dim3(64), lds, stream, KernArgs{a, tv});
 }
 
 hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t ev[2]) {
@@ -2495,6 +2638,7 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     a.long_span = p.long_span;
     TrieView tv{p.slots, p.slot_ids, p.slots4, p.root_base, p.n_slots, p.pair16};
     const bool wide = (p.mode & DPT_MODE_MASK) == DPT_MODE_ATOMS;   // atoms of up to 8 bytes
+    const bool raw = (p.mode & DPT_MODE_MASK) == DPT_MODE_RAW;
 
     if (p.n_str == 0) {
         // no finish kernel runs: id_off[0] = 0, and the call's claimed arena bytes ("last need") and
@@ -2518,12 +2662,16 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
                 if (wide) {
                     if (p.staging16) launch_tok<SMALL_CH, 16, false, true, 1>(a, tv, nu, n_cu, stream);
                     else launch_tok<SMALL_CH, 16, false, true, 2>(a, tv, nu, n_cu, stream);
+                } else if (raw) {
+                    if (p.staging16) launch_tok<SMALL_CH, 16, false, false, 1, true>(a, tv, nu, n_cu, stream);
+                    else launch_tok<SMALL_CH, 16, false, false, 2, true>(a, tv, nu, n_cu, stream);
                 } else {
                     if (p.staging16) launch_tok<SMALL_CH, 16, false, false, 1>(a, tv, nu, n_cu, stream);
                     else launch_tok<SMALL_CH, 16, false, false, 2>(a, tv, nu, n_cu, stream);
                 }
             } else {
                 if (wide) launch_tok<SMALL_CH, 64, false, true>(a, tv, p.n_str, n_cu, stream);
+                else if (raw) launch_tok<SMALL_CH, 64, false, false, 0, true>(a, tv, p.n_str, n_cu, stream);
                 else launch_tok<SMALL_CH, 64, false, false>(a, tv, p.n_str, n_cu, stream);
             }
         }
@@ -2538,6 +2686,7 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
         uint64_t fb_units = (uint64_t)(p.max_blocks / 64) / FALLBACK_DIV;
         fb_units = fb_units < p.n_str ? fb_units : p.n_str;
         if (wide) launch_tok<BIG_CH, 64, true, true>(b, tv, fb_units ? fb_units : 1, p.max_blocks / 64, stream);
+        else if (raw) launch_tok<BIG_CH, 64, true, false, 0, true>(b, tv, fb_units ? fb_units : 1, p.max_blocks / 64, stream);
         else launch_tok<BIG_CH, 64, true, false>(b, tv, fb_units ? fb_units : 1, p.max_blocks / 64, stream);
         // the unbounded pass over whatever the windowed passes could not hold (usually nothing:
         // its waves read a zero count and exit)
@@ -2615,6 +2764,9 @@ hipError_t kernel_init() {
     if (done) return hipSuccess;
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&tokenize_kernel<BIG_CH, 64, true, false>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, block_lds_bytes<BIG_CH, 64>());
+    if (e == hipSuccess)
+        e = hipFuncSetAttribute(reinterpret_cast<const void *>(&tokenize_kernel<BIG_CH, 64, true, false, 0, true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, block_lds_bytes<BIG_CH, 64>());
     if (e == hipSuccess)
         e = hipFuncSetAttribute(reinterpret_cast<const void *>(&tokenize_kernel<BIG_CH, 64, true, true>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, block_lds_bytes<BIG_CH, 64>());
