@@ -533,7 +533,8 @@ __device__ bool prep_window(GroupLDS<CH, G> &L, uint8_t *gw, const WinRegs<CH> &
                             unsigned wlen, int mode, unsigned lane, unsigned &n_atoms_o, unsigned &n_words_o) {
     const bool raw = mode == 0;
 #ifndef PREP_ASCII
-#define PREP_ASCII 1   // A/B knob: 0 = pure-ASCII raw windows take the general per-byte code below
+#define PREP_ASCII 0   // A/B knob: 1 = pure-ASCII raw windows take this SWAR path (cfg2 100.60 vs 100.95 GB/s,
+                       // cfg4 66.87 vs 66.62: no gain, 3 more VGPR spills; profiles/r03_ab.log)
 #endif
     if constexpr (PREP_ASCII && G == 16 && CH == 256 && !WIDE) {
         // Pure-ASCII raw windows: atom k is byte k, so the atom offsets are the identity and only the

@@ -30,8 +30,10 @@ def source_hash(read=None) -> str:
     return h.hexdigest()
 
 
-def run_pass(counter: str, n: int, out: str, rerun: bool = True) -> float:
+def run_pass(counter: str, n: int, out: str, rerun: bool = True, lib: str = None) -> float:
     env = dict(os.environ, TMPDIR="/tmp")
+    if lib:
+        env["DPT_LIB"] = lib
     cmd = ["rocprofv3", "--kernel-trace", "--pmc", counter, "-d", out, "-o", "run", "--output-format", "csv",
            "--", sys.executable, os.path.join(ROOT, "tools", "prof_driver.py"), str(n), "3", "ascii"]
     if rerun:
@@ -56,10 +58,23 @@ def main():
     rerun = os.environ.get("PMC_REUSE") != "1"   # PMC_REUSE=1: re-read the CSVs of a previous run
     fetch = run_pass("FETCH_SIZE", n, os.path.join(out, "fetch"), rerun)
     write = run_pass("WRITE_SIZE", n, os.path.join(out, "write"), rerun)
+    # FETCH_SIZE calibration on THIS kernel's access pattern: the build that stops
+    # after prep (-DDPT_STOP=1, `make variant V=stop1`) reads exactly the text (aligned dword buffer loads,
+    # n x 256 B) and the offsets (8 (n+1) B) from HBM -- the trie tables stay in L2 -- so known bytes /
+    # its raw FETCH_SIZE is the factor for the full kernel's fetches (the guide's x2 is for 16-B streams)
+    stop1 = os.path.join(ROOT, "dp-tokenization_amd", "csrc", "build", "var_stop1", "libdpt.so")
+    known = n * 256 + 8 * (n + 1)
+    factor, cal = 2.0, None
+    if os.path.exists(stop1):
+        cal = run_pass("FETCH_SIZE", n, os.path.join(out, "fetch_stop1"), rerun, lib=stop1)
+        factor = known / cal
     rec = {"source_sha256": source_hash(), "workload": "cfg2 %d x 256 B random ASCII" % n, "n_str": n,
-           "fetch_bytes_raw": fetch, "fetch_bytes": 2 * fetch, "write_bytes": write,
-           "traffic_bytes_per_launch": 2 * fetch + write,
-           "method": "rocprofv3 --kernel-trace --pmc FETCH_SIZE | WRITE_SIZE (separate passes); FETCH_SIZE x2 (gfx950)"}
+           "fetch_bytes_raw": fetch, "fetch_factor": factor, "fetch_bytes": factor * fetch, "write_bytes": write,
+           "traffic_bytes_per_launch": factor * fetch + write,
+           "calibration": {"build": "DPT_STOP=1 (prep only)", "known_fetch_bytes": known, "raw_fetch_bytes": cal,
+                           "factor": factor} if cal else None,
+           "method": "rocprofv3 --kernel-trace --pmc FETCH_SIZE | WRITE_SIZE (separate passes); FETCH_SIZE x factor, "
+                     "the factor calibrated on the prep-only build of the same kernel (known bytes / raw FETCH_SIZE)"}
     for path in (os.path.join(ROOT, "profiles", "pmc_traffic.json"), os.path.join(out, "pmc_traffic.json")):
         with open(path, "w") as fh:   # the gpurun_out copy is what travels back from a GPU box
             json.dump(rec, fh, indent=1)
