@@ -185,16 +185,25 @@ int ensure_workspace(dpt_ctx *c, const dpt_vocab *v, uint64_t n_bytes, uint64_t 
 // every token an unambiguous lookup.  For a token of the last vocabulary entry of equal bytes wins,
 // like the trie (dpt_vocab.cpp).
 std::vector<uint32_t> build_token_hash(const uint8_t *blob, const uint64_t *off, const int32_t *ids, uint32_t n) {
-    struct Key { uint32_t w[4]; uint32_t len; int32_t id; };
+    struct Key { uint32_t w[dpt::TOKHASH_MAX_BYTES_LONG / 4]; uint32_t len; int32_t id; };
     std::vector<Key> keys;
     keys.reserve(n);
     for (uint32_t t = 0; t < n; t++) {
         const uint64_t len = off[t + 1] - off[t];
-        if (len == 0 || len > dpt::TOKHASH_MAX_BYTES) continue;
-        Key k{{0, 0, 0, 0}, (uint32_t)len, ids ? ids[t] : (int32_t)t};
-        memcpy(k.w, blob + off[t], len);   // little-endian dwords, zero past the token
+        if (len == 0 || len > dpt::TOKHASH_MAX_BYTES_LONG) continue;
+        Key k;
+        memset(k.w, 0, sizeof(k.w));
+        k.len = (uint32_t)len;
+        k.id = ids ? ids[t] : (int32_t)t;
+        memcpy(k.w, blob + (off[t] - off[0]), len);   // little-endian dwords, zero past the token
         keys.push_back(k);
     }
+    auto khash = [](const Key &k, uint32_t seed, uint32_t &h, uint32_t &fp) {
+        const unsigned nd = k.len <= 16 ? 4u : (k.len + 3u) / 4u;
+        uint32_t a = dpt::tokhash_start(k.len, seed);
+        for (unsigned q = 0; q < nd; q++) a = dpt::tokhash_step(a, k.w[q], q, q + 1 == nd);
+        dpt::tokhash_end(a, h, fp);
+    };
     std::vector<uint32_t> none(4, 0u);
     if (keys.empty()) return none;
     uint32_t nb = 1;
@@ -207,7 +216,7 @@ std::vector<uint32_t> build_token_hash(const uint8_t *blob, const uint64_t *off,
         bool bad = false;
         for (size_t q = 0; q < keys.size() && !bad; q++) {
             uint32_t h, fp;
-            dpt::tokhash(keys[q].w[0], keys[q].w[1], keys[q].w[2], keys[q].w[3], keys[q].len, seed, h, fp);
+            khash(keys[q], seed, h, fp);
             uint32_t b = h & (nb - 1), p = 1;
             for (;; b = (b + 1) & (nb - 1), p++) {
                 uint32_t *e = bk + 4 * (size_t)b;
@@ -221,7 +230,7 @@ std::vector<uint32_t> build_token_hash(const uint8_t *blob, const uint64_t *off,
         // every key's lookup (the first entry of its fingerprint from its home bucket) is its own entry
         for (size_t q = 0; q < keys.size() && !bad; q++) {
             uint32_t h, fp;
-            dpt::tokhash(keys[q].w[0], keys[q].w[1], keys[q].w[2], keys[q].w[3], keys[q].len, seed, h, fp);
+            khash(keys[q], seed, h, fp);
             uint32_t b = h & (nb - 1);
             for (uint32_t p = 0; p < max_probe; p++, b = (b + 1) & (nb - 1)) {
                 const uint32_t *e = bk + 4 * (size_t)b;

@@ -76,7 +76,8 @@ __host__ __device__ inline unsigned child_bit(unsigned b) { return (b ^ (b >> 5)
 // probed linearly; fp != 0 (0 marks a free entry).  The builder checks that every token's lookup
 // finds its own entry within `max_probe` buckets (else it re-seeds): a span the DP selected is a
 // vocabulary token by construction (phase A matched it), so the lookup needs no key compare.
-constexpr unsigned TOKHASH_MAX_BYTES = 16;
+constexpr unsigned TOKHASH_MAX_BYTES = 16;        // the 16-lane kernels' keys (four dwords)
+constexpr unsigned TOKHASH_MAX_BYTES_LONG = 64;   // the table's tokens; the 64-lane kernels hash keys this long
 constexpr size_t TOKHASH_OFFSET = PAIR16_N * sizeof(int16_t) + 65536 * 8;   // bytes into the pair16 allocation
 struct TokHashHeader {
     uint32_t mask;        // buckets - 1 (a power of two)
@@ -93,16 +94,27 @@ __host__ __device__ inline uint32_t tokhash_fmix(uint32_t h) {
     h ^= h >> 16;
     return h;
 }
-// (h: the bucket hash, fp: the entry's fingerprint)
-__host__ __device__ inline void tokhash(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t len, uint32_t seed,
-                                        uint32_t &h, uint32_t &fp) {
-    uint32_t a = seed ^ (len * 0x9E3779B9u);
-    a = tokhash_rotl((a ^ w0) * 0xCC9E2D51u, 15);
-    a = tokhash_rotl((a ^ w1) * 0x1B873593u, 13);
-    a = tokhash_rotl((a ^ w2) * 0xCC9E2D51u, 15);
-    a = (a ^ w3) * 0x1B873593u;
+// The key is max(4, ceil(len / 4)) little-endian dwords of the token's bytes, zero past its length:
+// a = seed ^ len * golden; every dword but the last: a = rotl((a ^ w) * C, R) (C, R alternating); the
+// last: a = (a ^ w) * C; h = fmix(a); fp = fmix(h ^ K) | 1  (h: the bucket hash, fp: the fingerprint)
+__host__ __device__ inline uint32_t tokhash_start(uint32_t len, uint32_t seed) { return seed ^ (len * 0x9E3779B9u); }
+__host__ __device__ inline uint32_t tokhash_step(uint32_t a, uint32_t w, unsigned k, bool last) {
+    a = (a ^ w) * ((k & 1u) ? 0x1B873593u : 0xCC9E2D51u);
+    return last ? a : tokhash_rotl(a, (k & 1u) ? 13u : 15u);
+}
+__host__ __device__ inline void tokhash_end(uint32_t a, uint32_t &h, uint32_t &fp) {
     h = tokhash_fmix(a);
     fp = tokhash_fmix(h ^ 0x5BD1E995u) | 1u;
+}
+// four-dword keys (tokens of at most 16 bytes)
+__host__ __device__ inline void tokhash(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t len, uint32_t seed,
+                                        uint32_t &h, uint32_t &fp) {
+    uint32_t a = tokhash_start(len, seed);
+    a = tokhash_step(a, w0, 0, false);
+    a = tokhash_step(a, w1, 1, false);
+    a = tokhash_step(a, w2, 2, false);
+    a = tokhash_step(a, w3, 3, true);
+    tokhash_end(a, h, fp);
 }
 
 // kernel variants for the first pass (the 2048-byte window pass always follows for retries)

@@ -48,6 +48,14 @@
 
 namespace dpt {
 
+#ifndef LDS_ROT
+#define LDS_ROT 0   // A/B knob: lanes store their four consecutive dwords in an order rotated by lane / 8
+                    // (A0's end-mask updates): in order, lanes 8 apart hit one LDS bank
+#endif
+#ifndef PREP_ROT
+#define PREP_ROT 0  // the same for prep_window's atom stores (costs registers: the order is data-dependent)
+#endif
+
 // ------------------------------------------------------------------ wave primitives
 
 __device__ __forceinline__ unsigned lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
@@ -442,6 +450,55 @@ __device__ __forceinline__ bool token_key(const uint8_t *bytes, unsigned p0, uns
     return true;
 }
 
+// The 64-lane kernels' hash of a token of up to TOKHASH_MAX_BYTES_LONG expanded bytes (BLOOM-scale
+// vocabularies: tokens of up to 41 code points): the dwords streamed from the window bytes with the same
+// expansion and newline rule as token_key, mixed as they come (dpt_internal.h).  False: the walkers.
+template <int CH>
+__device__ __forceinline__ bool token_hash_long(const uint8_t *bytes, unsigned p0, unsigned nbytes, bool raw, unsigned first,
+                                                uint32_t seed, uint32_t &h, uint32_t &fp) {
+    const uint32_t *wp = reinterpret_cast<const uint32_t *>(bytes) + (p0 >> 2);
+    const unsigned sh = p0 & 3u;
+    uint32_t d0 = wp[0], d1 = wp[1];
+    const unsigned b0 = __builtin_amdgcn_alignbyte(d1, d0, sh) & 0xFFu;
+    const unsigned fi = raw ? first : 0u;
+    const unsigned sp = (raw ? 1u : 0u) & (fi ^ 1u) & (unsigned)(b0 == ' ');
+    const unsigned E = nbytes + 3u * fi + 2u * sp;
+    if (E > TOKHASH_MAX_BYTES_LONG || nbytes == 0) return false;
+    const unsigned nd = E <= 16u ? 4u : (E + 3u) >> 2;
+    const bool shift = (fi | sp) != 0;
+    const unsigned as = fi ? 1u : 2u;
+    uint32_t prev = fi ? 0x8196E200u : 0x96E20000u;   // the '\u2581' prefix ahead of raw dword 0
+    uint32_t a = tokhash_start(E, seed), nl = 0;
+    for (unsigned k = 0; k < nd; k++) {
+        uint32_t r = __builtin_amdgcn_alignbyte(d1, d0, sh);   // raw bytes 4k .. 4k+3
+        d0 = d1;
+        // (bytes past the token are masked off; the read stays within 16 bytes past the window's bytes:
+        // the slot states follow them)
+        const unsigned nxt = (p0 >> 2) + k + 2u;
+        d1 = reinterpret_cast<const uint32_t *>(bytes)[nxt < (unsigned)CH / 4u + 4u ? nxt : (unsigned)CH / 4u + 3u];
+        if (raw) {
+            // bytes [fi, nbytes) hold no '\n' (a non-first newline atom expands to six bytes)
+            const unsigned lo = 4u * k;
+            uint32_t v = r | (nbytes >= lo + 4u ? 0u : (nbytes <= lo ? 0xFFFFFFFFu : ~((1u << (8u * (nbytes - lo))) - 1u)));
+            if (k == 0 && fi) v |= 0xFFu;
+            v ^= 0x0A0A0A0Au;
+            nl |= (v - 0x01010101u) & ~v & 0x80808080u;
+            if (k == 0 && sp) r = (r & 0xFFFFFF00u) | 0x81u;
+        }
+        uint32_t w = r;
+        if (shift) {
+            w = __builtin_amdgcn_alignbyte(r, prev, as);
+            prev = r;
+        }
+        const unsigned lo = 4u * k;
+        w &= E >= lo + 4u ? 0xFFFFFFFFu : (E <= lo ? 0u : (1u << (8u * (E - lo))) - 1u);
+        a = tokhash_step(a, w, k, k + 1 == nd);
+    }
+    if (nl) return false;
+    tokhash_end(a, h, fp);
+    return true;
+}
+
 // ------------------------------------------------------------------ prep: one slot's window
 
 // The bytes (and cut-mask bytes) of a window, in registers: lane l holds bytes
@@ -627,25 +684,46 @@ __device__ bool prep_window(GroupLDS<CH, G> &L, uint8_t *gw, const WinRegs<CH> &
         const unsigned incl = wave_incl_scan_add(v);
         const unsigned tot = __builtin_amdgcn_readlane(incl, 63);
         const unsigned ex = incl - v;
-        unsigned ai = n_atoms + (ex & 0x1FFu);
+        const unsigned ai0 = n_atoms + (ex & 0x1FFu);
         unsigned wi = n_words + ((ex >> 9) & 0x1FFu);
-        unsigned cp = cp_tot + (ex >> 18);
+        const unsigned cp0 = cp_tot + (ex >> 18);
         if (c0 + lane * 4 < wlen) *reinterpret_cast<uint32_t *>(&L.bytes[c0 + lane * 4]) = W.t[c];
+        // the lane's atoms and their code-point prefixes, then the stores in an order rotated by
+        // lane / 8 (ASCII: atom index 4 lane + u, so in order lanes 8 apart hit one bank -- see A0)
+        unsigned aiu[4], cpu[4];
+        {
+            unsigned ai = ai0, cp = cp0;
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                aiu[u] = ai; cpu[u] = cp;
+                ai += ast[u] ? 1u : 0u;
+                cp += cpl[u];
+            }
+        }
+        const unsigned rot = (G == 16 && PREP_ROT) ? (lane >> 3) & 3u : 0u;
 #pragma unroll
         for (int u = 0; u < 4; u++) {
-            const unsigned k = c0 + lane * 4 + u;
-            if (ast[u]) {
-                L.aoff[ai] = (typename GroupLDS<CH, G>::Idx)k;
+            const unsigned uu = ((unsigned)u + rot) & 3u;
+            // (selects over the four registers: a variable index would put the arrays in scratch)
+            const unsigned a_ = uu == 0 ? aiu[0] : (uu == 1 ? aiu[1] : (uu == 2 ? aiu[2] : aiu[3]));
+            const unsigned c_ = uu == 0 ? cpu[0] : (uu == 1 ? cpu[1] : (uu == 2 ? cpu[2] : cpu[3]));
+            const bool as_ = uu == 0 ? ast[0] : (uu == 1 ? ast[1] : (uu == 2 ? ast[2] : ast[3]));
+            const bool ws_ = uu == 0 ? wst[0] : (uu == 1 ? wst[1] : (uu == 2 ? wst[2] : wst[3]));
+            const unsigned k = c0 + lane * 4 + uu;
+            if (as_) {
+                L.aoff[a_] = (typename GroupLDS<CH, G>::Idx)k;
                 if constexpr (G == 16)   // end masks start all-dead (inverted); phase A clears token bits
-                    reinterpret_cast<uint32_t *>(L.rec)[ai] = 0xFFFF0000u | cp | (wst[u] ? CP_WS : 0u);
+                    reinterpret_cast<uint32_t *>(L.rec)[a_] = 0xFFFF0000u | c_ | (ws_ ? CP_WS : 0u);
                 else
-                    L.rec[ai].cpos = (uint16_t)(cp | (wst[u] ? CP_WS : 0));
-                // (the 256-byte pass's word list lives in global scratch and is needed only by row-mode
-                // windows: C0 rebuilds it there -- a store here would hold phase A's first loads back)
-                if (wst[u]) { if constexpr (!GroupLDS<CH, G>::WSLG) L.set_word_start(gw, wi, ai); wi++; }
-                ai++;
+                    L.rec[a_].cpos = (uint16_t)(c_ | (ws_ ? CP_WS : 0));
             }
-            cp += cpl[u];
+        }
+        // (the 256-byte pass's word list lives in global scratch and is needed only by row-mode
+        // windows: C0 rebuilds it there -- a store here would hold phase A's first loads back)
+        if constexpr (!GroupLDS<CH, G>::WSLG) {
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                if (ast[u] && wst[u]) { L.set_word_start(gw, wi, aiu[u]); wi++; }
         }
         n_atoms += tot & 0x1FFu;
         n_words += (tot >> 9) & 0x1FFu;
@@ -1124,10 +1202,15 @@ tokenize_kernel(KernArgs ka) {
                         // end k0+1+u: tk1 bit u, and tk2 bit u-1 (u = 0: the previous lane's bit 3)
                         const unsigned t2e = ((tk2 << 1) & 0xEu) | wave_shift_in((tk2 >> 3) & 1u, 0u);
                         if (ballot((tk1 | t2e) != 0)) {
+                            // lane l's dwords are 4l+1 .. 4l+4: in order, lanes l, l+8, l+16, l+24 of a 32-lane
+                            // group hit one bank (4-way, 2x on a store); rotated by (l / 8) % 4 no two do
+                            const unsigned rot = LDS_ROT ? (lane >> 3) & 3u : 0u;
 #pragma unroll
-                            for (int u = 0; u < 4; u++)
-                                __hip_atomic_fetch_and(&r32[k0 + 1u + (unsigned)u], ~((((tk1 >> u) & 1u) << 16) | (((t2e >> u) & 1u) << 17)),
+                            for (int u = 0; u < 4; u++) {
+                                const unsigned uu = ((unsigned)u + rot) & 3u;
+                                __hip_atomic_fetch_and(&r32[k0 + 1u + uu], ~((((tk1 >> uu) & 1u) << 16) | (((t2e >> uu) & 1u) << 17)),
                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            }
                         }
                         if (ballot(nocap) && lane == 0) SS[g].capb = 1;
                         // the slot's marked atoms, in order, into its fin[] (free until phase B)
@@ -1978,7 +2061,7 @@ tokenize_kernel(KernArgs ka) {
             auto hash_pass = [&](unsigned n, auto src) -> unsigned {
                 const uint8_t *hbase = reinterpret_cast<const uint8_t *>(tv.pair16) + TOKHASH_OFFSET;
                 const TokHashHeader hh = *reinterpret_cast<const TokHashHeader *>(hbase);
-                if (!C2_HASH || !hh.max_probe || G != 16) {   // 64-lane rows: the walkers (BLOOM-scale: -3.5 % with it)
+                if (!C2_HASH || !hh.max_probe) {
                     for (unsigned i = lane; i < n; i += 64u) list_ref(i) = (uint16_t)src(i);
                     return n;
                 }
@@ -2000,12 +2083,18 @@ tokenize_kernel(KernArgs ka) {
                     const unsigned j1 = k + 1 < q.ntk ? nx : q.na;
                     const unsigned p0 = L.aoff[jj];
                     const unsigned nbytes = (typename GL::Idx)(L.aoff[j1] - p0);
-                    uint32_t w[4];
-                    unsigned E = 0;
-                    const bool hashed = in && token_key<CH>(L.bytes, p0, nbytes, raw, (raw ? 1u : 0u) & q.fw & (unsigned)(jj == 0), w, E);
+                    const unsigned fa = (raw ? 1u : 0u) & q.fw & (unsigned)(jj == 0);
+                    uint32_t h = 0, fp = 0;
+                    bool hashed;
+                    if constexpr (G == 16) {
+                        uint32_t w[4];
+                        unsigned E = 0;
+                        hashed = in && token_key<CH>(L.bytes, p0, nbytes, raw, fa, w, E);
+                        if (hashed) tokhash(w[0], w[1], w[2], w[3], E, hh.seed, h, fp);
+                    } else {   // 64-lane rows (BLOOM-scale vocabularies): keys of up to 64 bytes
+                        hashed = in && token_hash_long<CH>(L.bytes, p0, nbytes, raw, fa, hh.seed, h, fp);
+                    }
                     if (hashed) {
-                        uint32_t h, fp;
-                        tokhash(w[0], w[1], w[2], w[3], E, hh.seed, h, fp);
                         int32_t idv = -1;
                         unsigned b = h & hh.mask;
                         for (unsigned pr = 0; pr < hh.max_probe; pr++) {

@@ -8,7 +8,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 out=gpurun_out/$1; N=$2; GEN=$3; shift 3; mkdir -p $out
 [ "$GEN" != ascii ] && { timeout -k 10 300 python3 tools/prof_driver.py $N 1 $GEN gen-only || exit 1; }
-CTRS="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES"
+CTRS="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES"
 for lib in "$@"; do
   tag=$(basename $(dirname $lib))
   DPT_LIB=$PWD/$lib timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $out/$tag/trace -o run --output-format csv -- python3 tools/prof_driver.py $N 4 $GEN > $out/$tag.trace.log 2>&1 || { tail -5 $out/$tag.trace.log; exit 1; }
@@ -16,7 +16,7 @@ for lib in "$@"; do
   echo "== $tag"
   python3 tools/pmc_summary.py $out/$tag | grep -A12 "kernel<256"
 done
-if [ -f dp-tokenization_amd/csrc/build/libdpt_stamps.so ]; then
+if [ -f dp-tokenization_amd/csrc/build/libdpt_stamps.so ] && [ "$GEN" != bloom ]; then
   timeout -k 10 120 python3 tools/stamps.py $N 256 $GEN > $out/stamps.log 2>&1 || { tail -5 $out/stamps.log; exit 1; }
   cat $out/stamps.log
 fi

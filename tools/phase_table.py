@@ -20,9 +20,10 @@ for line in open(sys.argv[1]):
     if m and kern:
         cur[m.group(1)] = float(m.group(2))
 prev = 0.0
-print("%-22s %8s %8s %9s %9s %9s" % ("build", "ms", "+ms", "VALU(G)", "SALU(G)", "LDS(G)"))
+print("%-22s %8s %8s %9s %9s %9s %10s" % ("build", "ms", "+ms", "VALU(G)", "SALU(G)", "LDS(G)", "LDSconf(G)"))
 for r in rows:
     ms = r.get("ns", 0) / 1e6
-    print("%-22s %8.3f %8.3f %9.3f %9.3f %9.3f" % (names.get(r["tag"], r["tag"]), ms, ms - prev, r.get("SQ_INSTS_VALU", 0) / 1e9,
-                                                r.get("SQ_INSTS_SALU", 0) / 1e9, r.get("SQ_INSTS_LDS", 0) / 1e9))
+    print("%-22s %8.3f %8.3f %9.3f %9.3f %9.3f %10.3f" % (names.get(r["tag"], r["tag"]), ms, ms - prev, r.get("SQ_INSTS_VALU", 0) / 1e9,
+                                                r.get("SQ_INSTS_SALU", 0) / 1e9, r.get("SQ_INSTS_LDS", 0) / 1e9,
+                                                r.get("SQ_LDS_BANK_CONFLICT", 0) / 1e9))
     prev = ms
