@@ -39,7 +39,10 @@ def _engine_for(vocabulary) -> Encoder:
     """The engine of a vocabulary (set, dict or list of token strings; non-strings and '' are not
     tokens).  Looked up by object identity + size first (O(1) for the callers that pass the same
     vocabulary every call), then by content (O(|V|), e.g. a set rebuilt per call), and built and
-    uploaded only for a vocabulary not seen before."""
+    uploaded only for a vocabulary not seen before.  Restriction: a vocabulary object changed IN PLACE
+    without a change of size (one token swapped for another) hits the identity entry and is not
+    re-read -- pass a new object (or a frozenset) after such a change; the reference re-reads its
+    ``vocabulary`` on every call (dp_tokenize.py:39)."""
     key_id = (id(vocabulary), len(vocabulary))
     hit = _BY_ID.get(key_id)
     if hit is not None and hit[0] is vocabulary:
