@@ -764,12 +764,15 @@ static_assert(NPART >= 1 && NPART <= NPART_MAX, "NPART");
 #ifndef A_REFILL
 #define A_REFILL 32   // phase A: idle lanes needed before a batched refill (1/8/16/32 within 2 %)
 #endif
-#ifndef DPT_DOUBLE   // diagnostic builds only: run one phase twice to measure its marginal cost
+#ifndef DPT_DOUBLE   // diagnostic builds only: run one phase twice to measure its marginal cost (1 A, 3 C1, 4 C2, 5 prep)
 #define DPT_DOUBLE 0
 #endif
 #ifndef DPT_STOP     // diagnostic builds only (wrong results): 1 = prep only, 21 = + A0, 2 = + A, 25 / 26 / 27 =
                      // + lane-mode B's cut points / recurrence / transfer scan + fix-up, 3 = + B/C0/C1
 #define DPT_STOP 9
+#endif
+#ifndef DPT_C2STOP   // diagnostic builds only (wrong results): C2 stops after its bulk pass (1) / hash pass (2)
+#define DPT_C2STOP 0
 #endif
 #define DPT_RUN_B (DPT_STOP >= 3 && DPT_STOP != 21)
 #define DPT_RUN_C2 (DPT_STOP == 9)
@@ -971,6 +974,25 @@ tokenize_kernel(KernArgs ka) {
 #pragma unroll
             for (int g = 0; g < NG; g++) todo |= (uni(SS[g].active) && !((prepared >> g) & 1u)) ? (1u << g) : 0u;
             if (!todo) break;
+#if DPT_DOUBLE == 5   // diagnostic: the slots' loads and prep once more, results dropped
+            {
+                WinRegs<CH> W[NG];
+#pragma unroll
+                for (int g = 0; g < NG; g++) {
+                    if (!((todo >> g) & 1u)) continue;
+                    const uint64_t sb = uni64(SS[g].sb);
+                    load_window<CH>(W[g], a.text + sb, raw ? nullptr : a.cut_mask + sb, uni64(SS[g].pos), uni64(SS[g].slen), raw, lane);
+                }
+#pragma unroll
+                for (int g = 0; g < NG; g++) {
+                    if (!((todo >> g) & 1u)) continue;
+                    unsigned wlen = 0, na = 0, nw = 0;
+                    if (uni(SS[g].status) != 2 && window_bounds<CH>(W[g], uni64(SS[g].slen), uni64(SS[g].pos), mode, lane, wlen))
+                        prep_window<CH, G, WIDE>(grp(g), wsl_of(g), W[g], uni64(SS[g].pos), wlen, mode, lane, na, nw);
+                }
+                wave_sync();
+            }
+#endif
             WinRegs<CH> W[NG];
 #pragma unroll
             for (int g = 0; g < NG; g++) {
@@ -1060,7 +1082,8 @@ tokenize_kernel(KernArgs ka) {
             // atoms matched so far (len), the trie node, the expanded bytes left of the current atom
             // (seq, cnt) and its descriptor (info).  Finished walks take the next start (ballot +
             // mbcnt), so the wave stays busy.
-            unsigned j = 0, lbase = 0, len = 0, cnt = 0, info = 0, t2 = 0;
+            unsigned j = 0, lbase = 0, len = 0, cnt = 0, info = 0, t2 = 0, gsel = 0;
+            unsigned capm = 0;   // bit g: slot g's capb (set after the walks)
             bool split = false;
             int32_t nb = tv.root_base, node = 0;
             uint64_t seq = 0;
@@ -1080,6 +1103,7 @@ tokenize_kernel(KernArgs ka) {
             };
             auto start_gj = [&](unsigned gs, unsigned jj) {
                 j = jj;
+                gsel = gs;
                 lbase = gs * (unsigned)group_lds_bytes<CH, G>();
                 const GL &L = *reinterpret_cast<const GL *>(smem + lbase);
                 info = ainfo_get(L, j, raw && ((fwmask >> gs) & 1u));
@@ -1226,6 +1250,9 @@ tokenize_kernel(KernArgs ka) {
                     }
                 }
             }
+#ifndef A_SCHED
+#define A_SCHED 1   // A/B knob: 0 = no scheduling barrier between the ASCII walker's byte read and trie load
+#endif
 #ifndef A_FAST
 #define A_FAST 1   // A/B knob: 0 = the generic walker takes A0's marked starts too
 #endif
@@ -1251,6 +1278,7 @@ tokenize_kernel(KernArgs ka) {
                     const unsigned nsl = tv.n_slots;
                     constexpr uint64_t NL5 = 0x3E41307830ull;   // "0x0A>" after the '<'
                     unsigned fj = 0, flen = 0, fp = 0, fwl = 0, cur = 0, pc = 0, fgs = 0, fl = 0, isr = 0, one = 0;
+                    // (the walker's "capb" flags, per lane and slot, written once after the walk)
                     uint64_t pend = 0;
                     int32_t fnode = 0, fnb = 0, ft2 = 0;
                     bool act = false;
@@ -1315,7 +1343,7 @@ tokenize_kernel(KernArgs ka) {
                                     const unsigned uu = nxt + __builtin_amdgcn_mbcnt_hi((unsigned)(im >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)im, 0u));
                                     if (uu < ftotal) {
                                         act = fstart(uu);
-                                        if (!act && !one) SS[fgs].capb = 1;   // the start atom is no token
+                                        capm |= (unsigned)(!act && !one) << fgs;   // the start atom is no token
                                     }
                                 }
                                 nxt += nidle;
@@ -1327,12 +1355,18 @@ tokenize_kernel(KernArgs ka) {
                             continue;
                         }
                         // the next raw byte, read before the trie load returns (masked off past the window)
+                        // (kept ahead of the load: else its address register may reuse the load's dead .z
+                        // and wait for it)
                         const unsigned nbv = grp_bytes_at(fl, fp);
+                        if (A_SCHED) __builtin_amdgcn_sched_barrier(0);
                         const int32_t t = isr ? ft2 : fnb + (int32_t)cur;
                         const int4 ent = trie_slotA(tv, t);
                         const unsigned y = (unsigned)ent.y;
                         const unsigned av = act ? 1u : 0u;
-                        const unsigned ok = av & (isr ? (((y >> 30) & 1u) & (unsigned)((y & 0x3FFFFFFFu) != 0)) : (unsigned)(ent.y == fnode));
+                        // (both lookups' tests as 0/1 integers: a ?: over them became an exec-mask diamond)
+                        const unsigned okr = ((y >> 30) & 1u) & (unsigned)((y & 0x3FFFFFFFu) != 0);
+                        const unsigned okp = (unsigned)(ent.y == fnode);
+                        const unsigned ok = av & ((isr & okr) | ((isr ^ 1u) & okp));
                         fnode = isr ? (int32_t)(y & 0x3FFFFFFFu) : t;
                         fnb = ent.x & BASE_MASK;
                         const unsigned leaf = ((unsigned)ent.x >> 30) & 1u;
@@ -1358,10 +1392,8 @@ tokenize_kernel(KernArgs ka) {
                         fp += nxa;
                         const unsigned nochild = (((unsigned)ent.w >> child_bit(cur)) & 1u) ^ 1u;
                         const unsigned done = av & ((ok ^ 1u) | leaf | stop | nochild);
-                        if (done) {
-                            if (!one) SS[fgs].capb = 1;
-                            act = false;
-                        }
+                        capm |= (done & (one ^ 1u)) << fgs;
+                        act = act && !done;
                     }
                 }
             }
@@ -1446,13 +1478,19 @@ tokenize_kernel(KernArgs ka) {
                 // node has no child for the next byte (over without that lookup)
                 const unsigned nochild = (((unsigned)ent.w >> child_bit((unsigned)(seq & 0xFFu))) & 1u) ^ 1u;
                 const unsigned done = act & ((ok ^ 1u) | (aend ? ((cont ^ 1u) | nochild) : (leaf | nochild)));
-                if (done) {
-                    GL &L = *reinterpret_cast<GL *>(smem + lbase);
-                    if constexpr (G != 16) L.rec[j].smask = mask;   // G = 16: end masks, set by end_token
-                    if (!(mask & 1u)) SS[lbase / (unsigned)group_lds_bytes<CH, G>()].capb = 1;
-                    active = false;
+                if constexpr (G != 16) {
+                    if (done) {
+                        GL &L = *reinterpret_cast<GL *>(smem + lbase);
+                        L.rec[j].smask = mask;   // G = 16: end masks, set by end_token
+                    }
                 }
+                capm |= (done & (((unsigned)mask & 1u) ^ 1u)) << gsel;
+                active = active && !done;
             }
+            // the slots whose walk found an atom that is no token by itself
+#pragma unroll
+            for (int g = 0; g < NG; g++)
+                if (ballot((capm >> g) & 1u) && lane == 0) SS[g].capb = 1;
         }
 #if DPT_DOUBLE == 1
         }
@@ -1463,6 +1501,30 @@ tokenize_kernel(KernArgs ka) {
 
         // ---------------------------------------------------------- B: forward recurrence
         KREFRESH();
+#ifndef PF_NEXT
+#define PF_NEXT 0   // A/B knob: the next windows of continuing strings pulled into L2 during B (1) / B and C1 (2)
+#endif
+        // B and C1 issue no vector-memory loads (16-lane rows), so a load issued here waits for nothing
+        // and holds nothing up: one dword per 128-byte line of each continuing slot's next window,
+        // so that the next prep's window load hits L2 instead of HBM.  (Inline asm: a compiler-visible
+        // load may be sunk next to its only use; the compiler's waitcnts stay correct -- vmcnt returns
+        // in issue order, so its waits for later loads also cover this one -- and the register is held
+        // until the explicit wait at the end of B or C1.)
+        uint32_t pfv = 0;
+        if constexpr (PF_NEXT && G == 16 && !BIG) {
+            if (lane < 3u * (unsigned)NG) {
+                const unsigned g = lane / 3u, k = lane - 3u * g;
+                const SlotState &S = SS[g];
+                const uint64_t np = (uint64_t)S.pos + S.wlen;
+                if (S.active && S.n_atoms > 0 && np < S.slen) {
+                    uint64_t off = (uint64_t)S.sb + np + 128u * k;
+                    const uint64_t last = (uint64_t)S.sb + S.slen - 1u;
+                    off = (off < last ? off : last) & ~(uint64_t)3;
+                    const uint8_t *p = a.text + off;
+                    asm volatile("global_load_dword %0, %1, off" : "=v"(pfv) : "v"(p));
+                }
+            }
+        }
         bool lane_mode = false;   // B ran per chunk and did C0 and C1 itself (G = 16, capless, no edges)
         if (DPT_RUN_B) {
             GL &L = grp(mg);
@@ -1858,6 +1920,7 @@ tokenize_kernel(KernArgs ka) {
             }
         }
         wave_sync();
+        if constexpr (PF_NEXT == 1 && G == 16 && !BIG) asm volatile("s_waitcnt vmcnt(0)" : : "v"(pfv));
         STAMP(2);
         PRIO_PHASE(2);
 
@@ -1983,6 +2046,7 @@ tokenize_kernel(KernArgs ka) {
         }
 #endif
         wave_sync();
+        if constexpr (PF_NEXT == 2 && G == 16 && !BIG) asm volatile("s_waitcnt vmcnt(0)" : : "v"(pfv));
         STAMP(3);
         PRIO_PHASE(3);
 
@@ -2067,50 +2131,80 @@ tokenize_kernel(KernArgs ka) {
                 }
                 const __amdgpu_buffer_rsrc_t hr = __builtin_amdgcn_make_buffer_rsrc(
                     (void *)(hbase + sizeof(TokHashHeader)), (short)0, (int)((hh.mask + 1u) * 16u), 0x00020000);
+#ifndef HP_U
+#define HP_U 2   // A/B knob: token rounds of 64 per hash-pass iteration (their loads before any store: a load
+                 // waits for every older store of the wave)
+#endif
                 unsigned r2 = 0;
-                for (unsigned i0 = 0; i0 < n; i0 += 64u) {
-                    const unsigned i = i0 + lane;
-                    const bool in = i < n;
-                    const unsigned t = in ? src(i) : 0u;
-                    unsigned g = 0;
+                for (unsigned i0 = 0; i0 < n; i0 += 64u * HP_U) {
+                    unsigned tt[HP_U], hh2[HP_U], fpv[HP_U];
+                    uint64_t oqv[HP_U];
+                    bool hs[HP_U], inr[HP_U];
 #pragma unroll
-                    for (int k = 1; k < NG; k++) g += t >= pre[k] ? 1u : 0u;
-                    const GL &L = *reinterpret_cast<const GL *>(smem + g * (unsigned)group_lds_bytes<CH, G>());
-                    const C2Slot q = *reinterpret_cast<const C2Slot *>(&L.fin[0]);
-                    const unsigned k = in ? t - q.base : 0u;
-                    const unsigned jj = (unsigned)L.rec[k].smask;
-                    const unsigned nx = (unsigned)L.rec[k + 1].smask;   // k + 1 <= ntk < NA
-                    const unsigned j1 = k + 1 < q.ntk ? nx : q.na;
-                    const unsigned p0 = L.aoff[jj];
-                    const unsigned nbytes = (typename GL::Idx)(L.aoff[j1] - p0);
-                    const unsigned fa = (raw ? 1u : 0u) & q.fw & (unsigned)(jj == 0);
-                    uint32_t h = 0, fp = 0;
-                    bool hashed;
-                    if constexpr (G == 16) {
-                        uint32_t w[4];
-                        unsigned E = 0;
-                        hashed = in && token_key<CH>(L.bytes, p0, nbytes, raw, fa, w, E);
-                        if (hashed) tokhash(w[0], w[1], w[2], w[3], E, hh.seed, h, fp);
-                    } else {   // 64-lane rows (BLOOM-scale vocabularies): keys of up to 64 bytes
-                        hashed = in && token_hash_long<CH>(L.bytes, p0, nbytes, raw, fa, hh.seed, h, fp);
-                    }
-                    if (hashed) {
-                        int32_t idv = -1;
-                        unsigned b = h & hh.mask;
-                        for (unsigned pr = 0; pr < hh.max_probe; pr++) {
-                            const auto e = __builtin_amdgcn_raw_buffer_load_b128(hr, b * 16u, 0, 0);
-                            if (e[0] == fp) { idv = (int32_t)e[1]; break; }
-                            if (e[2] == fp) { idv = (int32_t)e[3]; break; }
-                            b = (b + 1u) & hh.mask;
+                    for (int u = 0; u < HP_U; u++) {
+                        const unsigned i = i0 + 64u * (unsigned)u + lane;
+                        const bool in = i < n;
+                        const unsigned t = in ? src(i) : 0u;
+                        unsigned g = 0;
+#pragma unroll
+                        for (int k = 1; k < NG; k++) g += t >= pre[k] ? 1u : 0u;
+                        const GL &L = *reinterpret_cast<const GL *>(smem + g * (unsigned)group_lds_bytes<CH, G>());
+                        const C2Slot q = *reinterpret_cast<const C2Slot *>(&L.fin[0]);
+                        const unsigned k = in ? t - q.base : 0u;
+                        const unsigned jj = (unsigned)L.rec[k].smask;
+                        const unsigned nx = (unsigned)L.rec[k + 1].smask;   // k + 1 <= ntk < NA
+                        const unsigned j1 = k + 1 < q.ntk ? nx : q.na;
+                        const unsigned p0 = L.aoff[jj];
+                        const unsigned nbytes = (typename GL::Idx)(L.aoff[j1] - p0);
+                        const unsigned fa = (raw ? 1u : 0u) & q.fw & (unsigned)(jj == 0);
+                        uint32_t h = 0, fp = 0;
+                        bool hashed;
+                        if constexpr (G == 16) {
+                            uint32_t w[4];
+                            unsigned E = 0;
+                            hashed = in && token_key<CH>(L.bytes, p0, nbytes, raw, fa, w, E);
+                            if (hashed) tokhash(w[0], w[1], w[2], w[3], E, hh.seed, h, fp);
+                        } else {   // 64-lane rows (BLOOM-scale vocabularies): keys of up to 64 bytes
+                            hashed = in && token_hash_long<CH>(L.bytes, p0, nbytes, raw, fa, hh.seed, h, fp);
                         }
-                        if (n16) a.staging16[q.ob + k] = (int16_t)idv;
-                        else a.staging[q.ob + k] = idv;
+                        tt[u] = t; hh2[u] = h & hh.mask; fpv[u] = fp; oqv[u] = q.ob + k; hs[u] = hashed; inr[u] = in;
                     }
-                    // every lane read its entry above (a list source): the compacted rest lands below i0 + 64
-                    const bool rest = in && !hashed;
-                    const uint64_t m = ballot(rest);
-                    if (rest) list_ref(r2 + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u))) = (uint16_t)t;
-                    r2 += (unsigned)__builtin_popcountll(m);
+                    // every round's first probe, then the rare further probes, then the stores
+                    int32_t idv[HP_U];
+#pragma unroll
+                    for (int u = 0; u < HP_U; u++) {
+                        const auto e = __builtin_amdgcn_raw_buffer_load_b128(hr, hh2[u] * 16u, 0, 0);
+                        idv[u] = e[0] == fpv[u] ? (int32_t)e[1] : (e[2] == fpv[u] ? (int32_t)e[3] : INT32_MIN);
+                    }
+#pragma unroll
+                    for (int u = 0; u < HP_U; u++) {
+                        if (hs[u] && idv[u] == INT32_MIN) {
+                            int32_t v = -1;
+                            unsigned b = hh2[u];
+                            for (unsigned pr = 1; pr < hh.max_probe; pr++) {
+                                b = (b + 1u) & hh.mask;
+                                const auto e = __builtin_amdgcn_raw_buffer_load_b128(hr, b * 16u, 0, 0);
+                                if (e[0] == fpv[u]) { v = (int32_t)e[1]; break; }
+                                if (e[2] == fpv[u]) { v = (int32_t)e[3]; break; }
+                            }
+                            idv[u] = v;
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < HP_U; u++) {
+                        if (hs[u]) {
+                            if (n16) a.staging16[oqv[u]] = (int16_t)idv[u];
+                            else a.staging[oqv[u]] = idv[u];
+                        }
+                    }
+                    // every lane read its entries above (list sources): the compacted rest lands below i0 + 64 * HP_U
+#pragma unroll
+                    for (int u = 0; u < HP_U; u++) {
+                        const bool rest = inr[u] && !hs[u];
+                        const uint64_t m = ballot(rest);
+                        if (rest) list_ref(r2 + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u))) = (uint16_t)tt[u];
+                        r2 += (unsigned)__builtin_popcountll(m);
+                    }
                 }
                 return r2;
             };
@@ -2224,10 +2318,12 @@ tokenize_kernel(KernArgs ka) {
                     }
                 }
                 wave_sync();
+                if (DPT_C2STOP == 1) r = 0;   // diagnostic: the bulk pass only
                 if (r > 0) {
                     r = hash_pass(r, [&](unsigned i) -> unsigned { return list_ref(i); });
                     wave_sync();
                 }
+                if (DPT_C2STOP == 2) r = 0;   // diagnostic: + the hash pass
                 wend = r;
                 if (r > 0 && r < (unsigned)PEND_CAP) {
                     uint4 ent = make_uint4(0u, 0u, 0u, 0u);
@@ -2678,11 +2774,14 @@ static_assert(block_lds_bytes<SMALL_CH, 16>() <= 64 * 1024, "small LDS");
 static_assert(block_lds_bytes<SMALL_CH, 64>() <= 64 * 1024, "small LDS");
 static_assert(block_lds_bytes<BIG_CH, 64>() <= 160 * 1024, "big LDS");
 
+constexpr int MAX_DEVICES = 64;
 // Resident waves per CU for an instantiation (LDS / VGPR limited); DPT_WAVES_PER_CU overrides.
 template <int CH, int G, bool BIG, bool WIDE, int SW = 0, bool RAW = false>
 static unsigned resident_per_cu() {
-    static unsigned cached = 0;
-    if (cached) return cached;
+    static unsigned cached[MAX_DEVICES] = {};   // per device: a process may drive several
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAX_DEVICES) dev = 0;
+    if (cached[dev]) return cached[dev];
     int nb = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, tokenize_kernel<CH, G, BIG, WIDE, SW, RAW>, 64, block_lds_bytes<CH, G>()) != hipSuccess || nb <= 0)
         nb = 8;
@@ -2690,8 +2789,8 @@ static unsigned resident_per_cu() {
         const int v = atoi(e);
         if (v > 0) nb = v;
     }
-    cached = (unsigned)nb;
-    return cached;
+    cached[dev] = (unsigned)nb;
+    return cached[dev];
 }
 
 // Persistent grid: every resident wave pulls strings from the work counter until it runs dry.
@@ -2850,8 +2949,11 @@ hipError_t launch_histogram(const uint64_t *id_off, const int32_t *status, uint6
 }
 
 hipError_t kernel_init() {
-    static bool done = false;
-    if (done) return hipSuccess;
+    // function attributes are per device: set them once on each device a call runs on
+    static bool done[MAX_DEVICES] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAX_DEVICES) dev = 0;
+    if (done[dev]) return hipSuccess;
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&tokenize_kernel<BIG_CH, 64, true, false>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, block_lds_bytes<BIG_CH, 64>());
     if (e == hipSuccess)
@@ -2860,7 +2962,7 @@ hipError_t kernel_init() {
     if (e == hipSuccess)
         e = hipFuncSetAttribute(reinterpret_cast<const void *>(&tokenize_kernel<BIG_CH, 64, true, true>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, block_lds_bytes<BIG_CH, 64>());
-    if (e == hipSuccess) done = true;
+    if (e == hipSuccess) done[dev] = true;
     return e;
 }
 
