@@ -326,9 +326,9 @@ __device__ unsigned g_lanedbg[16 * 16 + 4];
 #ifdef DPT_STAMPS
 // diagnostic build only: cycles per phase summed over waves (never in the product build)
 __device__ unsigned long long g_stamps[8];
-#define STAMP_DECL unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}; unsigned long long st_prev = __builtin_amdgcn_s_memtime();
+#define STAMP_DECL unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; unsigned long long st_prev = __builtin_amdgcn_s_memtime();
 #define STAMP(k) do { const unsigned long long _t = __builtin_amdgcn_s_memtime(); st_acc[k] += _t - st_prev; st_prev = _t; } while (0)
-#define STAMP_FLUSH do { if (lane == 0) for (int _k = 0; _k < 6; _k++) atomicAdd(&g_stamps[_k], st_acc[_k]); } while (0)
+#define STAMP_FLUSH do { if (lane == 0) for (int _k = 0; _k < 8; _k++) atomicAdd(&g_stamps[_k], st_acc[_k]); } while (0)
 #else
 #define STAMP_DECL
 #define STAMP(k)
@@ -770,6 +770,9 @@ static_assert(NPART >= 1 && NPART <= NPART_MAX, "NPART");
 #ifndef DPT_STOP     // diagnostic builds only (wrong results): 1 = prep only, 21 = + A0, 2 = + A, 25 / 26 / 27 =
                      // + lane-mode B's cut points / recurrence / transfer scan + fix-up, 3 = + B/C0/C1
 #define DPT_STOP 9
+#endif
+#ifndef DPT_NOSTORE   // diagnostic builds only (wrong results): C2's bulk pass (1) / hash pass (2) store no ids
+#define DPT_NOSTORE 0
 #endif
 #ifndef DPT_C2STOP   // diagnostic builds only (wrong results): C2 stops after its bulk pass (1) / hash pass (2)
 #define DPT_C2STOP 0
@@ -1253,6 +1256,9 @@ tokenize_kernel(KernArgs ka) {
 #ifndef A_SCHED
 #define A_SCHED 1   // A/B knob: 0 = no scheduling barrier between the ASCII walker's byte read and trie load
 #endif
+#ifndef A_ONEEDGE
+#define A_ONEEDGE 1   // A/B knob: 0 = the ASCII walker skips the step when no lane is active (two back edges)
+#endif
 #ifndef A_FAST
 #define A_FAST 1   // A/B knob: 0 = the generic walker takes A0's marked starts too
 #endif
@@ -1276,10 +1282,11 @@ tokenize_kernel(KernArgs ka) {
                     const unsigned wst = a.ws_id >= 0 ? 1u : 0u;   // '\u2581' alone is a token
                     const int32_t rb = tv.root_base;
                     const unsigned nsl = tv.n_slots;
-                    constexpr uint64_t NL5 = 0x3E41307830ull;   // "0x0A>" after the '<'
+                    // "<0x0A>" after its '<': with pc bytes left the next is byte 5 - pc of "0x0A>" (a 32-bit
+                    // constant and '>' instead of a 64-bit register pair of the bytes still to come)
+                    auto nl_byte = [](unsigned pc) -> unsigned { return pc >= 2u ? (0x41307830u >> (8u * (5u - pc))) & 0xFFu : 0x3Eu; };
                     unsigned fj = 0, flen = 0, fp = 0, fwl = 0, cur = 0, pc = 0, fgs = 0, fl = 0, isr = 0, one = 0;
                     // (the walker's "capb" flags, per lane and slot, written once after the walk)
-                    uint64_t pend = 0;
                     int32_t fnode = 0, fnb = 0, ft2 = 0;
                     bool act = false;
                     // a start: (walk state, or over at once -- the '\u2581' node missing / the word ends)
@@ -1297,13 +1304,13 @@ tokenize_kernel(KernArgs ka) {
                         fj = jj;
                         fwl = SS[gs].wlen;
                         const unsigned b0 = L.bytes[jj];
-                        isr = 0; one = 0; pc = 0; pend = 0;
+                        isr = 0; one = 0; pc = 0;
                         if (((fwmask >> gs) & 1u) && jj == 0) {   // '\u2581' + b0: one atom
                             fnode = wsn; fnb = wsb; cur = b0; fp = 1; flen = 0;
                             return wsn >= 0;
                         }
                         if (b0 == '\n') {
-                            fnode = 0; fnb = rb; cur = '<'; pend = NL5; pc = 5; fp = jj + 1; flen = 0;
+                            fnode = 0; fnb = rb; cur = '<'; pc = 5; fp = jj + 1; flen = 0;
                             return true;
                         }
                         if (b0 != ' ') {   // a "more" start: the root table over (b0, next byte)
@@ -1311,12 +1318,12 @@ tokenize_kernel(KernArgs ka) {
                             isr = 1; one = 1;
                             if (n1 == '\n') {   // inside atom jj+1's "<0x0A>" after its '<'
                                 ft2 = (int32_t)(nsl + (b0 << 8) + (unsigned)'<');
-                                flen = 1; cur = '0'; pend = NL5 >> 8; pc = 4; fp = jj + 2;
+                                flen = 1; cur = '0'; pc = 4; fp = jj + 2;
                             } else {             // two atoms; A0 saw a third that is no word start
                                 ft2 = (int32_t)(nsl + (b0 << 8) + n1);
                                 const unsigned n2 = L.bytes[jj + 2];
                                 flen = 2; fp = jj + 3;
-                                if (n2 == '\n') { cur = '<'; pend = NL5; pc = 5; }
+                                if (n2 == '\n') { cur = '<'; pc = 5; }
                                 else cur = n2;
                             }
                             return true;
@@ -1329,7 +1336,7 @@ tokenize_kernel(KernArgs ka) {
                         const unsigned n1 = L.bytes[jj + 1];
                         if (n1 == ' ') return false;
                         fp = jj + 2;
-                        if (n1 == '\n') { cur = '<'; pend = NL5; pc = 5; }
+                        if (n1 == '\n') { cur = '<'; pc = 5; }
                         else cur = n1;
                         return true;
                     };
@@ -1349,8 +1356,12 @@ tokenize_kernel(KernArgs ka) {
                                 nxt += nidle;
                             }
                         }
-                        // (a start can be over at once, so a refill may leave every lane idle with starts left)
-                        if (!ballot(act)) {
+                        // (a start can be over at once, so a refill may leave every lane idle with starts left:
+                        // the step then runs with no lane active and changes nothing -- one back edge, so
+                        // the walk state stays in its registers across it)
+                        if (A_ONEEDGE) {
+                            if (!ballot(act) && nxt >= ftotal) break;
+                        } else if (!ballot(act)) {
                             if (nxt >= ftotal) break;
                             continue;
                         }
@@ -1373,8 +1384,7 @@ tokenize_kernel(KernArgs ka) {
                         // plain step: cur consumed; the atom ends unless its expansion has bytes left
                         const unsigned aend = ok & (isr ^ 1u) & (unsigned)(pc == 0);
                         const unsigned inexp = (isr ^ 1u) & (unsigned)(pc != 0);
-                        cur = inexp ? (unsigned)(pend & 0xFFu) : cur;
-                        pend = inexp ? pend >> 8 : pend;
+                        cur = inexp ? nl_byte(pc) : cur;
                         pc = inexp ? pc - 1u : pc;
                         isr = 0;
                         flen += aend;
@@ -1387,7 +1397,6 @@ tokenize_kernel(KernArgs ka) {
                         const unsigned nxa = aend & (past ^ 1u);
                         const unsigned isnl = (unsigned)(nbv == '\n');
                         cur = nxa ? (isnl ? (unsigned)'<' : nbv) : cur;
-                        pend = (nxa & isnl) ? NL5 : pend;
                         pc = (nxa & isnl) ? 5u : pc;
                         fp += nxa;
                         const unsigned nochild = (((unsigned)ent.w >> child_bit(cur)) & 1u) ^ 1u;
@@ -2193,6 +2202,7 @@ tokenize_kernel(KernArgs ka) {
 #pragma unroll
                     for (int u = 0; u < HP_U; u++) {
                         if (hs[u]) {
+                            if (DPT_NOSTORE & 2) continue;   // diagnostic
                             if (n16) a.staging16[oqv[u]] = (int16_t)idv[u];
                             else a.staging[oqv[u]] = idv[u];
                         }
@@ -2300,7 +2310,7 @@ tokenize_kernel(KernArgs ka) {
                         for (int u = 0; u < 4; u++) pv[u] = tv.pair16[ix[u]];
 #pragma unroll
                         for (int u = 0; u < 4; u++)
-                            if (kind[u]) a.staging16[oq[u]] = pv[u];
+                            if (kind[u] && !(DPT_NOSTORE & 1)) a.staging16[oq[u]] = pv[u];
                         continue;
                     }
                     int4 ent[4];
@@ -2318,11 +2328,13 @@ tokenize_kernel(KernArgs ka) {
                     }
                 }
                 wave_sync();
+                STAMP(5);
                 if (DPT_C2STOP == 1) r = 0;   // diagnostic: the bulk pass only
                 if (r > 0) {
                     r = hash_pass(r, [&](unsigned i) -> unsigned { return list_ref(i); });
                     wave_sync();
                 }
+                STAMP(6);
                 if (DPT_C2STOP == 2) r = 0;   // diagnostic: + the hash pass
                 wend = r;
                 if (r > 0 && r < (unsigned)PEND_CAP) {
@@ -2460,6 +2472,7 @@ tokenize_kernel(KernArgs ka) {
         }
 #endif
         wave_sync();
+        STAMP(7);
 
         // ---------------------------------------------------------- advance slots, finish strings
         KREFRESH();

@@ -25,8 +25,8 @@ lib = _lib.lib()
 lib.dpt_debug_stamps(buf, 1)
 t0 = time.time(); enc.encode_csr(text, offs); dt = time.time() - t0
 lib.dpt_debug_stamps(buf, 0)
-names = ["prep", "A_match", "B_forward", "C1_select", "C2_ids+win", "tail"]
-tot = sum(buf[k] for k in range(6))
+names = ["prep", "A_match", "B_forward", "C0/C1_select", "finish", "C2_bulk", "C2_hash", "C2_pend+walk"]
+tot = sum(buf[k] for k in range(8))
 print(f"{gen} n={n} wall={dt*1e3:.1f} ms (host path incl. copies)")
-for k in range(6):
+for k in (0, 1, 2, 3, 5, 6, 7, 4):
     print(f"  {names[k]:12s} {buf[k]/tot*100:6.2f}%  {buf[k]/n:10.0f} cycles/string(wave)")
