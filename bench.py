@@ -379,9 +379,9 @@ def main():
         if pending[b] is not None:   # the stream waits for this buffer's previous all-reduce
             pending[b].wait()
             pending[b] = None
-        h.zero_()
-        # the histogram is folded into the encode's finish pass (dpt_ctx_set_histogram)
-        enc.set_histogram(h.data_ptr(), N_BINS)
+        # the histogram is folded into the encode's finish pass, which replaces h's contents
+        # (dpt_ctx_set_histogram_ex, DPT_HIST_OVERWRITE: no memset launch per step)
+        enc.set_histogram(h.data_ptr(), N_BINS, overwrite=True)
         enc.encode_device(d_text.data_ptr(), n_bytes, d_off.data_ptr(), M, d_ids.data_ptr(), max(n_bytes, 1),
                           d_idoff.data_ptr(), d_status.data_ptr(), stream=stream,
                           cut_ptr=d_cut.data_ptr() if bloom else 0, mode="atoms" if bloom else "raw")

@@ -54,6 +54,7 @@ struct dpt_ctx {
     // dpt_ctx_set_histogram: folded into the next encode's finish pass
     int64_t *hist = nullptr;
     uint32_t hist_bins = 0;
+    bool hist_overwrite = false;
     // profiling
     bool profile = false;
     std::vector<hipEvent_t> events;   // groups of 4 per call
@@ -130,8 +131,9 @@ int ensure_workspace(dpt_ctx *c, const dpt_vocab *v, uint64_t n_bytes, uint64_t 
     hipError_t e;
     bool fresh = false;   // zeroed buffers were (re)allocated
     const bool need16 = staging && (!v || v->ids16), need32 = staging && (!v || !v->ids16);
-    if (need16 && (e = grow(&c->staging16, &c->cap16, n_bytes)) != hipSuccess) return hip_fail(e, "hipMalloc(staging16)");
-    if (need32 && (e = grow(&c->staging32, &c->cap32, n_bytes)) != hipSuccess) return hip_fail(e, "hipMalloc(staging32)");
+    // (+8 elements: the finish pass reads staged ids as whole dwords, up to 2 elements past the last)
+    if (need16 && (e = grow(&c->staging16, &c->cap16, n_bytes + 8)) != hipSuccess) return hip_fail(e, "hipMalloc(staging16)");
+    if (need32 && (e = grow(&c->staging32, &c->cap32, n_bytes + 8)) != hipSuccess) return hip_fail(e, "hipMalloc(staging32)");
     // long_bytes = 0 (the encode path): the default size, unless the caller reserved the arena -- a
     // reserved arena is left alone, so a reserved call never reallocates (capture-safe, dpt.h)
     const uint64_t lb = long_bytes ? long_bytes : default_long_bytes(n_bytes);
@@ -522,7 +524,9 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
     p.pend = c->pend;
     p.hist = padded ? nullptr : c->hist;   // (dpt_encode_padded has no offsets to count)
     p.hist_bins = c->hist_bins;
+    p.hist_overwrite = c->hist_overwrite;
     c->hist = nullptr;                     // one call only
+    c->hist_overwrite = false;
     if (padded) {   // the ids go straight to their final place (int32), the counts to the caller's array
         p.staging = ids;
         p.staging16 = nullptr;
@@ -775,13 +779,17 @@ int dpt_token_histogram(const uint64_t *id_off, const int32_t *status, uint64_t 
     return DPT_OK;
 }
 
-int dpt_ctx_set_histogram(dpt_ctx *c, int64_t *hist, uint32_t n_bins) {
+int dpt_ctx_set_histogram_ex(dpt_ctx *c, int64_t *hist, uint32_t n_bins, int flags) {
     if (!c) return fail(DPT_E_ARG, "null ctx");
     if (hist && n_bins < 2) return fail(DPT_E_ARG, "n_bins < 2");
+    if (flags & ~DPT_HIST_OVERWRITE) return fail(DPT_E_ARG, "unknown histogram flags");
     c->hist = hist;
     c->hist_bins = hist ? n_bins : 0;
+    c->hist_overwrite = hist && (flags & DPT_HIST_OVERWRITE);
     return DPT_OK;
 }
+
+int dpt_ctx_set_histogram(dpt_ctx *c, int64_t *hist, uint32_t n_bins) { return dpt_ctx_set_histogram_ex(c, hist, n_bins, 0); }
 
 int dpt_ctx_profile(dpt_ctx *c, int enable) {
     if (!c) return fail(DPT_E_ARG, "null ctx");

@@ -1,6 +1,7 @@
 // Internal interface between the C-ABI (dpt_api.cpp) and the kernels (dpt_kernels.hip).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stddef.h>
 #include <stdint.h>
 
@@ -39,6 +40,7 @@ struct EncodeLaunch {
     uint4 *pend;             // 16-lane first pass: each wave's pending residual tokens (pend_scratch_bytes)
     int64_t *hist;           // nullable: the token-count histogram to add to in the finish pass (dpt_ctx_set_histogram)
     uint32_t hist_bins;
+    bool hist_overwrite;     // DPT_HIST_OVERWRITE: the call's histogram replaces hist (zeroed on the device first)
     uint8_t *arena;          // the unbounded pass's scratch: 20 bytes per input byte of the strings it takes
     uint64_t arena_cap;      // input bytes the arena holds
     // vocabulary
@@ -151,7 +153,7 @@ struct LongLaunch {
     int long_span;
     unsigned blocks;
 };
-void launch_long(const LongLaunch &p, hipStream_t stream);
+void launch_long(const LongLaunch &p, hipStream_t stream, hipEvent_t ev_stop = nullptr);
 
 hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t ev[2]);
 size_t wsl_scratch_bytes(unsigned max_blocks);

@@ -2588,7 +2588,11 @@ __device__ __forceinline__ void reset_counters(uint32_t *ctr) {
 // inside a persistent finish kernel, which chained the batches: a finish block could not start its
 // copy before its look-back, so each block took its batches one after another.
 __global__ void __launch_bounds__(SCAN_THREADS) batch_scan_kernel(uint64_t n_str, unsigned long long *bsum,
-                                                                  unsigned long long *bpre, uint32_t *ctr) {
+                                                                  unsigned long long *bpre, uint32_t *ctr,
+                                                                  unsigned long long *hist_zero, uint32_t n_hist) {
+    // DPT_HIST_OVERWRITE: the histogram the finish pass adds to starts from zero (stream order)
+    if (hist_zero)
+        for (uint32_t b = threadIdx.x; b < n_hist; b += SCAN_THREADS) hist_zero[b] = 0;
     __shared__ uint64_t s_w[SCAN_THREADS / 64];
     const unsigned tid = threadIdx.x;
     const uint64_t nb = (n_str + FIN_BATCH - 1) / FIN_BATCH;
@@ -2619,6 +2623,7 @@ struct FinishArgs {
     unsigned long long *bsum;         // one-batch calls (no scan kernel): zeroed here ...
     uint32_t *ctr;                    // ... and the counter block reset here (both null otherwise)
     unsigned long long *hist;         // nullable: the token-count histogram (dpt_ctx_set_histogram) ...
+    int hist_store;                   // ... stored, not added (DPT_HIST_OVERWRITE in a one-batch call) ...
     const int32_t *status;            // ... with the statuses it counts
     uint32_t n_bins;
 };
@@ -2678,8 +2683,10 @@ __global__ void __launch_bounds__(FIN_THREADS) finish_kernel(FinishArgs f) {
             lh[f.n_bins + 1] += (unsigned long long)(f.n_str - s0 < FIN_BATCH ? f.n_str - s0 : FIN_BATCH);
         }
         __syncthreads();
-        for (uint32_t b = tid; b < nbh; b += FIN_THREADS)
-            if (lh[b]) atomicAdd(&f.hist[b], lh[b]);
+        for (uint32_t b = tid; b < nbh; b += FIN_THREADS) {
+            if (f.hist_store) f.hist[b] = lh[b];   // the call's only batch
+            else if (lh[b]) atomicAdd(&f.hist[b], lh[b]);
+        }
     }
     if (sl == 0) {
         if (has) f.id_off[s0 + tid + 1] = o0 + incl;
@@ -2808,7 +2815,8 @@ static unsigned resident_per_cu() {
 
 // Persistent grid: every resident wave pulls strings from the work counter until it runs dry.
 template <int CH, int G, bool BIG, bool WIDE, int SW = 0, bool RAW = false>
-static void launch_tok(const EncodeArgs &a, const TrieView &tv, uint64_t n_units, unsigned n_cu, hipStream_t stream) {
+static void launch_tok(const EncodeArgs &a, const TrieView &tv, uint64_t n_units, unsigned n_cu, hipStream_t stream,
+                       hipEvent_t ev_start = nullptr) {
     constexpr int lds = block_lds_bytes<CH, G>();
     uint64_t wpc = resident_per_cu<CH, G, BIG, WIDE, SW, RAW>();
     if constexpr (G == 16 && !BIG) {
@@ -2822,7 +2830,11 @@ static void launch_tok(const EncodeArgs &a, const TrieView &tv, uint64_t n_units
     uint64_t blocks = (uint64_t)n_cu * wpc;
     if (blocks > (uint64_t)n_cu * 64u) blocks = (uint64_t)n_cu * 64u;   // the scratch is sized for 64 per CU
     if (blocks > n_units) blocks = n_units ? n_units : 1;
-    hipLaunchKernelGGL((tokenize_kernel<CH, G, BIG, WIDE, SW, RAW>), dim3((unsigned)blocks), dim3(64), lds, stream, KernArgs{a, tv});
+    if (ev_start)   // the start timestamp rides on the dispatch (a separate hipEventRecord left a ~6 us bubble)
+        hipExtLaunchKernelGGL((tokenize_kernel<CH, G, BIG, WIDE, SW, RAW>), dim3((unsigned)blocks), dim3(64), lds, stream,
+                              ev_start, nullptr, 0, KernArgs{a, tv});
+    else
+        hipLaunchKernelGGL((tokenize_kernel<CH, G, BIG, WIDE, SW, RAW>), dim3((unsigned)blocks), dim3(64), lds, stream, KernArgs{a, tv});
 }
 
 hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t ev[2]) {
@@ -2849,12 +2861,14 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
             const hipError_t e0 = hipMemsetAsync(p.id_off, 0, sizeof(uint64_t), stream);
             if (e0 != hipSuccess) return e0;
         }
+        if (p.hist && p.hist_overwrite) {   // the histogram of no strings
+            const hipError_t e1 = hipMemsetAsync(p.hist, 0, ((size_t)p.hist_bins + 8u) * sizeof(int64_t), stream);
+            if (e1 != hipSuccess) return e1;
+        }
         return hipMemsetAsync(reinterpret_cast<uint64_t *>(p.retry_count) + CTR_LASTNEED64, 0, 3 * sizeof(uint64_t), stream);
     }
-    if (ev) {
-        const hipError_t er = hipEventRecord(ev[0], stream);
-        if (er != hipSuccess) return er;
-    }
+    // profiling (dpt_ctx_profile): the first pass's dispatch records ev[0], the unbounded pass's ev[1]
+    hipEvent_t e0 = ev ? ev[0] : nullptr;
     if (p.n_str > 0) {
         {
             const unsigned n_cu = p.max_blocks / 64;
@@ -2862,19 +2876,19 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
                 // the hot kernel gets the staged id width as a template constant
                 const uint64_t nu = (p.n_str + 3) / 4;
                 if (wide) {
-                    if (p.staging16) launch_tok<SMALL_CH, 16, false, true, 1>(a, tv, nu, n_cu, stream);
-                    else launch_tok<SMALL_CH, 16, false, true, 2>(a, tv, nu, n_cu, stream);
+                    if (p.staging16) launch_tok<SMALL_CH, 16, false, true, 1>(a, tv, nu, n_cu, stream, e0);
+                    else launch_tok<SMALL_CH, 16, false, true, 2>(a, tv, nu, n_cu, stream, e0);
                 } else if (raw) {
-                    if (p.staging16) launch_tok<SMALL_CH, 16, false, false, 1, true>(a, tv, nu, n_cu, stream);
-                    else launch_tok<SMALL_CH, 16, false, false, 2, true>(a, tv, nu, n_cu, stream);
+                    if (p.staging16) launch_tok<SMALL_CH, 16, false, false, 1, true>(a, tv, nu, n_cu, stream, e0);
+                    else launch_tok<SMALL_CH, 16, false, false, 2, true>(a, tv, nu, n_cu, stream, e0);
                 } else {
-                    if (p.staging16) launch_tok<SMALL_CH, 16, false, false, 1>(a, tv, nu, n_cu, stream);
-                    else launch_tok<SMALL_CH, 16, false, false, 2>(a, tv, nu, n_cu, stream);
+                    if (p.staging16) launch_tok<SMALL_CH, 16, false, false, 1>(a, tv, nu, n_cu, stream, e0);
+                    else launch_tok<SMALL_CH, 16, false, false, 2>(a, tv, nu, n_cu, stream, e0);
                 }
             } else {
-                if (wide) launch_tok<SMALL_CH, 64, false, true>(a, tv, p.n_str, n_cu, stream);
-                else if (raw) launch_tok<SMALL_CH, 64, false, false, 0, true>(a, tv, p.n_str, n_cu, stream);
-                else launch_tok<SMALL_CH, 64, false, false>(a, tv, p.n_str, n_cu, stream);
+                if (wide) launch_tok<SMALL_CH, 64, false, true>(a, tv, p.n_str, n_cu, stream, e0);
+                else if (raw) launch_tok<SMALL_CH, 64, false, false, 0, true>(a, tv, p.n_str, n_cu, stream, e0);
+                else launch_tok<SMALL_CH, 64, false, false>(a, tv, p.n_str, n_cu, stream, e0);
             }
         }
         // second pass over the strings whose single word (or expansion) did not fit the small window
@@ -2905,11 +2919,7 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
         const uint64_t lcap = (uint64_t)(p.max_blocks / 16) / FALLBACK_DIV;
         const uint64_t lb = p.n_str < lcap ? p.n_str : lcap;
         l.blocks = (unsigned)(lb ? lb : 1);
-        launch_long(l, stream);
-    }
-    if (ev) {
-        const hipError_t er = hipEventRecord(ev[1], stream);
-        if (er != hipSuccess) return er;
+        launch_long(l, stream, ev ? ev[1] : nullptr);
     }
     if (p.padded) {   // dpt_encode_padded: the ids are in place; only the counters need their reset
         hipLaunchKernelGGL(reset_kernel, dim3(1), dim3(64), 0, stream, p.retry_count);
@@ -2924,7 +2934,10 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     f.hist = fold_hist ? reinterpret_cast<unsigned long long *>(p.hist) : nullptr;
     f.status = p.status;
     f.n_bins = p.hist_bins;
-    if (nb > 1) hipLaunchKernelGGL(batch_scan_kernel, dim3(1), dim3(SCAN_THREADS), 0, stream, p.n_str, p.flags, p.bpre, p.retry_count);
+    f.hist_store = (fold_hist && p.hist_overwrite && nb <= 1) ? 1 : 0;
+    unsigned long long *hz = (fold_hist && p.hist_overwrite && nb > 1) ? f.hist : nullptr;
+    if (nb > 1) hipLaunchKernelGGL(batch_scan_kernel, dim3(1), dim3(SCAN_THREADS), 0, stream, p.n_str, p.flags, p.bpre, p.retry_count,
+                                   hz, p.hist_bins + 8u);
     else { f.bsum = p.flags; f.ctr = p.retry_count; }
     f.staging = p.staging16 ? (const void *)p.staging16 : (const void *)p.staging;
     f.str_off = p.str_off; f.counts = p.counts; f.n_str = p.n_str; f.id_off = p.id_off; f.ids = p.ids;
@@ -2935,8 +2948,10 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     if (p.staging16) hipLaunchKernelGGL(finish_kernel<int16_t>, dim3((unsigned)fb), dim3(FIN_THREADS), 0, stream, f);
     else hipLaunchKernelGGL(finish_kernel<int32_t>, dim3((unsigned)fb), dim3(FIN_THREADS), 0, stream, f);
     if (p.hist && !fold_hist) {   // too many bins for the finish pass's LDS: the separate pass
-        const hipError_t eh = hipGetLastError();
+        hipError_t eh = hipGetLastError();
         if (eh != hipSuccess) return eh;
+        if (p.hist_overwrite && (eh = hipMemsetAsync(p.hist, 0, ((size_t)p.hist_bins + 8u) * sizeof(int64_t), stream)) != hipSuccess)
+            return eh;
         return launch_histogram(p.id_off, p.status, p.n_str, p.hist, p.hist_bins, stream);
     }
     return hipGetLastError();

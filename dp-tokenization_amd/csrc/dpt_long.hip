@@ -555,7 +555,7 @@ __global__ void __launch_bounds__(64) long_kernel(Args a) {
 
 }  // namespace lng
 
-void launch_long(const LongLaunch &p, hipStream_t stream) {
+void launch_long(const LongLaunch &p, hipStream_t stream, hipEvent_t ev_stop) {
     lng::Args a;
     a.text = p.text; a.str_off = p.str_off; a.cut_mask = p.cut_mask;
     a.staging = p.staging; a.staging16 = p.staging16; a.counts = p.counts; a.bsum = p.bsum; a.status = p.status; a.capped = p.capped;
@@ -566,7 +566,10 @@ void launch_long(const LongLaunch &p, hipStream_t stream) {
     a.edges = p.edges; a.far = p.far; a.far_cap = p.far_cap; a.far_count = p.far_count; a.list = p.list; a.list_count = p.list_count; a.work_next = p.work_next;
     a.slots = p.slots; a.slots4 = p.slots4; a.n_slots = p.n_slots; a.root_base = p.root_base;
     a.max_tok_bytes = p.max_tok_bytes; a.long_span = p.long_span; a.mode = p.mode;
-    hipLaunchKernelGGL(lng::long_kernel, dim3(p.blocks), dim3(64), 0, stream, a);
+    if (ev_stop)   // the end timestamp of the tokenize passes rides on this dispatch (dpt_ctx_profile)
+        hipExtLaunchKernelGGL(lng::long_kernel, dim3(p.blocks), dim3(64), 0, stream, nullptr, ev_stop, 0, a);
+    else
+        hipLaunchKernelGGL(lng::long_kernel, dim3(p.blocks), dim3(64), 0, stream, a);
 }
 
 }  // namespace dpt

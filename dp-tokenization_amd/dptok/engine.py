@@ -421,11 +421,12 @@ class Encoder:
         check(_lib.lib().dpt_ctx_long_need(self.handle, ctypes.byref(a), ctypes.byref(b)), "dpt_ctx_long_need")
         return a.value, b.value
 
-    def set_histogram(self, hist_ptr: int, n_bins: int) -> None:
-        """Fold the token-count histogram into the next encode on this engine (dpt_ctx_set_histogram:
-        its finish pass adds to hist, device int64[n_bins + 8]); 0 cancels."""
-        check(_lib.lib().dpt_ctx_set_histogram(self.handle, ctypes.c_void_p(hist_ptr) if hist_ptr else None, n_bins),
-              "dpt_ctx_set_histogram")
+    def set_histogram(self, hist_ptr: int, n_bins: int, overwrite: bool = False) -> None:
+        """Fold the token-count histogram into the next encode on this engine (dpt_ctx_set_histogram_ex:
+        its finish pass adds to hist, device int64[n_bins + 8], or with ``overwrite`` replaces it -- the
+        device zeroes it first, in stream order); 0 cancels."""
+        check(_lib.lib().dpt_ctx_set_histogram_ex(self.handle, ctypes.c_void_p(hist_ptr) if hist_ptr else None, n_bins,
+                                                  1 if overwrite else 0), "dpt_ctx_set_histogram_ex")
 
     def histogram_device(self, idoff_ptr: int, status_ptr: int, n_str: int, hist_ptr: int, n_bins: int,
                          stream: int = 0) -> None:

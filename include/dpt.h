@@ -198,6 +198,11 @@ int dpt_token_histogram(const uint64_t *id_off, const int32_t *status, uint64_t 
  */
 int dpt_ctx_set_histogram(dpt_ctx *c, int64_t *hist, uint32_t n_bins);
 
+/* As dpt_ctx_set_histogram; flags DPT_HIST_OVERWRITE: the call's histogram REPLACES hist's contents
+ * (the device zeroes it in stream order first) -- a per-step histogram without a memset launch. */
+#define DPT_HIST_OVERWRITE 1
+int dpt_ctx_set_histogram_ex(dpt_ctx *c, int64_t *hist, uint32_t n_bins, int flags);
+
 /* Per-ctx kernel timing with HIP events on the encode stream (for bench.py's roofline): one event
  * pair per call around the tokenize passes (first pass, 2048-byte pass, unbounded pass). */
 int dpt_ctx_profile(dpt_ctx *c, int enable);

@@ -201,6 +201,13 @@ def test_histogram_folded_into_encode(n, n_bins, engines):
     torch.cuda.synchronize()
     assert torch.equal(folded, sep), (folded.cpu().numpy()[-8:], sep.cpu().numpy()[-8:])
     assert int(sep[n_bins + 1]) == m + 7
+    # DPT_HIST_OVERWRITE: the call's histogram replaces whatever the buffer held
+    over = torch.full((n_bins + 8,), -5, dtype=torch.int64, device="cuda")
+    enc.set_histogram(over.data_ptr(), n_bins, overwrite=True)
+    enc.encode_device(dt.data_ptr(), int(offs[-1]), do.data_ptr(), m, ids.data_ptr(), len(text), id_off.data_ptr(),
+                      st.data_ptr(), stream=s)
+    torch.cuda.synchronize()
+    assert torch.equal(over[: n_bins + 7], sep[: n_bins + 7] - 7), (over.cpu().numpy()[-8:], sep.cpu().numpy()[-8:])
 
 
 @pytest.mark.parametrize("variant", ["rows16", "rows64"])
