@@ -804,6 +804,9 @@ __device__ __forceinline__ TrieView tv_of(ConstKernArgs *kp) {
     t.root_base = kp->tv.root_base; t.n_slots = kp->tv.n_slots; t.pair16 = kp->tv.pair16;
     return t;
 }
+#ifndef KREF_MORE
+#define KREF_MORE 0   // A/B knob: also refresh inside phases A and C2 (before the walkers and the hash pass)
+#endif
 #if KARG_REFRESH
 // (the 16-lane instantiations: the 64-lane ones do not spill, and measured 1.7 % slower with it)
 #define KREFRESH() do { if constexpr (G == 16) asm volatile("" : "+s"(kp)); } while (0)
@@ -1262,6 +1265,7 @@ tokenize_kernel(KernArgs ka) {
 #ifndef A_FAST
 #define A_FAST 1   // A/B knob: 0 = the generic walker takes A0's marked starts too
 #endif
+            if (KREF_MORE) KREFRESH();
             // ASCII walker: the marked starts of A0 slots (pure-ASCII raw windows: an atom is one byte, a
             // word start ' ' is '\u2581' = the trie node ws_node, '\n' is "<0x0A>", the string's first
             // atom '\u2581' + its byte) walked byte by byte without the generic walker's atom
@@ -1406,6 +1410,7 @@ tokenize_kernel(KernArgs ka) {
                     }
                 }
             }
+            if (KREF_MORE) KREFRESH();
             unsigned pre[NG + 1];
             pre[0] = 0;
 #pragma unroll
@@ -2329,6 +2334,7 @@ tokenize_kernel(KernArgs ka) {
                 }
                 wave_sync();
                 STAMP(5);
+                if (KREF_MORE) KREFRESH();
                 if (DPT_C2STOP == 1) r = 0;   // diagnostic: the bulk pass only
                 if (r > 0) {
                     r = hash_pass(r, [&](unsigned i) -> unsigned { return list_ref(i); });
@@ -2376,6 +2382,7 @@ tokenize_kernel(KernArgs ka) {
                     wave_sync();
                 }
             }
+            if (KREF_MORE) KREFRESH();
             auto tok_at = [&](unsigned i) -> unsigned { return list_ref(i); };
             // One token walk per lane; a lane whose token is resolved writes the id and takes the
             // next token (ballot + mbcnt), so each iteration is one trie step for 64 tokens.  A
