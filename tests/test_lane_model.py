@@ -55,3 +55,28 @@ def test_lane_model_matches_reference_port_short():
         except ValueError:
             continue
         assert lane_model.model(text, set(vocab)) == want, (text, vocab)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_lane_model64_matches_oracle(seed):
+    """forward_lanes64 (the 64-lane kernel's capless B): tokens up to 40 letters, words up to 256."""
+    import lane_model
+    from oracle import oracle
+    from dptok import pack_strings
+    rng = np.random.default_rng(300 + seed)
+    for n in range(120):
+        vocab, text = tie_heavy_case(rng, max_len=256 if n % 2 else 120)
+        vocab = set(vocab)
+        for _ in range(int(rng.integers(0, 30))):   # long tokens: substrings of the text's words
+            w = rng.choice(text.split(" "))
+            if len(w) > 17:
+                a = int(rng.integers(0, len(w) - 17)); b = a + int(rng.integers(17, min(40, len(w) - a) + 1))
+                vocab.add(w[a:b])
+        vocab = sorted(vocab)
+        t2i = {t: i for i, t in enumerate(vocab)}
+        txt, offs = pack_strings([text])
+        ids, off, st, _ = oracle.OracleVocab(t2i).encode_csr(txt, offs)
+        if st[0] != 0:
+            continue
+        want = [vocab[i] for i in ids.tolist()]
+        assert lane_model.model64(text, set(vocab)) == want, (text, vocab)

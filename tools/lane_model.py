@@ -167,6 +167,101 @@ def model(text, vocab, verbose=False):
             print(d, {k: l[k] for k in ("rs", "re", "pe", "T", "tb", "gin", "gre", "ls1", "left", "sel", "stop", "fin_in", "n1", "p1in", "re_ws")})
     return toks
 
+FRESH64 = 0x7FFF
+
+def model64(text, vocab, verbose=False):
+    """forward_lanes64 (tokenize_kernel, G = 64, capless windows) over the 64 lanes of a wave, then
+    the row-mode C1 walk (one word per lane: dg while the longest token so far is below the
+    word's G, de after).  Keys: cost << 16 | 0x7FFF - G; entries {dg | de << 8 | cp(i) << 16, key}."""
+    atoms, wsf, cpos = window(text)
+    na = len(atoms)
+    # start masks: bit d of sm[j] = atoms j .. j+d form a token (within a word, <= 64 atoms)
+    sm = [0] * (na + 1)
+    for j in range(na):
+        s = ""
+        for L in range(1, 65):
+            if j + L > na or (L > 1 and wsf[j + L - 1]):
+                break
+            s += atoms[j + L - 1]
+            if s in vocab:
+                sm[j] |= 1 << (L - 1)
+    assert all(sm[j] & 1 for j in range(na)), "not capless"
+    # cut points: p is one iff max_{j < p} (j + 1 + hb(sm[j])) <= p
+    cut = [False] * (na + 1)
+    run = 0
+    for p in range(na + 1):
+        cut[p] = run <= p
+        if p < na:
+            run = max(run, p + sm[p].bit_length())
+    nextcut = lambda c: next(p for p in range(c, na + 1) if cut[p])
+    C = (na + 63) >> 6
+    fx = [0] * (na + 2); fy = [0] * (na + 2)
+    lanes = []
+    for d in range(64):
+        c0 = min(d * C, na); c1 = min(c0 + C, na)
+        rs, re = nextcut(c0), nextcut(c1)
+        pe = 0
+        for i in range(rs + 1, re + 1):
+            fx[i] = cpos[i] << 16; fy[i] = 0xFFFFFFFF
+            if not pe and wsf[i]:
+                pe = i
+        for j in range(rs, re):
+            kj = FRESH64 if (j == rs or wsf[j]) else fy[j]
+            a1 = kj + 0x10000
+            m = sm[j]
+            while m:
+                dd = (m & -m).bit_length() - 1
+                m &= m - 1
+                i = j + 1 + dd
+                assert i <= re
+                a2 = (a1 | 0x7FFF) + cpos[j] - (fx[i] >> 16)
+                kk = min(a1, a2)
+                if (kk >> 15) <= (fy[i] >> 15):
+                    fx[i] = (fx[i] & ~0x7F00) | dd << 8
+                if kk <= fy[i]:
+                    fx[i] = (fx[i] & ~0x7F) | dd
+                fy[i] = min(kk, fy[i])
+        x = FRESH64 if rs == re else ((0x80000000 if pe else 0) | (FRESH64 if wsf[re] else fy[re]))
+        lanes.append(dict(rs=rs, re=re, pe=pe, x=x))
+    inn = FRESH64
+    for l in lanes:
+        l["in"] = inn
+        x = l["x"]
+        if x & 0x80000000:
+            inn = x & 0x7FFFFFFF
+        else:
+            inn = ((inn & 0x7FFF0000) + (x & 0x7FFF0000)) | min(inn & 0x7FFF, x & 0x7FFF)
+    for l in lanes:
+        rs, re, pe, inn = l["rs"], l["re"], l["pe"], l["in"]
+        gin = 0x7FFF - (inn & 0x7FFF)
+        if gin:
+            lim = pe if pe else re
+            for q in range(rs + 1, lim + 1):
+                if gin >= 0x7FFF - (fy[q] & 0x7FFF):
+                    fx[q] = (fx[q] & ~0x7F) | ((fx[q] >> 8) & 0x7F)
+            if pe:
+                kl = fy[pe]
+                fy[pe] = ((inn & 0x7FFF0000) + (kl & 0x7FFF0000)) | min(inn & 0x7FFF, kl & 0x7FFF)
+    if verbose:
+        print([(l["rs"], l["re"], l["pe"]) for l in lanes if l["rs"] < l["re"]])
+    # row-mode C1 per word
+    toks = []
+    wstarts = [i for i in range(na) if wsf[i]] + [na]
+    for w in range(len(wstarts) - 1):
+        e = wstarts[w + 1]
+        F = fy[e]
+        cost, Ls = F >> 16, 0x7FFF - (F & 0x7FFF)
+        i, A, pend, out = e, 0, cpos[e], []
+        for _ in range(cost):
+            A = max(A, pend - cpos[i])
+            dd = (fx[i] & 127) if A < Ls else ((fx[i] >> 8) & 127)
+            j = i - 1 - dd
+            out.append("".join(atoms[j:i]))
+            pend = cpos[i]; i = j
+        assert i == wstarts[w], (w, i)
+        toks += out[::-1]
+    return toks
+
 def ref_tokens(text, vocab):
     out = []
     for w in ref_port.raw_words(text):
