@@ -71,6 +71,17 @@ __device__ __forceinline__ unsigned wave_incl_scan_add(unsigned v) {
     return v;
 }
 
+// inclusive max-scan over 64 lanes (values >= 0; the same DPP steps as the add scan)
+__device__ __forceinline__ unsigned wave_incl_scan_max(unsigned v) {
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0u, v, 0x111, 0xF, 0xF, true));  // row_shr:1
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0u, v, 0x112, 0xF, 0xF, true));  // row_shr:2
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0u, v, 0x114, 0xF, 0xF, true));  // row_shr:4
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0u, v, 0x118, 0xF, 0xF, true));  // row_shr:8
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0u, v, 0x142, 0xA, 0xF, false)); // row_bcast:15
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0u, v, 0x143, 0xC, 0xF, false)); // row_bcast:31
+    return v;
+}
+
 // min within each row of 16 lanes, result in every lane of the row
 // (mov_dpp with bound_ctrl lets hipcc fold each step into one v_min_u32_dpp)
 __device__ __forceinline__ unsigned row_min_u32(unsigned v) {
@@ -762,6 +773,9 @@ __device__ bool prep_window(GroupLDS<CH, G> &L, uint8_t *gw, const WinRegs<CH> &
 #endif
 static_assert(NPART >= 1 && NPART <= NPART_MAX, "NPART");
 #ifndef A_REFILL
+#ifndef LANES64
+#define LANES64 1   // A/B knob: 0 = capless 64-lane windows run the row recurrence
+#endif
 #define A_REFILL 32   // phase A: idle lanes needed before a batched refill (1/8/16/32 within 2 %)
 #endif
 #ifndef DPT_DOUBLE   // diagnostic builds only: run one phase twice to measure its marginal cost (1 A, 3 C1, 4 C2, 5 prep)
@@ -1906,6 +1920,111 @@ tokenize_kernel(KernArgs ka) {
                 }
               }
             };
+            // Capless windows of the 256-byte 64-lane kernel without edge recording (one string per
+            // wave: BLOOM-scale byte-level vocabularies).  The row recurrence is one wave-min per atom,
+            // a dependent chain over the whole window (55 % of that kernel, profiles/r03_phase_diag.txt).
+            // Here each lane takes a chunk of end positions cut at cut points, as forward_lanes does,
+            // and relaxes forward ("push") from every start j of its chunk over j's span mask (phase
+            // A's start masks, rec[j].smask): the token j..i updates i's entry {dg | de << 8 | cp(i)
+            // << 16, key} in fin[].  Starts are taken in ascending order, so "<=" keeps the largest j
+            // of a tie -- the row recurrence's lowest lane (dp_tokenize.py:40-46).  A wave scan of the
+            // chunk transfers and forward_lanes' fix-up follow; C0/C1 then run as in row mode (they
+            // read fin[] only).
+            auto forward_lanes64 = [&]() {
+              if constexpr (G == 64 && !BIG) {
+                if (na == 0) return;
+                constexpr unsigned FRESH = 0x7FFFu;       // key of a fresh start: cost 0, reachable, G 0
+                constexpr unsigned RESET = 0x80000000u;   // transfer flag: a word ends in the chunk
+                uint2 *fin2 = reinterpret_cast<uint2 *>(L.fin);
+                // ---- cut points (bit p of cm[p / 64]): p is one iff max_{j < p} (j + 1 + hb(smask_j))
+                //      <= p -- no token crosses it; 0 and na always are
+                uint64_t cm[(CH + 64) / 64];
+                unsigned carry = 0;
+#pragma unroll
+                for (int r = 0; r < (CH + 64) / 64; r++) {
+                    const unsigned p = 64u * (unsigned)r + lane;
+                    // the end of the longest token from p: p + 1 + (63 - clz)
+                    const unsigned v = p < na ? p + 64u - (unsigned)__builtin_clzll(L.rec[p].smask | 1ull) : 0u;
+                    const unsigned inc = wave_incl_scan_max(v);
+                    const unsigned ex = max(carry, wave_shift_in(inc, 0u));
+                    carry = max(carry, __builtin_amdgcn_readlane(inc, 63));
+                    cm[r] = ballot(p <= na && ex <= p);
+                }
+                // the first cut at or after c (<= na)
+                auto nextcut = [&](unsigned c) -> unsigned {
+                    unsigned res = na;
+#pragma unroll
+                    for (int r = (CH + 64) / 64 - 1; r >= 0; r--) {
+                        const unsigned lo = 64u * (unsigned)r;
+                        const uint64_t keep = c <= lo ? ~0ull : (c >= lo + 64u ? 0ull : (~0ull << (c - lo)));
+                        const uint64_t m = cm[r] & keep;
+                        res = m ? lo + (unsigned)__builtin_ctzll(m) : res;
+                    }
+                    return res;
+                };
+                const unsigned C = (na + 63u) >> 6;
+                const unsigned c0 = min(lane * C, na), c1 = min(c0 + C, na);
+                const unsigned rs = nextcut(c0), re = nextcut(c1);
+                if (DPT_STOP == 25) return;   // diagnostic: cut points only
+                // ---- the chunk's entries: no candidate yet, cp(i) in the high half; pe = its first word end
+                unsigned pe = 0;
+                for (unsigned i = rs + 1u; i <= re; i++) {
+                    const unsigned cp = L.rec[i].cpos;
+                    fin2[i] = make_uint2((cp & 0x7FFFu) << 16, 0xFFFFFFFFu);
+                    pe = (!pe && (cp & CP_WS)) ? i : pe;
+                }
+                // ---- push: j ascending; j's key is final once every earlier start of the chunk ran
+                for (unsigned j = rs; j < re; j++) {
+                    const uint64_t sm = L.rec[j].smask;
+                    const unsigned cj = L.rec[j].cpos;
+                    const unsigned kj = (j == rs || (cj & CP_WS)) ? FRESH : fin2[j].y;
+                    const unsigned a1 = kj + 0x10000u;             // cost + 1
+                    const unsigned a1g = (a1 | 0x7FFFu) + (cj & 0x7FFFu);
+                    uint64_t m = sm;
+                    while (m) {
+                        const unsigned dd = (unsigned)__builtin_ctzll(m);
+                        m &= m - 1ull;
+                        const unsigned i = j + 1u + dd;              // <= re: no token crosses a cut
+                        uint2 f = fin2[i];
+                        const unsigned a2 = a1g - (f.x >> 16);       // G = max(G[j], cp(j..i))
+                        const unsigned kk = a1 < a2 ? a1 : a2;
+                        f.x = ((kk >> 15) <= (f.y >> 15)) ? ((f.x & ~0x7F00u) | (dd << 8)) : f.x;   // de
+                        f.x = (kk <= f.y) ? ((f.x & ~0x7Fu) | dd) : f.x;                            // dg
+                        f.y = kk < f.y ? kk : f.y;
+                        fin2[i] = f;
+                    }
+                }
+                if (DPT_STOP == 26) return;   // diagnostic: + the recurrence
+                // ---- wave scan of the chunk transfers (forward_lanes' compose, 64 lanes, keys)
+                const bool re_wb = (L.rec[re].cpos & CP_WS) != 0;
+                unsigned x = rs == re ? FRESH : ((pe ? RESET : 0u) | (re_wb ? FRESH : fin2[re].y));
+                auto compose = [&](unsigned y) {   // y (the earlier lanes) then x
+                    const unsigned comb = ((y & 0x7FFF0000u) + (x & 0x7FFF0000u)) | min(y & 0x7FFFu, x & 0x7FFFu);
+                    x = (x & RESET) ? x : ((y & RESET) | comb);
+                };
+                compose((unsigned)__builtin_amdgcn_update_dpp((int)FRESH, (int)x, 0x111, 0xF, 0xF, false));   // row_shr:1
+                compose((unsigned)__builtin_amdgcn_update_dpp((int)FRESH, (int)x, 0x112, 0xF, 0xF, false));   // row_shr:2
+                compose((unsigned)__builtin_amdgcn_update_dpp((int)FRESH, (int)x, 0x114, 0xF, 0xF, false));   // row_shr:4
+                compose((unsigned)__builtin_amdgcn_update_dpp((int)FRESH, (int)x, 0x118, 0xF, 0xF, false));   // row_shr:8
+                compose((unsigned)__builtin_amdgcn_update_dpp((int)FRESH, (int)x, 0x142, 0xA, 0xF, false));   // row_bcast:15
+                compose((unsigned)__builtin_amdgcn_update_dpp((int)FRESH, (int)x, 0x143, 0xC, 0xF, false));   // row_bcast:31
+                const unsigned in = (unsigned)__builtin_amdgcn_update_dpp((int)FRESH, (int)x, 0x138, 0xF, 0xF, false) & ~RESET;   // wave_shr:1
+                const unsigned gin = 0x7FFFu - (in & 0x7FFFu);   // G at rs (0: a word starts there, cost 0)
+                if (gin) {
+                    // before the first word end: dg = de wherever the incoming G attains G[q];
+                    // the first word end's key = in (+) local
+                    const unsigned lim = pe ? pe : re;
+                    for (unsigned q = rs + 1u; q <= lim; q++) {
+                        const uint2 f = fin2[q];
+                        if (gin >= 0x7FFFu - (f.y & 0x7FFFu)) fin2[q].x = (f.x & ~0x7Fu) | ((f.x >> 8) & 0x7Fu);
+                    }
+                    if (pe) {
+                        const unsigned kl = fin2[pe].y;
+                        fin2[pe].y = ((in & 0x7FFF0000u) + (kl & 0x7FFF0000u)) | min(in & 0x7FFFu, kl & 0x7FFFu);
+                    }
+                }
+              }
+            };
             using T_ = std::true_type;
             using F_ = std::false_type;
             using C0_ = std::integral_constant<int, 0>;
@@ -1924,6 +2043,8 @@ tokenize_kernel(KernArgs ka) {
 #ifdef DPT_LANEDBG
                         if (lane == 0) atomicAdd(&g_lanedbg[16 * 16 + 1], 1u);
 #endif
+                    } else if constexpr (!BIG && LANES64) {
+                        forward_lanes64();
                     } else {
                         forward(F_{}, C2_{});
                     }
