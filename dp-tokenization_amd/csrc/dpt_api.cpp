@@ -46,6 +46,7 @@ struct dpt_ctx {
     uint4 *pend = nullptr;            // pending residual tokens of the 256-byte pass (dpt::pend_scratch_bytes)
     unsigned long long *flags = nullptr;   // batch sums, then (from cap_flags / 2) batch prefixes: one each per 256 strings
     uint64_t cap_flags = 0;
+    int flag_parity = 0;   // which half of flags holds the batch sums (all zero between calls); see fin_fold
     unsigned max_blocks = 0;
     // host path: one device buffer in (text | offsets | cut) and one out (id_off | status | capped |
     // counters | ids | edges), each mirrored by a pinned host buffer so every copy is one async DMA
@@ -512,8 +513,9 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
     p.wsl_scratch = c->wsl_scratch;
     p.long_span = v->stats.max_cp > 64 ? 1 : 0;
     p.max_tok_bytes = v->stats.max_bytes;
-    p.flags = c->flags;
-    p.bpre = c->flags + c->cap_flags / 2;
+    p.flags_half = c->cap_flags / 2;
+    p.flags = c->flags + (c->flag_parity ? p.flags_half : 0);
+    p.bpre = c->flags + (c->flag_parity ? 0 : p.flags_half);
     p.max_blocks = c->max_blocks;
     p.arena = c->arena;
     p.arena_cap = c->arena_cap;
@@ -556,6 +558,7 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
         (void)hipMemsetAsync(c->flags, 0, c->cap_flags * sizeof(unsigned long long), st);   // nor zero the batch sums
         return hip_fail(e, "encode launch");
     }
+    if (!padded && dpt::fin_fold(n_str)) c->flag_parity ^= 1;   // the finish pass zeroed the other half
     return DPT_OK;
 }
 

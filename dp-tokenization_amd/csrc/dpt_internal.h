@@ -33,7 +33,8 @@ struct EncodeLaunch {
     uint32_t max_tok_bytes;  // longest vocabulary token, bytes
     unsigned long long *flags;   // per FIN_BATCH-string batch: the sum of its counts, added by the tokenize passes as
                                  //   strings finish; batch_scan_kernel zeroes it for the next call
-    unsigned long long *bpre;    // per batch: its exclusive id prefix (batch_scan_kernel)
+    unsigned long long *bpre;    // per batch: its exclusive id prefix (batch_scan_kernel); the other of the two arrays
+    uint64_t flags_half;         // entries of each array (flags, bpre)
     unsigned max_blocks;
     int variant;             // KERNEL_* below
     bool padded;             // dpt_encode_padded: staging = the caller's ids, counts = the caller's; no finish pass
@@ -64,6 +65,18 @@ constexpr unsigned PAIR16_N = 65536 + 256;
 // strings per finish batch (the batch arrays are sized one per 64 strings, two arrays)
 constexpr unsigned FIN_BATCH = 256;
 constexpr unsigned PART_STRIDE = 64;
+// Calls of 2..FIN_FOLD_MAX batches run no batch_scan_kernel: each finish block sums the batch sums
+// before its own batch (<= FIN_FOLD_MAX / FIN_THREADS loads per thread), zeroes the OTHER array for
+// the next call (the two arrays swap roles: dpt_ctx's flag parity) and block 0 resets the counter
+// block.  Saves a launch (~5 us) on the strong-scaling shard sizes (125k..500k strings).
+#ifndef FIN_FOLD_MAX_DEF
+#define FIN_FOLD_MAX_DEF 2048   // A/B knob (both the API and the kernels must see the same value)
+#endif
+constexpr unsigned FIN_FOLD_MAX = FIN_FOLD_MAX_DEF;
+__host__ __device__ inline bool fin_fold(uint64_t n_str) {
+    const uint64_t nb = (n_str + FIN_BATCH - 1) / FIN_BATCH;
+    return nb > 1 && nb <= FIN_FOLD_MAX;
+}
 constexpr unsigned FIN_MAX_BINS = 1024;   // histogram bins the finish pass folds in (more: the separate pass)
 constexpr size_t PART_CTR_OFFSET = 256;
 constexpr size_t CTR_ALLOC_BYTES = PART_CTR_OFFSET + (NPART_MAX + 1) * PART_STRIDE * 4;

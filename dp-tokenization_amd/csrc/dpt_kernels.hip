@@ -321,6 +321,8 @@ struct EncodeArgs {
     int long_span;              // the vocabulary has tokens longer than 64 code points
     uint64_t *edges;            // nullable: per atom end, the E(i) & reachable back-distance mask
     int mode;                   // DPT_MODE_* | DPT_FLAG_*
+    unsigned long long *hist_zero;   // 2048-byte pass, fin_fold calls with DPT_HIST_OVERWRITE: the histogram to
+    uint32_t n_hist;                 //   zero before the finish pass adds to it (the scan kernel's duty otherwise)
 };
 
 #ifdef DPT_LANEDBG
@@ -852,6 +854,9 @@ tokenize_kernel(KernArgs ka) {
     const unsigned mg = lane / G;        // my group
     const unsigned d = lane % G;         // my back distance - 1
     const uint64_t n_work = BIG ? (uint64_t)(*a.work_count) : a.n_str;
+    if constexpr (BIG)
+        if (a.hist_zero && blockIdx.x == 0)
+            for (uint32_t b = lane; b < a.n_hist; b += 64u) a.hist_zero[b] = 0;
     if (BIG && n_work == 0) return;   // no retries: no counter traffic
     const uint64_t base_off = a.str_off[0];
     // (the other instantiations keep the mode a run-time value: folding raw = false into the atoms-mode
@@ -1730,15 +1735,56 @@ tokenize_kernel(KernArgs ka) {
                 unsigned cprev = rec32[rs] & 0x7FFu;
                 unsigned nxt = rec32[rs + 1u];   // rs + 1 <= na + 1 < NA
                 unsigned T = 0;                  // tokens of the chunk: the pieces' costs
+#ifndef LANE_PF
+#define LANE_PF 0   // A/B knob: candidates of the next position read a step ahead (0..2); 1 and 2 measured
+                    // slower (cfg4 67.6 -> 65.5 / 62.7 GB/s, cfg2 101.2 -> 99.6 / 94.9: profiles/r03_ab.log r03y)
+#endif
+                // LANE_PF > 0: the entries of position i+1's first candidates (j = i - dd, final by step
+                // i) are read during step i, from its end mask loaded a step earlier (nxt2), so their
+                // LDS latency overlaps step i's work instead of heading step i+1's chain
+                unsigned nxt2 = LANE_PF ? rec32[rs + 2u] : 0u;   // (<= NA: rec[NA] is the next LDS field, unused)
+                unsigned pda = 0, pdb = 0, pra = 0, prb = 0;     // this position's prefetched candidates (dd 0: none)
                 while (ballot(i < re)) {
                     if (i < re) {
                         i++;
                         const unsigned r = nxt;
-                        nxt = rec32[i + 1u];
+                        unsigned qa = 0, qb = 0, qra = 0, qrb = 0;
+                        if (LANE_PF) {
+                            nxt = nxt2;
+                            nxt2 = rec32[i + 2u];
+                            unsigned mn = i < re ? (~nxt >> 17) & 0x7FFFu : 0u;   // position i+1's longer tokens
+                            qa = mn ? ffbl(mn) + 1u : 0u;
+                            mn &= mn - 1u;
+                            qra = rec32[i - qa];                 // (qa 0: rec[i] -- read, unused)
+                            if (LANE_PF > 1) {
+                                qb = mn ? ffbl(mn) + 1u : 0u;
+                                qrb = rec32[i - qb];
+                            }
+                        } else {
+                            nxt = rec32[i + 1u];
+                        }
                         const unsigned cpi = r & 0x7FFu;             // bits 11..14: see below
                         unsigned best = relax(sprev, cpi - cprev);   // j = i-1: the single atom
                         unsigned dg = 0, de = 0;
                         unsigned m = (~r >> 17) & 0x7FFFu;          // longer tokens ending at i: bit d-1
+                        if (LANE_PF) {
+                            // the prefetched candidates are m's lowest bits, in order
+                            auto cand = [&](unsigned dd, unsigned rj) {
+                                const unsigned j = i - 1u - dd;
+                                const unsigned sj = j == ws ? FRESH : (rj >> 16);
+                                const unsigned kk = dd ? relax(sj, cpi - (rj & 0x7FFu)) : 0xFFFFFFFFu;
+                                if ((kk >> 5) < (best >> 5)) de = dd;
+                                if (kk < best) dg = dd;
+                                best = kk < best ? kk : best;
+                            };
+                            cand(pda, pra);
+                            m &= pda ? m - 1u : m;
+                            if (LANE_PF > 1) {
+                                cand(pdb, prb);
+                                m &= pdb ? m - 1u : m;
+                            }
+                            pda = qa; pdb = qb; pra = qra; prb = qrb;
+                        }
 #ifndef B_PAIR
 #define B_PAIR 0   // A/B knob: candidates per inner iteration taken two at a time (both LDS reads in flight):
                    // cfg4 +0.9 %, cfg2 -0.9 % (profiles/r03_ab.log)
@@ -1973,25 +2019,51 @@ tokenize_kernel(KernArgs ka) {
                     fin2[i] = make_uint2((cp & 0x7FFFu) << 16, 0xFFFFFFFFu);
                     pe = (!pe && (cp & CP_WS)) ? i : pe;
                 }
-                // ---- push: j ascending; j's key is final once every earlier start of the chunk ran
+                // ---- push: j ascending; j's key is final once every earlier start of the chunk ran --
+                //      it is the j-1 -> j edge's result (bit 0: capless windows have it at every start),
+                //      carried in a register.  The edges of a start go in batches of PUSH_B: their entry
+                //      reads in flight together (distinct entries), then the updates, then the writes.
+#ifndef PUSH_B
+#define PUSH_B 1   // A/B knob: edges per batch (BLOOM 17.2 GB/s at 1, 17.1 at 2, 16.5 at 4: profiles/r03_ab.log r03x)
+#endif
+                unsigned kcarry = FRESH;
                 for (unsigned j = rs; j < re; j++) {
                     const uint64_t sm = L.rec[j].smask;
                     const unsigned cj = L.rec[j].cpos;
-                    const unsigned kj = (j == rs || (cj & CP_WS)) ? FRESH : fin2[j].y;
+                    const unsigned kj = (j == rs || (cj & CP_WS)) ? FRESH : kcarry;
                     const unsigned a1 = kj + 0x10000u;             // cost + 1
                     const unsigned a1g = (a1 | 0x7FFFu) + (cj & 0x7FFFu);
-                    uint64_t m = sm;
-                    while (m) {
-                        const unsigned dd = (unsigned)__builtin_ctzll(m);
-                        m &= m - 1ull;
-                        const unsigned i = j + 1u + dd;              // <= re: no token crosses a cut
-                        uint2 f = fin2[i];
+                    auto upd = [&](uint2 &f, unsigned dd) {
                         const unsigned a2 = a1g - (f.x >> 16);       // G = max(G[j], cp(j..i))
                         const unsigned kk = a1 < a2 ? a1 : a2;
                         f.x = ((kk >> 15) <= (f.y >> 15)) ? ((f.x & ~0x7F00u) | (dd << 8)) : f.x;   // de
                         f.x = (kk <= f.y) ? ((f.x & ~0x7Fu) | dd) : f.x;                            // dg
                         f.y = kk < f.y ? kk : f.y;
-                        fin2[i] = f;
+                    };
+                    {   // the j -> j+1 edge (bit 0): j+1's final key
+                        uint2 f = fin2[j + 1u];
+                        upd(f, 0u);
+                        fin2[j + 1u] = f;
+                        kcarry = f.y;
+                    }
+                    uint64_t m = sm & ~1ull;
+                    while (m) {
+                        unsigned dd[PUSH_B];
+                        bool hv[PUSH_B];
+#pragma unroll
+                        for (int q = 0; q < PUSH_B; q++) {
+                            hv[q] = m != 0;
+                            dd[q] = hv[q] ? (unsigned)__builtin_ctzll(m) : 0u;
+                            m &= m - 1ull;   // (m = 0 stays 0)
+                        }
+                        uint2 f[PUSH_B];
+#pragma unroll
+                        for (int q = 0; q < PUSH_B; q++) f[q] = fin2[j + 1u + dd[q]];   // <= re: no token crosses a cut
+#pragma unroll
+                        for (int q = 0; q < PUSH_B; q++) upd(f[q], dd[q]);
+#pragma unroll
+                        for (int q = 0; q < PUSH_B; q++)
+                            if (hv[q]) fin2[j + 1u + dd[q]] = f[q];
                     }
                 }
                 if (DPT_STOP == 26) return;   // diagnostic: + the recurrence
@@ -2045,6 +2117,7 @@ tokenize_kernel(KernArgs ka) {
 #endif
                     } else if constexpr (!BIG && LANES64) {
                         forward_lanes64();
+                        lane_mode = DPT_STOP >= 25 && DPT_STOP <= 27;   // stop builds: no C0/C1 over unfinished fin[]
                     } else {
                         forward(F_{}, C2_{});
                     }
@@ -2749,7 +2822,10 @@ struct FinishArgs {
     const unsigned long long *bpre;   // per batch: its first id (batch_scan_kernel)
     unsigned slices;                  // blocks per batch
     unsigned long long *bsum;         // one-batch calls (no scan kernel): zeroed here ...
-    uint32_t *ctr;                    // ... and the counter block reset here (both null otherwise)
+    uint32_t *ctr;                    // ... and the counter block reset here (null when the scan kernel ran)
+    const unsigned long long *fold;   // fin_fold calls: the batch sums, summed here per block (else null) ...
+    unsigned long long *fold_zero;    // ... while the other array is zeroed for the next call
+    uint64_t fold_n;                  // (its entries)
     unsigned long long *hist;         // nullable: the token-count histogram (dpt_ctx_set_histogram) ...
     int hist_store;                   // ... stored, not added (DPT_HIST_OVERWRITE in a one-batch call) ...
     const int32_t *status;            // ... with the statuses it counts
@@ -2774,12 +2850,21 @@ __global__ void __launch_bounds__(FIN_THREADS) finish_kernel(FinishArgs f) {
     const uint64_t base_off = f.str_off[0];
     const ST *__restrict__ staging = reinterpret_cast<const ST *>(f.staging);
     const uint64_t s0 = t * FIN_BATCH;
-    const uint64_t o0 = f.bsum ? 0ull : f.bpre[t];   // one batch: its first id is 0
     // the first FIN_BATCH threads hold one string each; every thread copies
     const bool has = tid < FIN_BATCH && tid < f.n_str - s0;
     const uint64_t c = has ? f.counts[s0 + tid] : 0ull;
     const uint64_t src = has ? f.str_off[s0 + tid] - base_off : 0ull;
     uint64_t total;
+    uint64_t o0 = 0;   // one batch: its first id is 0
+    if (f.fold) {   // the batch's first id: the sums of the batches before it (t <= FIN_FOLD_MAX)
+        uint64_t ps = 0;
+        for (uint64_t k = tid; k < t; k += FIN_THREADS) ps += f.fold[k];
+        (void)block_incl_scan_add64<FIN_THREADS>(ps, s_w, &o0);
+        for (uint64_t k = (uint64_t)blockIdx.x * FIN_THREADS + tid; k < f.fold_n; k += (uint64_t)gridDim.x * FIN_THREADS)
+            f.fold_zero[k] = 0;
+    } else if (!f.bsum) {
+        o0 = f.bpre[t];
+    }
     const uint64_t incl = block_incl_scan_add64<FIN_THREADS>(c, s_w, &total);
     if (tid < FIN_BATCH) {
         s_rel[tid] = incl - c;
@@ -2820,10 +2905,9 @@ __global__ void __launch_bounds__(FIN_THREADS) finish_kernel(FinishArgs f) {
         if (has) f.id_off[s0 + tid + 1] = o0 + incl;
         if (t == 0 && tid == 0) {
             f.id_off[0] = 0;
-            if (f.bsum) {   // one-batch call: the scan kernel's other duties (every tokenize pass is done)
-                f.bsum[0] = 0;
-                reset_counters(f.ctr);
-            }
+            // without the scan kernel: its other duties (every tokenize pass is done)
+            if (f.bsum) f.bsum[0] = 0;   // one-batch call (fold calls zero the other array instead)
+            if (f.ctr) reset_counters(f.ctr);
         }
     }
     const uint64_t k_beg = total * sl / f.slices, k_end = total * (sl + 1) / f.slices;
@@ -2978,6 +3062,7 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     a.wsl_scratch = p.wsl_scratch;
     a.pend = p.pend; a.ws_node = p.ws_node; a.ws_base = p.ws_base; a.ws_id = p.ws_id;
     a.long_span = p.long_span;
+    a.hist_zero = nullptr; a.n_hist = 0;
     TrieView tv{p.slots, p.slot_ids, p.slots4, p.root_base, p.n_slots, p.pair16};
     const bool wide = (p.mode & DPT_MODE_MASK) == DPT_MODE_ATOMS;   // atoms of up to 8 bytes
     const bool raw = (p.mode & DPT_MODE_MASK) == DPT_MODE_RAW;
@@ -3023,6 +3108,10 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
         EncodeArgs b = a;
         b.work_list = p.retry_list; b.work_count = p.retry_count;
         b.work_next = p.retry_count + 2;
+        if (!p.padded && fin_fold(p.n_str) && p.hist && p.hist_overwrite && p.hist_bins >= 2 && p.hist_bins <= FIN_MAX_BINS) {
+            b.hist_zero = reinterpret_cast<unsigned long long *>(p.hist);   // (the finish pass adds to it)
+            b.n_hist = p.hist_bins + 8u;
+        }
 #ifndef FALLBACK_DIV
 #define FALLBACK_DIV 4   // the fallback passes' grids: 1/FALLBACK_DIV of a full one (usually they find no work)
 #endif
@@ -3057,15 +3146,17 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     // strings: the drop-in's per-string calls) needs no prefix, and its finish block does the rest
     const uint64_t nb = (p.n_str + FIN_BATCH - 1) / FIN_BATCH;
     FinishArgs f;
-    f.bsum = nullptr; f.ctr = nullptr;
+    f.bsum = nullptr; f.ctr = nullptr; f.fold = nullptr; f.fold_zero = nullptr; f.fold_n = 0;
+    const bool fold = fin_fold(p.n_str);
     const bool fold_hist = p.hist && p.hist_bins >= 2 && p.hist_bins <= FIN_MAX_BINS;
     f.hist = fold_hist ? reinterpret_cast<unsigned long long *>(p.hist) : nullptr;
     f.status = p.status;
     f.n_bins = p.hist_bins;
     f.hist_store = (fold_hist && p.hist_overwrite && nb <= 1) ? 1 : 0;
-    unsigned long long *hz = (fold_hist && p.hist_overwrite && nb > 1) ? f.hist : nullptr;
-    if (nb > 1) hipLaunchKernelGGL(batch_scan_kernel, dim3(1), dim3(SCAN_THREADS), 0, stream, p.n_str, p.flags, p.bpre, p.retry_count,
-                                   hz, p.hist_bins + 8u);
+    unsigned long long *hz = (fold_hist && p.hist_overwrite && nb > 1 && !fold) ? f.hist : nullptr;
+    if (fold) { f.fold = p.flags; f.fold_zero = p.bpre; f.fold_n = p.flags_half; f.ctr = p.retry_count; }
+    else if (nb > 1) hipLaunchKernelGGL(batch_scan_kernel, dim3(1), dim3(SCAN_THREADS), 0, stream, p.n_str, p.flags, p.bpre, p.retry_count,
+                                        hz, p.hist_bins + 8u);
     else { f.bsum = p.flags; f.ctr = p.retry_count; }
     f.staging = p.staging16 ? (const void *)p.staging16 : (const void *)p.staging;
     f.str_off = p.str_off; f.counts = p.counts; f.n_str = p.n_str; f.id_off = p.id_off; f.ids = p.ids;

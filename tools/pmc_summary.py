@@ -12,7 +12,7 @@ for f in glob.glob(os.path.join(root, "trace", "**", "*kernel_stats.csv"), recur
     for row in csv.DictReader(open(f)):
         dur[row["Name"]] = float(row["AverageNs"])
 for k, d in vals.items():
-    if "tokenize" not in k and "lane" not in k and "compact" not in k:
+    if "tokenize" not in k and "lane" not in k and "compact" not in k and "finish" not in k:
         continue
     short = k.split("(")[0][-60:]
     print(short, " avg_ns=%s" % next((v for n, v in dur.items() if n.split("(")[0] == k.split("(")[0]), "?"))
