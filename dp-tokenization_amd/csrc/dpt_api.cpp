@@ -203,7 +203,7 @@ std::vector<uint32_t> build_token_hash(const uint8_t *blob, const uint64_t *off,
     }
     auto khash = [](const Key &k, uint32_t seed, uint32_t &h, uint32_t &fp) {
         const unsigned nd = k.len <= 16 ? 4u : (k.len + 3u) / 4u;
-        uint32_t a = dpt::tokhash_start(k.len, seed);
+        dpt::TokHashState a = dpt::tokhash_start(k.len, seed);
         for (unsigned q = 0; q < nd; q++) a = dpt::tokhash_step(a, k.w[q], q, q + 1 == nd);
         dpt::tokhash_end(a, h, fp);
     };

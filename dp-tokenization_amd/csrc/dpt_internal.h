@@ -109,27 +109,38 @@ __host__ __device__ inline uint32_t tokhash_fmix(uint32_t h) {
     h ^= h >> 16;
     return h;
 }
-// The key is max(4, ceil(len / 4)) little-endian dwords of the token's bytes, zero past its length:
-// a = seed ^ len * golden; every dword but the last: a = rotl((a ^ w) * C, R) (C, R alternating); the
-// last: a = (a ^ w) * C; h = fmix(a); fp = fmix(h ^ K) | 1  (h: the bucket hash, fp: the fingerprint)
-__host__ __device__ inline uint32_t tokhash_start(uint32_t len, uint32_t seed) { return seed ^ (len * 0x9E3779B9u); }
-__host__ __device__ inline uint32_t tokhash_step(uint32_t a, uint32_t w, unsigned k, bool last) {
-    a = (a ^ w) * ((k & 1u) ? 0x1B873593u : 0xCC9E2D51u);
-    return last ? a : tokhash_rotl(a, (k & 1u) ? 13u : 15u);
+// The key is max(4, ceil(len / 4)) little-endian dwords of the token's bytes, zero past its length,
+// mixed into two independent 32-bit states: a = seed ^ len * golden; every dword but the last:
+// a = rotl((a ^ w) * C, R) (C, R alternating); the last: a = (a ^ w) * C -- and b, xxHash32's round
+// b = rotl(b + w * P2, 13) * P1 per dword; h = fmix(a) (the bucket hash), fp = fmix(b) | 1 (the
+// fingerprint).  An fp derived from h alone (round 2) left 32 bits per key: the 250,680-token BLOOM
+// vocabulary has ~7 full collisions among its keys, so no seed built a table and every C2 token
+// went to the walkers.
+struct TokHashState {
+    uint32_t a, b;
+};
+__host__ __device__ inline TokHashState tokhash_start(uint32_t len, uint32_t seed) {
+    return {seed ^ (len * 0x9E3779B9u), (seed + 0x165667B1u) ^ (len * 0x85EBCA77u)};
 }
-__host__ __device__ inline void tokhash_end(uint32_t a, uint32_t &h, uint32_t &fp) {
-    h = tokhash_fmix(a);
-    fp = tokhash_fmix(h ^ 0x5BD1E995u) | 1u;
+__host__ __device__ inline TokHashState tokhash_step(TokHashState s, uint32_t w, unsigned k, bool last) {
+    s.a = (s.a ^ w) * ((k & 1u) ? 0x1B873593u : 0xCC9E2D51u);
+    if (!last) s.a = tokhash_rotl(s.a, (k & 1u) ? 13u : 15u);
+    s.b = tokhash_rotl(s.b + w * 0x85EBCA77u, 13u) * 0x9E3779B1u;
+    return s;
+}
+__host__ __device__ inline void tokhash_end(TokHashState s, uint32_t &h, uint32_t &fp) {
+    h = tokhash_fmix(s.a);
+    fp = tokhash_fmix(s.b ^ 0x5BD1E995u) | 1u;
 }
 // four-dword keys (tokens of at most 16 bytes)
 __host__ __device__ inline void tokhash(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t len, uint32_t seed,
                                         uint32_t &h, uint32_t &fp) {
-    uint32_t a = tokhash_start(len, seed);
-    a = tokhash_step(a, w0, 0, false);
-    a = tokhash_step(a, w1, 1, false);
-    a = tokhash_step(a, w2, 2, false);
-    a = tokhash_step(a, w3, 3, true);
-    tokhash_end(a, h, fp);
+    TokHashState s = tokhash_start(len, seed);
+    s = tokhash_step(s, w0, 0, false);
+    s = tokhash_step(s, w1, 1, false);
+    s = tokhash_step(s, w2, 2, false);
+    s = tokhash_step(s, w3, 3, true);
+    tokhash_end(s, h, fp);
 }
 
 // kernel variants for the first pass (the 2048-byte window pass always follows for retries)

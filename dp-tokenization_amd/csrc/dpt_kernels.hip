@@ -481,7 +481,8 @@ __device__ __forceinline__ bool token_hash_long(const uint8_t *bytes, unsigned p
     const bool shift = (fi | sp) != 0;
     const unsigned as = fi ? 1u : 2u;
     uint32_t prev = fi ? 0x8196E200u : 0x96E20000u;   // the '\u2581' prefix ahead of raw dword 0
-    uint32_t a = tokhash_start(E, seed), nl = 0;
+    TokHashState a = tokhash_start(E, seed);
+    uint32_t nl = 0;
     for (unsigned k = 0; k < nd; k++) {
         uint32_t r = __builtin_amdgcn_alignbyte(d1, d0, sh);   // raw bytes 4k .. 4k+3
         d0 = d1;
@@ -1466,6 +1467,22 @@ tokenize_kernel(KernArgs ka) {
                 if (!ballot(active)) break;
                 const int32_t t = t2 ? (int32_t)t2 : nb + (int32_t)(seq & 0xFFu);
                 const int4 ent = trie_slotA(tv, t);   // buffer load: inactive lanes read harmlessly
+#ifndef A_PREF
+#define A_PREF 0   // A/B knob: 1 = the next atom's descriptor + bytes read before the trie load returns (measured
+                   // slower: BLOOM 17.6 -> 17.25, cfg5 81.6 -> 80.8 GB/s; profiles/r03_ab.log r03z)
+#endif
+                // The atom after this step's byte, if the byte ends the current one: j + len after the
+                // step (the root-table split sets len to 1 first).  Known without the trie entry, so its
+                // two dependent LDS reads overlap the load; used only when the atom ends (cont).
+                unsigned inf_pre = 0, cn_pre = 0;
+                uint64_t sq_pre = 0;
+                if (A_PREF) {
+                    const unsigned cpost = t2 ? cnt : cnt - 1u;
+                    const unsigned lpre = ((t2 && split) ? 1u : len) + (cpost == 0 ? 1u : 0u);
+                    const GL &L = *reinterpret_cast<const GL *>(smem + lbase);
+                    inf_pre = ainfo_get(L, j + lpre, false);
+                    sq_pre = atom_from_info<CH, WIDE>(L.bytes, inf_pre, raw, cn_pre);
+                }
                 // The step as selects (few exec-mask branches: their scalar bookkeeping costs issue
                 // slots like the vector work does).  Root-table entry (t2): .y = node after two
                 // bytes (0: none) | first byte exists << 30 | first byte ends a token << 31; .x =
@@ -1500,9 +1517,13 @@ tokenize_kernel(KernArgs ka) {
                 {
                     // the next atom, read by every lane (j + len <= n_atoms: in the window's arrays)
                     const GL &L = *reinterpret_cast<const GL *>(smem + lbase);
-                    unsigned cn;
-                    const unsigned inf = ainfo_get(L, j + len, false);
-                    const uint64_t sq = atom_from_info<CH, WIDE>(L.bytes, inf, raw, cn);
+                    unsigned cn = cn_pre;
+                    unsigned inf = inf_pre;
+                    uint64_t sq = sq_pre;
+                    if (!A_PREF) {
+                        inf = ainfo_get(L, j + len, false);
+                        sq = atom_from_info<CH, WIDE>(L.bytes, inf, raw, cn);
+                    }
                     info = cont ? inf : info;
                     seq = cont ? sq : seq;
                     cnt = cont ? cn : cnt;
