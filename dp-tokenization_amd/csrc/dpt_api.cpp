@@ -386,6 +386,8 @@ int dpt_vocab_create(const uint8_t *utf8_blob, const uint64_t *tok_off, const in
     v->stats.n_slots = da.n_slots;
     v->stats.max_bytes = da.max_bytes;
     v->stats.max_cp = da.max_cp;
+    v->stats.hash_max_probe = v->hash_probe;
+    v->stats.hash_buckets = v->hash_buckets;
     v->stats.device_bytes = (uint64_t)da.n_slots * (sizeof(int2) + sizeof(int32_t) + sizeof(int4)) + 65536 * (sizeof(int2) + sizeof(int4)) + (65536 + 256) * sizeof(int16_t) + 65536 * sizeof(uint2);
     dpt::free_double_array(&da);
     *out = v;

@@ -27,7 +27,8 @@ class DptError(RuntimeError):
 
 class VocabStats(ctypes.Structure):
     _fields_ = [("n_tokens", ctypes.c_uint32), ("n_nodes", ctypes.c_uint32), ("n_slots", ctypes.c_uint32),
-                ("max_bytes", ctypes.c_uint32), ("max_cp", ctypes.c_uint32), ("device_bytes", ctypes.c_uint64)]
+                ("max_bytes", ctypes.c_uint32), ("max_cp", ctypes.c_uint32), ("device_bytes", ctypes.c_uint64),
+                ("hash_max_probe", ctypes.c_uint32), ("hash_buckets", ctypes.c_uint32)]
 
 
 _lib = None

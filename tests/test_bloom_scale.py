@@ -61,6 +61,17 @@ def test_oracle_atoms_mode_matches_reference(big):
 
 
 @pytest.mark.gpu
+def test_token_hash_table_builds_at_bloom_scale(big):
+    """C2's token hash table (one bucket load per selected token) exists for the 250,680-entry
+    vocabulary.  Round 2's fingerprint was a function of the bucket hash (32 bits per key): the
+    vocabulary's ~7 expected full collisions made every seed fail, and C2 re-walked every token."""
+    import dptok
+    st = dptok.Vocab(big["vocab"]).stats
+    assert st["n_tokens"] == 250680
+    assert st["hash_max_probe"] > 0 and st["hash_buckets"] >= 250680 // 2
+
+
+@pytest.mark.gpu
 def test_dp_tokenize_bloom_scale_matches_reference(big):
     from packages.tokenizer_utils import dp_tokenize_bloom
     g = big["g"]

@@ -21,6 +21,13 @@ def oracles(vocabs):
     return {k: oracle.OracleVocab(v) for k, v in vocabs.items()}
 
 
+def test_token_hash_tables_build(engines):
+    """C2's one-lookup token hash exists for both test vocabularies (dpt_vocab_stats, ABI 2)."""
+    for k, e in engines.items():
+        st = e.vocab.stats
+        assert st["hash_max_probe"] > 0 and st["hash_buckets"] >= st["n_tokens"] // 2, (k, st)
+
+
 def _csr(texts):
     from dptok import pack_strings
     return pack_strings(texts)
