@@ -350,6 +350,13 @@ int dpt_vocab_create(const uint8_t *utf8_blob, const uint64_t *tok_off, const in
     if (e == hipSuccess) e = hipMemcpy(v->d_ids, da.id, sizeof(int32_t) * da.n_slots, hipMemcpyHostToDevice);
     // C2's token hash table (dpt_internal.h): header + buckets, after a0
     std::vector<uint32_t> th = build_token_hash(utf8_blob, tok_off, ids, n_tok);
+    if (th[1]) {   // the header's last word: 1 + the id of "<0x0A>" (a '\n' atom's expansion; last duplicate wins), 0 = none
+        for (uint32_t t = 0; t < n_tok; t++) {
+            const uint64_t o = tok_off[t] - tok_off[0], len = tok_off[t + 1] - tok_off[t];
+            const int32_t id = ids ? ids[t] : (int32_t)t;
+            if (len == 6 && !memcmp(utf8_blob + o, "<0x0A>", 6)) th[3] = id >= 0 ? (uint32_t)id + 1u : 0u;
+        }
+    }
     // one allocation, one kernel pointer (SGPRs are what the hot kernel spills): pair16, then a0, then the hash
     if (e == hipSuccess) e = hipMalloc((void **)&v->d_pair16, dpt::TOKHASH_OFFSET + sizeof(uint32_t) * th.size());
     if (e == hipSuccess) e = hipMemcpy(v->d_pair16, pair16.data(), sizeof(int16_t) * pair16.size(), hipMemcpyHostToDevice);

@@ -98,7 +98,7 @@ struct TokHashHeader {
     uint32_t mask;        // buckets - 1 (a power of two)
     uint32_t max_probe;   // buckets a lookup may visit (0: no table -- the walkers resolve every token)
     uint32_t seed;
-    uint32_t pad;
+    uint32_t nl_id1;      // 1 + the id of "<0x0A>" (0: none): raw mode's one-atom '\n' tokens take it without a lookup
 };
 __host__ __device__ inline uint32_t tokhash_rotl(uint32_t x, unsigned r) { return (x << r) | (x >> (32u - r)); }
 __host__ __device__ inline uint32_t tokhash_fmix(uint32_t h) {

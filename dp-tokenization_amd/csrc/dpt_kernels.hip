@@ -775,11 +775,14 @@ __device__ bool prep_window(GroupLDS<CH, G> &L, uint8_t *gw, const WinRegs<CH> &
 #define NPART 16      // first-pass work partitions (<= NPART_MAX)
 #endif
 static_assert(NPART >= 1 && NPART <= NPART_MAX, "NPART");
-#ifndef A_REFILL
 #ifndef LANES64
 #define LANES64 1   // A/B knob: 0 = capless 64-lane windows run the row recurrence
 #endif
+#ifndef A_REFILL
 #define A_REFILL 32   // phase A: idle lanes needed before a batched refill (1/8/16/32 within 2 %)
+#endif
+#ifndef A_REFILL64
+#define A_REFILL64 32   // the same for the 64-lane kernels (one string per wave: long walks leave lanes idle)
 #endif
 #ifndef DPT_DOUBLE   // diagnostic builds only: run one phase twice to measure its marginal cost (1 A, 3 C1, 4 C2, 5 prep)
 #define DPT_DOUBLE 0
@@ -797,6 +800,10 @@ static_assert(NPART >= 1 && NPART <= NPART_MAX, "NPART");
 #define DPT_RUN_B (DPT_STOP >= 3 && DPT_STOP != 21)
 #define DPT_RUN_C2 (DPT_STOP == 9)
 
+#ifndef WPE64
+#define WPE64 6   // the 256-byte 64-lane kernel: 6 waves per SIMD by VGPRs (<= 80; LDS allows 24 per CU):
+                  // BLOOM 17.4 -> 19.8 GB/s against no cap (95 VGPRs, 20 waves; profiles/r03_ab.log r03aa)
+#endif
 // 256-byte 16-lane rows: 6 waves per SIMD by VGPRs (<= 80), so LDS (22 waves per CU) binds
 #ifndef WPE16
 #define WPE16 6
@@ -835,7 +842,7 @@ __device__ __forceinline__ TrieView tv_of(ConstKernArgs *kp) {
 // constant (its expansions and word starts fold away in the other modes' code and vice versa -- the
 // 16-lane kernel sits at its register limit)
 template <int CH, int G, bool BIG, bool WIDE, int SW = 0, bool RAW = false>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CH == 256 && G == 16) ? WPE16 : 1)))
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CH == 256 && G == 16) ? WPE16 : ((CH == 256 && G == 64) ? WPE64 : 1))))
 tokenize_kernel(KernArgs ka) {
     ConstKernArgs *kp = (ConstKernArgs *)__builtin_amdgcn_kernarg_segment_ptr();
 #define a (kp->ea)
@@ -1456,7 +1463,7 @@ tokenize_kernel(KernArgs ka) {
                 {
                     const uint64_t im = ballot(!active);
                     const unsigned nidle = (unsigned)__builtin_popcountll(im);
-                    if (nxt < total && (nidle >= A_REFILL || total - nxt <= nidle)) {
+                    if (nxt < total && (nidle >= (G == 64 ? A_REFILL64 : A_REFILL) || total - nxt <= nidle)) {
                         if (!active) {
                             const unsigned uu = nxt + __builtin_amdgcn_mbcnt_hi((unsigned)(im >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)im, 0u));
                             if (uu < total) { active = true; start(uu); }
@@ -1466,7 +1473,17 @@ tokenize_kernel(KernArgs ka) {
                 }
                 if (!ballot(active)) break;
                 const int32_t t = t2 ? (int32_t)t2 : nb + (int32_t)(seq & 0xFFu);
-                const int4 ent = trie_slotA(tv, t);   // buffer load: inactive lanes read harmlessly
+#ifndef A_SLOT8
+#define A_SLOT8 1   // A/B knob: the 64-lane kernels' walks read the 8-byte slots (no child filter: half the
+                    // footprint of a BLOOM-scale trie, one more failing lookup per walk)
+#endif
+                int4 ent;
+                if constexpr (A_SLOT8 && G == 64) {
+                    const int2 e2 = trie_slot(tv, t);
+                    ent = make_int4(e2.x, e2.y, 0, -1);
+                } else {
+                    ent = trie_slotA(tv, t);   // buffer load: inactive lanes read harmlessly
+                }
 #ifndef A_PREF
 #define A_PREF 0   // A/B knob: 1 = the next atom's descriptor + bytes read before the trie load returns (measured
                    // slower: BLOOM 17.6 -> 17.25, cfg5 81.6 -> 80.8 GB/s; profiles/r03_ab.log r03z)
@@ -2360,6 +2377,10 @@ tokenize_kernel(KernArgs ka) {
                 }
                 const __amdgpu_buffer_rsrc_t hr = __builtin_amdgcn_make_buffer_rsrc(
                     (void *)(hbase + sizeof(TokHashHeader)), (short)0, (int)((hh.mask + 1u) * 16u), 0x00020000);
+#ifndef C2_NL
+#define C2_NL 0   // A/B knob: 1 = one-atom newline tokens take the header's id without a lookup (neutral on
+                  // cfg4, -0.5 % on cfg5: profiles/r03_ab.log r03aa)
+#endif
 #ifndef HP_U
 #define HP_U 2   // A/B knob: token rounds of 64 per hash-pass iteration (their loads before any store: a load
                  // waits for every older store of the wave)
@@ -2368,7 +2389,7 @@ tokenize_kernel(KernArgs ka) {
                 for (unsigned i0 = 0; i0 < n; i0 += 64u * HP_U) {
                     unsigned tt[HP_U], hh2[HP_U], fpv[HP_U];
                     uint64_t oqv[HP_U];
-                    bool hs[HP_U], inr[HP_U];
+                    bool hs[HP_U], inr[HP_U], nlv[HP_U];
 #pragma unroll
                     for (int u = 0; u < HP_U; u++) {
                         const unsigned i = i0 + 64u * (unsigned)u + lane;
@@ -2386,6 +2407,8 @@ tokenize_kernel(KernArgs ka) {
                         const unsigned p0 = L.aoff[jj];
                         const unsigned nbytes = (typename GL::Idx)(L.aoff[j1] - p0);
                         const unsigned fa = (raw ? 1u : 0u) & q.fw & (unsigned)(jj == 0);
+                        // a non-first '\n' atom alone is the token "<0x0A>": its id from the header
+                        const bool nl1 = C2_NL && raw && in && nbytes == 1 && !fa && hh.nl_id1 && L.bytes[p0] == '\n';
                         uint32_t h = 0, fp = 0;
                         bool hashed;
                         if constexpr (G == 16) {
@@ -2396,7 +2419,8 @@ tokenize_kernel(KernArgs ka) {
                         } else {   // 64-lane rows (BLOOM-scale vocabularies): keys of up to 64 bytes
                             hashed = in && token_hash_long<CH>(L.bytes, p0, nbytes, raw, fa, hh.seed, h, fp);
                         }
-                        tt[u] = t; hh2[u] = h & hh.mask; fpv[u] = fp; oqv[u] = q.ob + k; hs[u] = hashed; inr[u] = in;
+                        tt[u] = t; hh2[u] = h & hh.mask; fpv[u] = fp; oqv[u] = q.ob + k; hs[u] = hashed || nl1; inr[u] = in;
+                        nlv[u] = nl1;
                     }
                     // every round's first probe, then the rare further probes, then the stores
                     int32_t idv[HP_U];
@@ -2404,6 +2428,7 @@ tokenize_kernel(KernArgs ka) {
                     for (int u = 0; u < HP_U; u++) {
                         const auto e = __builtin_amdgcn_raw_buffer_load_b128(hr, hh2[u] * 16u, 0, 0);
                         idv[u] = e[0] == fpv[u] ? (int32_t)e[1] : (e[2] == fpv[u] ? (int32_t)e[3] : INT32_MIN);
+                        idv[u] = nlv[u] ? (int32_t)(hh.nl_id1 - 1u) : idv[u];
                     }
 #pragma unroll
                     for (int u = 0; u < HP_U; u++) {
