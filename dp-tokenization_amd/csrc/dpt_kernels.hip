@@ -197,6 +197,23 @@ template <> struct Wfin<64> {
     static __device__ __forceinline__ unsigned gmax(T x) { return 0x7FFFu - (x & 0x7FFFu); }
 };
 
+// G = 64: rec[] as two arrays (span masks, code-point prefixes) -- 10 bytes per atom instead of the
+// 16 of an aligned struct, so LDS per wave (5.2 KB) holds more resident waves than the 24 that 80
+// VGPRs allow; rec[j] yields references to both fields, so the shared code reads L.rec[j].cpos alike
+template <int NA> struct RecSoA {
+    uint64_t sm[NA];
+    uint16_t cp[NA];
+    struct Ref { uint64_t &smask; uint16_t &cpos; };
+    struct CRef { const uint64_t &smask; const uint16_t &cpos; };
+    __device__ __forceinline__ Ref operator[](unsigned i) { return {sm[i], cp[i]}; }
+    __device__ __forceinline__ CRef operator[](unsigned i) const { return {sm[i], cp[i]}; }
+};
+#ifndef REC_SOA
+#define REC_SOA 1   // A/B knob: 0 = the 64-lane kernels' rec[] as an array of 16-byte structs (BLOOM 21.3 with
+                    // the arrays, 20.0 without, both at 24 waves per CU; 7 or 8 waves per SIMD with the arrays:
+                    // 20.4 / 20.3 -- spills; profiles/r03_ab.log r03ac)
+#endif
+
 template <int CH, int G>
 struct GroupLDS {
     using M = typename Group<G>::M;
@@ -204,7 +221,7 @@ struct GroupLDS {
     // rec[j]: code-point prefix of atom j (| CP_WS at word starts and at the window end) and the
     //         span mask of tokens of 1..G atoms starting at j; after phase B the mask field holds
     //         the first atom of selected token j (tokens tile the window)
-    typename Group<G>::Rec rec[NA];
+    std::conditional_t<(G == 64 && REC_SOA), RecSoA<NA>, typename Group<G>::Rec[NA]> rec;
     typename Group<G>::Fin fin[NA];   // per end position, see Group<G>
     // the final key of the word ending at atom e
     __device__ __forceinline__ typename Wfin<G>::T wkey(unsigned e) const {
@@ -2046,7 +2063,10 @@ tokenize_kernel(KernArgs ka) {
                     }
                     return res;
                 };
-                const unsigned C = (na + 63u) >> 6;
+#ifndef LANES64_ODD
+#define LANES64_ODD 0   // A/B knob: chunks of an odd number of ends (lanes' first entries on distinct LDS banks)
+#endif
+                const unsigned C = LANES64_ODD ? (((na + 63u) >> 6) | 1u) : (na + 63u) >> 6;
                 const unsigned c0 = min(lane * C, na), c1 = min(c0 + C, na);
                 const unsigned rs = nextcut(c0), re = nextcut(c1);
                 if (DPT_STOP == 25) return;   // diagnostic: cut points only
