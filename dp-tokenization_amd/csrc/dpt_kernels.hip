@@ -2084,8 +2084,17 @@ tokenize_kernel(KernArgs ka) {
 #ifndef PUSH_B
 #define PUSH_B 1   // A/B knob: edges per batch (BLOOM 17.2 GB/s at 1, 17.1 at 2, 16.5 at 4: profiles/r03_ab.log r03x)
 #endif
+#ifndef LANES64_ROW_T
+#define LANES64_ROW_T 0   // A/B knob: chunks spanning more ends than this run the 64-lane row recurrence (0: none;
+                          // BLOOM 16.4 / 18.7 / 20.7 GB/s at 8 / 16 / 32 against 21.5 without: profiles/r03_ab.log r03ae)
+#endif
+                // A long cut-free segment (a long word of overlapping tokens) is a sequential chain for
+                // its lane -- ends x edges of dependent LDS read-modify-writes, the wave's critical path.
+                // Such chunks are taken afterwards by the whole wave, one position per step with the
+                // candidates across the lanes (the row recurrence, restricted to the chunk).
+                const bool rowc = LANES64_ROW_T > 0 && re - rs > (unsigned)LANES64_ROW_T;
                 unsigned kcarry = FRESH;
-                for (unsigned j = rs; j < re; j++) {
+                for (unsigned j = rs; j < (rowc ? rs : re); j++) {
                     const uint64_t sm = L.rec[j].smask;
                     const unsigned cj = L.rec[j].cpos;
                     const unsigned kj = (j == rs || (cj & CP_WS)) ? FRESH : kcarry;
@@ -2122,6 +2131,37 @@ tokenize_kernel(KernArgs ka) {
 #pragma unroll
                         for (int q = 0; q < PUSH_B; q++)
                             if (hv[q]) fin2[j + 1u + dd[q]] = f[q];
+                    }
+                }
+                // ---- the long chunks, one after another, each over all lanes: lane d holds candidate
+                //      j = i-1-d with its state in row form ((cost+1) << 16 | G) and its span mask;
+                //      the chunk's first boundary is a fresh start (a cut), ends of words restart
+                for (uint64_t lm = ballot(rowc); lm; lm &= lm - 1ull) {
+                    const unsigned q = (unsigned)__builtin_ctzll(lm);
+                    const unsigned ra = __builtin_amdgcn_readlane(rs, q), rb = __builtin_amdgcn_readlane(re, q);
+                    constexpr unsigned ST0 = 0x10000u;
+                    const uint64_t m0 = L.rec[ra].smask;
+                    unsigned mlo = lane == 0 ? (unsigned)m0 : 0u, mhi = lane == 0 ? (unsigned)(m0 >> 32) : 0u;
+                    unsigned st = lane == 0 ? ST0 : 0u;
+                    unsigned cpj = lane == 0 ? (L.rec[ra].cpos & 0x7FFFu) : 0u;
+                    for (unsigned i = ra + 1u; i <= rb; i++) {
+                        const unsigned cur = L.rec[i].cpos;
+                        const uint64_t mi = L.rec[i].smask;
+                        const unsigned cpi = cur & 0x7FFFu;
+                        const unsigned span = cpi - cpj;
+                        const unsigned gj = st & 0x7FFFu;
+                        const unsigned kv = (st | 0x7FFFu) - (gj > span ? gj : span);
+                        const unsigned bit = (lane < 32u ? (mlo >> lane) : (mhi >> (lane - 32u))) & 1u;
+                        const unsigned key = bit ? kv : 0xFFFFFFFFu;
+                        const unsigned r = wave_min_u32(key);
+                        const uint64_t gmb = ballot(key == r);
+                        const uint64_t emb = ballot((key ^ r) < 0x8000u);
+                        if (lane == 0) fin2[i] = make_uint2((unsigned)__builtin_ctzll(gmb) | ((unsigned)__builtin_ctzll(emb) << 8), r);
+                        const bool wend = (cur & CP_WS) != 0;
+                        st = wave_shift_in(st, wend ? ST0 : (r ^ 0x7FFFu) + 0x10000u);
+                        cpj = wave_shift_in(cpj, cpi);
+                        mlo = wave_shift_in(mlo, (unsigned)mi);
+                        mhi = wave_shift_in(mhi, (unsigned)(mi >> 32));
                     }
                 }
                 if (DPT_STOP == 26) return;   // diagnostic: + the recurrence
