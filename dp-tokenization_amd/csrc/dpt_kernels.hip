@@ -3137,7 +3137,8 @@ static void launch_tok(const EncodeArgs &a, const TrieView &tv, uint64_t n_units
                        hipEvent_t ev_start = nullptr) {
     constexpr int lds = block_lds_bytes<CH, G>();
     uint64_t wpc = resident_per_cu<CH, G, BIG, WIDE, SW, RAW>();
-    if constexpr (G == 16 && !BIG) {
+    static const bool small_rule = getenv("DPT_NO_SMALL_WPC") == nullptr;   // (A/B: the rule below off)
+    if (G == 16 && !BIG && small_rule) {
         // small calls: no more resident waves than give every slot ~7 strings (rounds of 4 strings per
         // wave; a wave's last round is the tail): 125k strings run 3 % faster at 18 waves per CU than
         // at the occupancy limit of 22, 250k and more are fastest at 22 (profiles/r02_ab_issue_model.log)
