@@ -2113,6 +2113,23 @@ tokenize_kernel(KernArgs ka) {
                         fin2[j + 1u] = f;
                         kcarry = f.y;
                     }
+#ifndef PUSH32
+#define PUSH32 0   // A/B knob: 1 = the span mask walked as two 32-bit halves (one v_ffbl and 32-bit arithmetic per edge)
+#endif
+                    if (PUSH32 && PUSH_B == 1) {
+#pragma unroll
+                        for (int hh = 0; hh < 2; hh++) {
+                            uint32_t m32 = hh == 0 ? ((uint32_t)sm & ~1u) : (uint32_t)(sm >> 32);
+                            while (m32) {
+                                const unsigned dd = ffbl(m32) + 32u * (unsigned)hh;
+                                m32 &= m32 - 1u;
+                                uint2 f = fin2[j + 1u + dd];   // <= re: no token crosses a cut
+                                upd(f, dd);
+                                fin2[j + 1u + dd] = f;
+                            }
+                        }
+                        continue;
+                    }
                     uint64_t m = sm & ~1ull;
                     while (m) {
                         unsigned dd[PUSH_B];
