@@ -48,13 +48,9 @@
 
 namespace dpt {
 
-#ifndef LDS_ROT
-#define LDS_ROT 0   // A/B knob: lanes store their four consecutive dwords in an order rotated by lane / 8
-                    // (A0's end-mask updates): in order, lanes 8 apart hit one LDS bank
-#endif
-#ifndef PREP_ROT
-#define PREP_ROT 0  // the same for prep_window's atom stores (costs registers: the order is data-dependent)
-#endif
+// Compile-time options are diagnostics only (DPT_STOP, DPT_C2STOP, DPT_STAMPS: wrong results or extra
+// counters by design, never in the product build) plus PUSH32 (pending its A/B).  The alternatives
+// measured slower or neutral are gone from the source; DESIGN.md §9 lists them with their numbers.
 
 // ------------------------------------------------------------------ wave primitives
 
@@ -208,11 +204,6 @@ template <int NA> struct RecSoA {
     __device__ __forceinline__ Ref operator[](unsigned i) { return {sm[i], cp[i]}; }
     __device__ __forceinline__ CRef operator[](unsigned i) const { return {sm[i], cp[i]}; }
 };
-#ifndef REC_SOA
-#define REC_SOA 1   // A/B knob: 0 = the 64-lane kernels' rec[] as an array of 16-byte structs (BLOOM 21.3 with
-                    // the arrays, 20.0 without, both at 24 waves per CU; 7 or 8 waves per SIMD with the arrays:
-                    // 20.4 / 20.3 -- spills; profiles/r03_ab.log r03ac)
-#endif
 
 template <int CH, int G>
 struct GroupLDS {
@@ -221,7 +212,7 @@ struct GroupLDS {
     // rec[j]: code-point prefix of atom j (| CP_WS at word starts and at the window end) and the
     //         span mask of tokens of 1..G atoms starting at j; after phase B the mask field holds
     //         the first atom of selected token j (tokens tile the window)
-    std::conditional_t<(G == 64 && REC_SOA), RecSoA<NA>, typename Group<G>::Rec[NA]> rec;
+    std::conditional_t<(G == 64), RecSoA<NA>, typename Group<G>::Rec[NA]> rec;
     typename Group<G>::Fin fin[NA];   // per end position, see Group<G>
     // the final key of the word ending at atom e
     __device__ __forceinline__ typename Wfin<G>::T wkey(unsigned e) const {
@@ -342,17 +333,6 @@ struct EncodeArgs {
     uint32_t n_hist;                 //   zero before the finish pass adds to it (the scan kernel's duty otherwise)
 };
 
-#ifdef DPT_LANEDBG
-// diagnostic build only: lane-mode chunk values of string 0's first window
-__device__ unsigned g_lanedbg[16 * 16 + 4];
-#endif
-// A/B only: per-phase issue priority (PRIO_MODE 1: A and C2 -- the trie-walk phases -- at
-// priority 1; 2: B at priority 1; 0: none)
-#ifndef PRIO_MODE
-#define PRIO_MODE 0
-#endif
-#define PRIO_PHASE(k) do { if (PRIO_MODE == 1) __builtin_amdgcn_s_setprio((k) == 0 || (k) == 3 ? 1 : 0); \
-                           if (PRIO_MODE == 2) __builtin_amdgcn_s_setprio((k) == 1 ? 1 : 0); } while (0)
 #ifdef DPT_STAMPS
 // diagnostic build only: cycles per phase summed over waves (never in the product build)
 __device__ unsigned long long g_stamps[8];
@@ -620,64 +600,6 @@ template <int CH, int G, bool WIDE>
 __device__ bool prep_window(GroupLDS<CH, G> &L, uint8_t *gw, const WinRegs<CH> &W, uint64_t pos,
                             unsigned wlen, int mode, unsigned lane, unsigned &n_atoms_o, unsigned &n_words_o) {
     const bool raw = mode == 0;
-#ifndef PREP_ASCII
-#define PREP_ASCII 0   // A/B knob: 1 = pure-ASCII raw windows take this SWAR path (cfg2 100.60 vs 100.95 GB/s,
-                       // cfg4 66.87 vs 66.62: no gain, 3 more VGPR spills; profiles/r03_ab.log)
-#endif
-    if constexpr (PREP_ASCII && G == 16 && CH == 256 && !WIDE) {
-        // Pure-ASCII raw windows: atom k is byte k, so the atom offsets are the identity and only the
-        // newlines ('\n' = "<0x0A>", 6 code points) and the string's first atom ('\u2581' + c, 2) move the
-        // code-point prefixes -- per-byte equality masks of the lane's dword (SWAR) instead of per-byte
-        // flags, one scan, the lane's four rec[] entries in one 16-byte LDS store.
-        const uint32_t w = W.t[0];
-        const unsigned k0 = 4u * lane;
-        const unsigned nv = wlen > k0 ? min(wlen - k0, 4u) : 0u;   // the lane's bytes in the window
-        const uint32_t vm = nv >= 4u ? 0xFFFFFFFFu : ((1u << (8u * nv)) - 1u);
-        if (raw && !ballot((w & vm & 0x80808080u) != 0)) {
-            const bool first0 = pos == 0;   // byte 0 is the string's first atom
-            uint32_t nl = eq_bytes(w, 0x0A0A0A0Au) & vm;
-            uint32_t ws = eq_bytes(w, 0x20202020u) & vm;
-            if (lane == 0) {
-                if (first0) nl &= ~0x80u;   // '\u2581' + '\n': two code points, no expansion
-                ws |= 0x80u;                // a window starts with a word
-            }
-            const unsigned v = (unsigned)__builtin_popcount(nl) | ((unsigned)__builtin_popcount(ws) << 9);
-            const unsigned incl = wave_incl_scan_add(v);
-            const unsigned tot = __builtin_amdgcn_readlane(incl, 63);
-            const unsigned nlb = (incl - v) & 0x1FFu;   // newlines before the lane's first byte
-            const unsigned f1 = first0 ? 1u : 0u;
-            uint32_t r[4];
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const unsigned k = k0 + (unsigned)u;
-                const unsigned nlu = nlb + (unsigned)__builtin_popcount(nl & ((1u << (8u * (unsigned)u)) - 1u));
-                const unsigned cp = k + 5u * nlu + (k > 0 ? f1 : 0u);
-                r[u] = 0xFFFF0000u | cp | (((ws >> (8u * (unsigned)u + 7u)) & 1u) ? CP_WS : 0u);
-            }
-            uint32_t *rec32 = reinterpret_cast<uint32_t *>(L.rec);
-            if (nv == 4u) {
-                *reinterpret_cast<uint4 *>(&rec32[k0]) = make_uint4(r[0], r[1], r[2], r[3]);
-                *reinterpret_cast<uint32_t *>(&L.bytes[k0]) = w;
-            } else if (nv) {
-#pragma unroll
-                for (int u = 0; u < 4; u++)
-                    if ((unsigned)u < nv) rec32[k0 + u] = r[u];
-                *reinterpret_cast<uint32_t *>(&L.bytes[k0]) = w;
-            }
-#pragma unroll
-            for (int u = 0; u < 4; u++)
-                if ((unsigned)u < nv) L.aoff[k0 + u] = (typename GroupLDS<CH, G>::Idx)(k0 + (unsigned)u);
-            const unsigned cp_tot1 = wlen + 5u * (tot & 0x1FFu) + f1;
-            if (lane == 0) {
-                L.aoff[wlen] = (typename GroupLDS<CH, G>::Idx)wlen;
-                rec32[wlen] = 0xFFFF0000u | cp_tot1 | CP_WS;
-            }
-            n_atoms_o = wlen;
-            n_words_o = tot >> 9;
-            wave_sync();
-            return true;
-        }
-    }
     unsigned n_atoms = 0, cp_tot = 0, n_words = 0;
     bool hi_byte = false;   // some byte >= 0x80: atoms may be longer than one byte
 #pragma unroll
@@ -719,34 +641,23 @@ __device__ bool prep_window(GroupLDS<CH, G> &L, uint8_t *gw, const WinRegs<CH> &
         unsigned wi = n_words + ((ex >> 9) & 0x1FFu);
         const unsigned cp0 = cp_tot + (ex >> 18);
         if (c0 + lane * 4 < wlen) *reinterpret_cast<uint32_t *>(&L.bytes[c0 + lane * 4]) = W.t[c];
-        // the lane's atoms and their code-point prefixes, then the stores in an order rotated by
-        // lane / 8 (ASCII: atom index 4 lane + u, so in order lanes 8 apart hit one bank -- see A0)
-        unsigned aiu[4], cpu[4];
+        // the lane's atoms and their code-point prefixes
+        unsigned aiu[4];
         {
             unsigned ai = ai0, cp = cp0;
 #pragma unroll
             for (int u = 0; u < 4; u++) {
-                aiu[u] = ai; cpu[u] = cp;
+                aiu[u] = ai;
+                const unsigned k = c0 + lane * 4 + u;
+                if (ast[u]) {
+                    L.aoff[ai] = (typename GroupLDS<CH, G>::Idx)k;
+                    if constexpr (G == 16)   // end masks start all-dead (inverted); phase A clears token bits
+                        reinterpret_cast<uint32_t *>(L.rec)[ai] = 0xFFFF0000u | cp | (wst[u] ? CP_WS : 0u);
+                    else
+                        L.rec[ai].cpos = (uint16_t)(cp | (wst[u] ? CP_WS : 0));
+                }
                 ai += ast[u] ? 1u : 0u;
                 cp += cpl[u];
-            }
-        }
-        const unsigned rot = (G == 16 && PREP_ROT) ? (lane >> 3) & 3u : 0u;
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const unsigned uu = ((unsigned)u + rot) & 3u;
-            // (selects over the four registers: a variable index would put the arrays in scratch)
-            const unsigned a_ = uu == 0 ? aiu[0] : (uu == 1 ? aiu[1] : (uu == 2 ? aiu[2] : aiu[3]));
-            const unsigned c_ = uu == 0 ? cpu[0] : (uu == 1 ? cpu[1] : (uu == 2 ? cpu[2] : cpu[3]));
-            const bool as_ = uu == 0 ? ast[0] : (uu == 1 ? ast[1] : (uu == 2 ? ast[2] : ast[3]));
-            const bool ws_ = uu == 0 ? wst[0] : (uu == 1 ? wst[1] : (uu == 2 ? wst[2] : wst[3]));
-            const unsigned k = c0 + lane * 4 + uu;
-            if (as_) {
-                L.aoff[a_] = (typename GroupLDS<CH, G>::Idx)k;
-                if constexpr (G == 16)   // end masks start all-dead (inverted); phase A clears token bits
-                    reinterpret_cast<uint32_t *>(L.rec)[a_] = 0xFFFF0000u | c_ | (ws_ ? CP_WS : 0u);
-                else
-                    L.rec[a_].cpos = (uint16_t)(c_ | (ws_ ? CP_WS : 0));
             }
         }
         // (the 256-byte pass's word list lives in global scratch and is needed only by row-mode
@@ -788,28 +699,13 @@ __device__ bool prep_window(GroupLDS<CH, G> &L, uint8_t *gw, const WinRegs<CH> &
 
 // ------------------------------------------------------------------ the tokenize kernel
 
-#ifndef NPART
-#define NPART 16      // first-pass work partitions (<= NPART_MAX)
-#endif
+constexpr unsigned NPART = 16;   // first-pass work partitions (<= NPART_MAX)
 static_assert(NPART >= 1 && NPART <= NPART_MAX, "NPART");
-#ifndef LANES64
-#define LANES64 1   // A/B knob: 0 = capless 64-lane windows run the row recurrence
-#endif
-#ifndef A_REFILL
-#define A_REFILL 32   // phase A: idle lanes needed before a batched refill (1/8/16/32 within 2 %)
-#endif
-#ifndef A_REFILL64
-#define A_REFILL64 32   // the same for the 64-lane kernels (one string per wave: long walks leave lanes idle)
-#endif
-#ifndef DPT_DOUBLE   // diagnostic builds only: run one phase twice to measure its marginal cost (1 A, 3 C1, 4 C2, 5 prep)
-#define DPT_DOUBLE 0
-#endif
+constexpr unsigned A_REFILL = 32;     // phase A: idle lanes needed before a batched refill (1/8/16/32 within 2 %)
+constexpr unsigned A_REFILL64 = 32;   // the same for the 64-lane kernels (8 / 1: neutral / -0.5 %, r03aa)
 #ifndef DPT_STOP     // diagnostic builds only (wrong results): 1 = prep only, 21 = + A0, 2 = + A, 25 / 26 / 27 =
                      // + lane-mode B's cut points / recurrence / transfer scan + fix-up, 3 = + B/C0/C1
 #define DPT_STOP 9
-#endif
-#ifndef DPT_NOSTORE   // diagnostic builds only (wrong results): C2's bulk pass (1) / hash pass (2) store no ids
-#define DPT_NOSTORE 0
 #endif
 #ifndef DPT_C2STOP   // diagnostic builds only (wrong results): C2 stops after its bulk pass (1) / hash pass (2)
 #define DPT_C2STOP 0
@@ -817,14 +713,11 @@ static_assert(NPART >= 1 && NPART <= NPART_MAX, "NPART");
 #define DPT_RUN_B (DPT_STOP >= 3 && DPT_STOP != 21)
 #define DPT_RUN_C2 (DPT_STOP == 9)
 
-#ifndef WPE64
-#define WPE64 6   // the 256-byte 64-lane kernel: 6 waves per SIMD by VGPRs (<= 80; LDS allows 24 per CU):
-                  // BLOOM 17.4 -> 19.8 GB/s against no cap (95 VGPRs, 20 waves; profiles/r03_ab.log r03aa)
-#endif
-// 256-byte 16-lane rows: 6 waves per SIMD by VGPRs (<= 80), so LDS (22 waves per CU) binds
-#ifndef WPE16
-#define WPE16 6
-#endif
+// Waves per SIMD by VGPRs (<= 80 VGPRs each).  The 256-byte 16-lane rows: LDS (22 waves per CU) then
+// binds (96 VGPRs / 5 waves: no scratch spills, cfg2 -1.9 %, r03e).  The 256-byte 64-lane kernel: BLOOM
+// 17.4 -> 19.8 GB/s against no cap (95 VGPRs, 20 waves; 7 or 8 waves spill more: r03aa, r03ac).
+constexpr int WPE16 = 6;
+constexpr int WPE64 = 6;
 // The kernel's arguments, as one struct at the start of the kernarg segment
 struct KernArgs {
     EncodeArgs ea;
@@ -835,9 +728,6 @@ typedef __attribute__((address_space(4))) const KernArgs ConstKernArgs;
 // boundary: each phase then loads (s_load, scalar-cache hits) the few arguments it uses instead of
 // the compiler keeping all ~30 of them in SGPRs across the whole loop -- the hot kernel sits at the
 // SGPR limit and spills.
-#ifndef KARG_REFRESH
-#define KARG_REFRESH 1
-#endif
 // (a field-wise copy: only the fields a use reads are loaded)
 __device__ __forceinline__ TrieView tv_of(ConstKernArgs *kp) {
     TrieView t;
@@ -845,15 +735,8 @@ __device__ __forceinline__ TrieView tv_of(ConstKernArgs *kp) {
     t.root_base = kp->tv.root_base; t.n_slots = kp->tv.n_slots; t.pair16 = kp->tv.pair16;
     return t;
 }
-#ifndef KREF_MORE
-#define KREF_MORE 0   // A/B knob: also refresh inside phases A and C2 (before the walkers and the hash pass)
-#endif
-#if KARG_REFRESH
 // (the 16-lane instantiations: the 64-lane ones do not spill, and measured 1.7 % slower with it)
 #define KREFRESH() do { if constexpr (G == 16) asm volatile("" : "+s"(kp)); } while (0)
-#else
-#define KREFRESH() do { } while (0)
-#endif
 
 // SW: staged id width 0 = by a.staging16, 1 = int16, 2 = int32; RAW: DPT_MODE_RAW as a compile-time
 // constant (its expansions and word starts fold away in the other modes' code and vice versa -- the
@@ -1024,25 +907,6 @@ tokenize_kernel(KernArgs ka) {
 #pragma unroll
             for (int g = 0; g < NG; g++) todo |= (uni(SS[g].active) && !((prepared >> g) & 1u)) ? (1u << g) : 0u;
             if (!todo) break;
-#if DPT_DOUBLE == 5   // diagnostic: the slots' loads and prep once more, results dropped
-            {
-                WinRegs<CH> W[NG];
-#pragma unroll
-                for (int g = 0; g < NG; g++) {
-                    if (!((todo >> g) & 1u)) continue;
-                    const uint64_t sb = uni64(SS[g].sb);
-                    load_window<CH>(W[g], a.text + sb, raw ? nullptr : a.cut_mask + sb, uni64(SS[g].pos), uni64(SS[g].slen), raw, lane);
-                }
-#pragma unroll
-                for (int g = 0; g < NG; g++) {
-                    if (!((todo >> g) & 1u)) continue;
-                    unsigned wlen = 0, na = 0, nw = 0;
-                    if (uni(SS[g].status) != 2 && window_bounds<CH>(W[g], uni64(SS[g].slen), uni64(SS[g].pos), mode, lane, wlen))
-                        prep_window<CH, G, WIDE>(grp(g), wsl_of(g), W[g], uni64(SS[g].pos), wlen, mode, lane, na, nw);
-                }
-                wave_sync();
-            }
-#endif
             WinRegs<CH> W[NG];
 #pragma unroll
             for (int g = 0; g < NG; g++) {
@@ -1092,14 +956,9 @@ tokenize_kernel(KernArgs ka) {
         wave_sync();
         if (busy == 0) break;
         STAMP(0);
-        PRIO_PHASE(0);
 
         // ---------------------------------------------------------- A: match discovery (all slots)
         KREFRESH();
-#if DPT_DOUBLE == 1
-        for (int rep_ = 0; rep_ < 2; rep_++) {
-            if (rep_) wave_sync();
-#endif
         if (DPT_STOP > 1) {
             // A0 (16-lane rows, raw mode): slots whose window is pure ASCII -- atoms are its bytes --
             // get every walk's first lookup here, byte-parallel with four loads in flight per lane;
@@ -1195,71 +1054,36 @@ tokenize_kernel(KernArgs ka) {
                         auto byte_at = [&](unsigned q) -> unsigned {   // byte k0+q, END past the window
                             return k0 + q < wl ? (unsigned)((w >> (8u * q)) & 0xFFu) : END;
                         };
-#ifndef A0_PACK
-#define A0_PACK 1   // A/B knob: 0 = A0 reads the 16-B root-table / root-child entries (slots4)
-#endif
-#ifndef A0_INFLIGHT
-#define A0_INFLIGHT 4
-#endif
                         uint32_t *r32 = reinterpret_cast<uint32_t *>(smem + gbase);
                         bool nocap = false;
                         unsigned tk1 = 0, tk2 = 0;
+                        // the packed byte-pair table over (byte, next byte): the flags of the first byte do
+                        // not depend on the second; four lookups in flight per lane
+                        uint2 ent[4];
 #pragma unroll
-                        for (int u0 = 0; u0 < 4; u0 += A0_INFLIGHT) {
-                        int32_t idx[A0_INFLIGHT];
-#pragma unroll
-                        for (int uq = 0; uq < A0_INFLIGHT; uq++) {
-                            const int u = u0 + uq;
+                        for (int u = 0; u < 4; u++) {
                             const unsigned b = byte_at(u), n1 = byte_at(u + 1);
-                            // (flags as 0/1 integers combined with & and |: short-circuit forms become
-                            // exec-mask branches here)
-                            const unsigned stop = (unsigned)(n1 == END) | (unsigned)(n1 == ' ');
                             const unsigned e1 = n1 == '\n' ? (unsigned)'<' : n1;
-                            // a one-byte atom at the word's end: its own slot; else the two-byte root entry
-#if A0_PACK
-                            // the packed byte-pair table: the flags of b0 do not depend on the second byte
-                            (void)stop;
-                            idx[uq] = (int32_t)(((b & 0xFFu) << 8) | (e1 & 0xFFu));
-#else
-                            const int32_t i1 = tv.root_base + (int32_t)(b & 0xFFu);
-                            const int32_t i2 = (int32_t)(tv.n_slots + ((b & 0xFFu) << 8) + (e1 & 0xFFu));
-                            idx[uq] = stop ? i1 : i2;
-#endif
+                            ent[u] = reinterpret_cast<const uint2 *>(tv.pair16 + PAIR16_N)[((b & 0xFFu) << 8) | (e1 & 0xFFu)];
                         }
-#if A0_PACK
-                        uint2 ent[A0_INFLIGHT];
-#pragma unroll
-                        for (int uq = 0; uq < A0_INFLIGHT; uq++) ent[uq] = reinterpret_cast<const uint2 *>(tv.pair16 + PAIR16_N)[idx[uq]];
-#else
-                        int4 ent[A0_INFLIGHT];
-#pragma unroll
-                        for (int uq = 0; uq < A0_INFLIGHT; uq++) ent[uq] = trie_slotA(tv, idx[uq]);
-#endif
                         // Per byte: tk1 bit u = a one-atom token ends at k0+1+u, tk2 bit u = a two-atom
                         // token ends at k0+2+u (the end masks are written once below)
+                        // (flags as 0/1 integers combined with & and |: short-circuit forms become
+                        // exec-mask branches here)
 #pragma unroll
-                        for (int uq = 0; uq < A0_INFLIGHT; uq++) {
-                            const int u = u0 + uq;
+                        for (int u = 0; u < 4; u++) {
                             const unsigned k = k0 + (unsigned)u;
                             const unsigned b = byte_at(u), n1 = byte_at(u + 1), n2 = byte_at(u + 2);
-                            const auto e = ent[uq];
+                            const auto e = ent[u];
                             const unsigned valid = (unsigned)(b != END);
                             const unsigned special = (unsigned)(b == ' ') | (unsigned)(b == '\n') | ((unsigned)first & (unsigned)(k == 0));   // the walker's
                             const unsigned norm = valid & (special ^ 1u);
                             // n1 ends the word: the lookup was the atom's own root slot
                             const unsigned wend = (unsigned)(n1 == END) | (unsigned)(n1 == ' ');
-#if A0_PACK
                             const unsigned xterm = ((unsigned)e.x >> 3) & 1u, xleaf = ((unsigned)e.x >> 4) & 1u;
                             const unsigned tok1 = (unsigned)e.x & ((unsigned)e.x >> 1) & 1u;
                             const unsigned node2 = ((unsigned)e.x >> 2) & 1u;
                             const unsigned filt = (unsigned)e.y;
-#else
-                            const unsigned y30 = ((unsigned)e.y >> 30) & 1u, y31 = (unsigned)e.y >> 31;
-                            const unsigned xterm = (unsigned)e.x >> 31, xleaf = ((unsigned)e.x >> 30) & 1u;
-                            const unsigned tok1 = wend ? ((unsigned)(e.y == 0) & xterm) : (y30 & y31);
-                            const unsigned node2 = y30 & (unsigned)((e.y & 0x3FFFFFFF) != 0);
-                            const unsigned filt = (unsigned)e.w;
-#endif
                             nocap |= (norm & (tok1 ^ 1u)) != 0;
                             // a node after two bytes: n1 = '\n' leaves the walk inside "<0x0A>" after
                             // its '<'; otherwise atom k+1 is consumed (the span k .. k+2)
@@ -1272,19 +1096,15 @@ tokenize_kernel(KernArgs ka) {
                             tk2 |= (has2 & (nl1 ^ 1u) & xterm) << u;
                             mark |= ((valid & special) | more) << (4 * g + u);
                         }
-                        }
                         // end k0+1+u: tk1 bit u, and tk2 bit u-1 (u = 0: the previous lane's bit 3)
                         const unsigned t2e = ((tk2 << 1) & 0xEu) | wave_shift_in((tk2 >> 3) & 1u, 0u);
                         if (ballot((tk1 | t2e) != 0)) {
-                            // lane l's dwords are 4l+1 .. 4l+4: in order, lanes l, l+8, l+16, l+24 of a 32-lane
-                            // group hit one bank (4-way, 2x on a store); rotated by (l / 8) % 4 no two do
-                            const unsigned rot = LDS_ROT ? (lane >> 3) & 3u : 0u;
+                            // (lane l's dwords are 4l+1 .. 4l+4: lanes l, l+8, l+16, l+24 of a 32-lane group hit
+                            // one bank; a rotated order spilled VGPRs, r03)
 #pragma unroll
-                            for (int u = 0; u < 4; u++) {
-                                const unsigned uu = ((unsigned)u + rot) & 3u;
-                                __hip_atomic_fetch_and(&r32[k0 + 1u + uu], ~((((tk1 >> uu) & 1u) << 16) | (((t2e >> uu) & 1u) << 17)),
+                            for (int u = 0; u < 4; u++)
+                                __hip_atomic_fetch_and(&r32[k0 + 1u + u], ~((((tk1 >> u) & 1u) << 16) | (((t2e >> u) & 1u) << 17)),
                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                            }
                         }
                         if (ballot(nocap) && lane == 0) SS[g].capb = 1;
                         // the slot's marked atoms, in order, into its fin[] (free until phase B)
@@ -1300,16 +1120,6 @@ tokenize_kernel(KernArgs ka) {
                     }
                 }
             }
-#ifndef A_SCHED
-#define A_SCHED 1   // A/B knob: 0 = no scheduling barrier between the ASCII walker's byte read and trie load
-#endif
-#ifndef A_ONEEDGE
-#define A_ONEEDGE 1   // A/B knob: 0 = the ASCII walker skips the step when no lane is active (two back edges)
-#endif
-#ifndef A_FAST
-#define A_FAST 1   // A/B knob: 0 = the generic walker takes A0's marked starts too
-#endif
-            if (KREF_MORE) KREFRESH();
             // ASCII walker: the marked starts of A0 slots (pure-ASCII raw windows: an atom is one byte, a
             // word start ' ' is '\u2581' = the trie node ws_node, '\n' is "<0x0A>", the string's first
             // atom '\u2581' + its byte) walked byte by byte without the generic walker's atom
@@ -1317,7 +1127,7 @@ tokenize_kernel(KernArgs ka) {
             // and two-atom tokens already recorded by A0) repeats that lookup in the root table and goes on
             // from the node after two bytes.  The generic walker below takes the other slots.
             if constexpr (G == 16 && !BIG) {
-                if (A_FAST && a0mask) {
+                if (a0mask) {
                     unsigned fpre[NG + 1];
                     fpre[0] = 0;
 #pragma unroll
@@ -1407,17 +1217,12 @@ tokenize_kernel(KernArgs ka) {
                         // (a start can be over at once, so a refill may leave every lane idle with starts left:
                         // the step then runs with no lane active and changes nothing -- one back edge, so
                         // the walk state stays in its registers across it)
-                        if (A_ONEEDGE) {
-                            if (!ballot(act) && nxt >= ftotal) break;
-                        } else if (!ballot(act)) {
-                            if (nxt >= ftotal) break;
-                            continue;
-                        }
+                        if (!ballot(act) && nxt >= ftotal) break;
                         // the next raw byte, read before the trie load returns (masked off past the window)
-                        // (kept ahead of the load: else its address register may reuse the load's dead .z
-                        // and wait for it)
+                        // (kept ahead of the load by a scheduling barrier: else its address register may
+                        // reuse the load's dead .z and wait for it)
                         const unsigned nbv = grp_bytes_at(fl, fp);
-                        if (A_SCHED) __builtin_amdgcn_sched_barrier(0);
+                        __builtin_amdgcn_sched_barrier(0);
                         const int32_t t = isr ? ft2 : fnb + (int32_t)cur;
                         const int4 ent = trie_slotA(tv, t);
                         const unsigned y = (unsigned)ent.y;
@@ -1454,7 +1259,6 @@ tokenize_kernel(KernArgs ka) {
                     }
                 }
             }
-            if (KREF_MORE) KREFRESH();
             unsigned pre[NG + 1];
             pre[0] = 0;
 #pragma unroll
@@ -1490,32 +1294,14 @@ tokenize_kernel(KernArgs ka) {
                 }
                 if (!ballot(active)) break;
                 const int32_t t = t2 ? (int32_t)t2 : nb + (int32_t)(seq & 0xFFu);
-#ifndef A_SLOT8
-#define A_SLOT8 1   // A/B knob: the 64-lane kernels' walks read the 8-byte slots (no child filter: half the
-                    // footprint of a BLOOM-scale trie, one more failing lookup per walk)
-#endif
+                // (the 64-lane kernels' walks read the 8-byte slots -- no child filter: half the footprint
+                // of a BLOOM-scale trie, one more failing lookup per walk)
                 int4 ent;
-                if constexpr (A_SLOT8 && G == 64) {
+                if constexpr (G == 64) {
                     const int2 e2 = trie_slot(tv, t);
                     ent = make_int4(e2.x, e2.y, 0, -1);
                 } else {
                     ent = trie_slotA(tv, t);   // buffer load: inactive lanes read harmlessly
-                }
-#ifndef A_PREF
-#define A_PREF 0   // A/B knob: 1 = the next atom's descriptor + bytes read before the trie load returns (measured
-                   // slower: BLOOM 17.6 -> 17.25, cfg5 81.6 -> 80.8 GB/s; profiles/r03_ab.log r03z)
-#endif
-                // The atom after this step's byte, if the byte ends the current one: j + len after the
-                // step (the root-table split sets len to 1 first).  Known without the trie entry, so its
-                // two dependent LDS reads overlap the load; used only when the atom ends (cont).
-                unsigned inf_pre = 0, cn_pre = 0;
-                uint64_t sq_pre = 0;
-                if (A_PREF) {
-                    const unsigned cpost = t2 ? cnt : cnt - 1u;
-                    const unsigned lpre = ((t2 && split) ? 1u : len) + (cpost == 0 ? 1u : 0u);
-                    const GL &L = *reinterpret_cast<const GL *>(smem + lbase);
-                    inf_pre = ainfo_get(L, j + lpre, false);
-                    sq_pre = atom_from_info<CH, WIDE>(L.bytes, inf_pre, raw, cn_pre);
                 }
                 // The step as selects (few exec-mask branches: their scalar bookkeeping costs issue
                 // slots like the vector work does).  Root-table entry (t2): .y = node after two
@@ -1550,14 +1336,11 @@ tokenize_kernel(KernArgs ka) {
                 const unsigned cont = aend & ((leaf | (unsigned)((info & AInfo<CH>::STOP) != 0) | (unsigned)(len == (unsigned)G)) ^ 1u);
                 {
                     // the next atom, read by every lane (j + len <= n_atoms: in the window's arrays)
+                    // (reading it a step ahead, before the trie load returns, measured slower: r03z)
                     const GL &L = *reinterpret_cast<const GL *>(smem + lbase);
-                    unsigned cn = cn_pre;
-                    unsigned inf = inf_pre;
-                    uint64_t sq = sq_pre;
-                    if (!A_PREF) {
-                        inf = ainfo_get(L, j + len, false);
-                        sq = atom_from_info<CH, WIDE>(L.bytes, inf, raw, cn);
-                    }
+                    unsigned cn = 0;
+                    const unsigned inf = ainfo_get(L, j + len, false);
+                    const uint64_t sq = atom_from_info<CH, WIDE>(L.bytes, inf, raw, cn);
                     info = cont ? inf : info;
                     seq = cont ? sq : seq;
                     cnt = cont ? cn : cnt;
@@ -1580,39 +1363,11 @@ tokenize_kernel(KernArgs ka) {
             for (int g = 0; g < NG; g++)
                 if (ballot((capm >> g) & 1u) && lane == 0) SS[g].capb = 1;
         }
-#if DPT_DOUBLE == 1
-        }
-#endif
         wave_sync();
         STAMP(1);
-        PRIO_PHASE(1);
 
         // ---------------------------------------------------------- B: forward recurrence
         KREFRESH();
-#ifndef PF_NEXT
-#define PF_NEXT 0   // A/B knob: the next windows of continuing strings pulled into L2 during B (1) / B and C1 (2)
-#endif
-        // B and C1 issue no vector-memory loads (16-lane rows), so a load issued here waits for nothing
-        // and holds nothing up: one dword per 128-byte line of each continuing slot's next window,
-        // so that the next prep's window load hits L2 instead of HBM.  (Inline asm: a compiler-visible
-        // load may be sunk next to its only use; the compiler's waitcnts stay correct -- vmcnt returns
-        // in issue order, so its waits for later loads also cover this one -- and the register is held
-        // until the explicit wait at the end of B or C1.)
-        uint32_t pfv = 0;
-        if constexpr (PF_NEXT && G == 16 && !BIG) {
-            if (lane < 3u * (unsigned)NG) {
-                const unsigned g = lane / 3u, k = lane - 3u * g;
-                const SlotState &S = SS[g];
-                const uint64_t np = (uint64_t)S.pos + S.wlen;
-                if (S.active && S.n_atoms > 0 && np < S.slen) {
-                    uint64_t off = (uint64_t)S.sb + np + 128u * k;
-                    const uint64_t last = (uint64_t)S.sb + S.slen - 1u;
-                    off = (off < last ? off : last) & ~(uint64_t)3;
-                    const uint8_t *p = a.text + off;
-                    asm volatile("global_load_dword %0, %1, off" : "=v"(pfv) : "v"(p));
-                }
-            }
-        }
         bool lane_mode = false;   // B ran per chunk and did C0 and C1 itself (G = 16, capless, no edges)
         if (DPT_RUN_B) {
             GL &L = grp(mg);
@@ -1790,86 +1545,28 @@ tokenize_kernel(KernArgs ka) {
                 unsigned cprev = rec32[rs] & 0x7FFu;
                 unsigned nxt = rec32[rs + 1u];   // rs + 1 <= na + 1 < NA
                 unsigned T = 0;                  // tokens of the chunk: the pieces' costs
-#ifndef LANE_PF
-#define LANE_PF 0   // A/B knob: candidates of the next position read a step ahead (0..2); 1 and 2 measured
-                    // slower (cfg4 67.6 -> 65.5 / 62.7 GB/s, cfg2 101.2 -> 99.6 / 94.9: profiles/r03_ab.log r03y)
-#endif
-                // LANE_PF > 0: the entries of position i+1's first candidates (j = i - dd, final by step
-                // i) are read during step i, from its end mask loaded a step earlier (nxt2), so their
-                // LDS latency overlaps step i's work instead of heading step i+1's chain
-                unsigned nxt2 = LANE_PF ? rec32[rs + 2u] : 0u;   // (<= NA: rec[NA] is the next LDS field, unused)
-                unsigned pda = 0, pdb = 0, pra = 0, prb = 0;     // this position's prefetched candidates (dd 0: none)
+                // (reading the next position's first candidates a step ahead, or two candidates per inner
+                // iteration, measured slower: r03y, r03)
                 while (ballot(i < re)) {
                     if (i < re) {
                         i++;
                         const unsigned r = nxt;
-                        unsigned qa = 0, qb = 0, qra = 0, qrb = 0;
-                        if (LANE_PF) {
-                            nxt = nxt2;
-                            nxt2 = rec32[i + 2u];
-                            unsigned mn = i < re ? (~nxt >> 17) & 0x7FFFu : 0u;   // position i+1's longer tokens
-                            qa = mn ? ffbl(mn) + 1u : 0u;
-                            mn &= mn - 1u;
-                            qra = rec32[i - qa];                 // (qa 0: rec[i] -- read, unused)
-                            if (LANE_PF > 1) {
-                                qb = mn ? ffbl(mn) + 1u : 0u;
-                                qrb = rec32[i - qb];
-                            }
-                        } else {
-                            nxt = rec32[i + 1u];
-                        }
+                        nxt = rec32[i + 1u];
                         const unsigned cpi = r & 0x7FFu;             // bits 11..14: see below
                         unsigned best = relax(sprev, cpi - cprev);   // j = i-1: the single atom
                         unsigned dg = 0, de = 0;
                         unsigned m = (~r >> 17) & 0x7FFFu;          // longer tokens ending at i: bit d-1
-                        if (LANE_PF) {
-                            // the prefetched candidates are m's lowest bits, in order
-                            auto cand = [&](unsigned dd, unsigned rj) {
-                                const unsigned j = i - 1u - dd;
-                                const unsigned sj = j == ws ? FRESH : (rj >> 16);
-                                const unsigned kk = dd ? relax(sj, cpi - (rj & 0x7FFu)) : 0xFFFFFFFFu;
-                                if ((kk >> 5) < (best >> 5)) de = dd;
-                                if (kk < best) dg = dd;
-                                best = kk < best ? kk : best;
-                            };
-                            cand(pda, pra);
-                            m &= pda ? m - 1u : m;
-                            if (LANE_PF > 1) {
-                                cand(pdb, prb);
-                                m &= pdb ? m - 1u : m;
-                            }
-                            pda = qa; pdb = qb; pra = qra; prb = qrb;
-                        }
-#ifndef B_PAIR
-#define B_PAIR 0   // A/B knob: candidates per inner iteration taken two at a time (both LDS reads in flight):
-                   // cfg4 +0.9 %, cfg2 -0.9 % (profiles/r03_ab.log)
-#endif
                         while (m) {
                             const unsigned dd = ffbl(m) + 1u;
                             m &= m - 1u;
                             const unsigned j = i - 1u - dd;          // j >= ws: spans cross no cut
                             const unsigned rj = rec32[j];
-                            unsigned dd2 = dd, rj2 = 0;
-                            const bool two = B_PAIR && m != 0;
-                            if (B_PAIR) {
-                                dd2 = two ? ffbl(m) + 1u : dd;
-                                m &= two ? m - 1u : m;
-                                rj2 = rec32[i - 1u - dd2];           // (dd2 = dd when there is no second: read again, unused)
-                            }
                             const unsigned sj = j == ws ? FRESH : (rj >> 16);
                             const unsigned kk = relax(sj, cpi - (rj & 0x7FFu));
                             // ascending d = descending j: the first strict improvement is the largest j
                             if ((kk >> 5) < (best >> 5)) de = dd;
                             if (kk < best) dg = dd;
                             best = kk < best ? kk : best;
-                            if (B_PAIR) {
-                                const unsigned j2 = i - 1u - dd2;
-                                const unsigned sj2 = j2 == ws ? FRESH : (rj2 >> 16);
-                                const unsigned kk2 = two ? relax(sj2, cpi - (rj2 & 0x7FFu)) : 0xFFFFFFFFu;
-                                if ((kk2 >> 5) < (best >> 5)) de = dd2;
-                                if (kk2 < best) dg = dd2;
-                                best = kk2 < best ? kk2 : best;
-                            }
                         }
                         L.rec[i].smask = (uint16_t)best;   // this end's mask was read above
                         L.fin[i].v = (uint8_t)(dg | (de << 4));
@@ -1999,15 +1696,6 @@ tokenize_kernel(KernArgs ka) {
                 flag_r((unsigned)__builtin_amdgcn_update_dpp(0, (int)fl, 0x108, 0xF, 0xF, false));   // row_shl:8
                 const unsigned fln = (unsigned)__builtin_amdgcn_update_dpp(0, (int)fl, 0x101, 0xF, 0xF, false);
                 const bool fin_in = !re_ws && (fln & 1u) != 0;
-#ifdef DPT_LANEDBG
-                if (lane == 0) atomicAdd(&g_lanedbg[16 * 16 + 2], 1u);
-                if (SS[mg].s == 0 && na > 0) {
-                    unsigned *o = g_lanedbg + d * 16;
-                    o[0] = rs; o[1] = re; o[2] = pe; o[3] = T; o[4] = tb; o[5] = gin; o[6] = gre; o[7] = ls1;
-                    o[8] = left_of_q; o[9] = fl; o[10] = fin_in; o[11] = n1; o[12] = afin; o[13] = lsm;
-                    o[14] = re_ws | (p1in << 1) | (walk << 2); o[15] = in;
-                }
-#endif
                 // q's chunk with a chance L* token to the right: P1 again in de mode (A = L*);
                 // P1 starts below L* only from rs with gin < L* or from a word start inside
                 if (walk && fin_in && !left_of_q && (!p1in || gin < ls1)) {
@@ -2063,10 +1751,7 @@ tokenize_kernel(KernArgs ka) {
                     }
                     return res;
                 };
-#ifndef LANES64_ODD
-#define LANES64_ODD 0   // A/B knob: chunks of an odd number of ends (lanes' first entries on distinct LDS banks)
-#endif
-                const unsigned C = LANES64_ODD ? (((na + 63u) >> 6) | 1u) : (na + 63u) >> 6;
+                const unsigned C = (na + 63u) >> 6;   // (odd chunk lengths: -0.5 %, r03ad)
                 const unsigned c0 = min(lane * C, na), c1 = min(c0 + C, na);
                 const unsigned rs = nextcut(c0), re = nextcut(c1);
                 if (DPT_STOP == 25) return;   // diagnostic: cut points only
@@ -2079,22 +1764,11 @@ tokenize_kernel(KernArgs ka) {
                 }
                 // ---- push: j ascending; j's key is final once every earlier start of the chunk ran --
                 //      it is the j-1 -> j edge's result (bit 0: capless windows have it at every start),
-                //      carried in a register.  The edges of a start go in batches of PUSH_B: their entry
-                //      reads in flight together (distinct entries), then the updates, then the writes.
-#ifndef PUSH_B
-#define PUSH_B 1   // A/B knob: edges per batch (BLOOM 17.2 GB/s at 1, 17.1 at 2, 16.5 at 4: profiles/r03_ab.log r03x)
-#endif
-#ifndef LANES64_ROW_T
-#define LANES64_ROW_T 0   // A/B knob: chunks spanning more ends than this run the 64-lane row recurrence (0: none;
-                          // BLOOM 16.4 / 18.7 / 20.7 GB/s at 8 / 16 / 32 against 21.5 without: profiles/r03_ab.log r03ae)
-#endif
-                // A long cut-free segment (a long word of overlapping tokens) is a sequential chain for
-                // its lane -- ends x edges of dependent LDS read-modify-writes, the wave's critical path.
-                // Such chunks are taken afterwards by the whole wave, one position per step with the
-                // candidates across the lanes (the row recurrence, restricted to the chunk).
-                const bool rowc = LANES64_ROW_T > 0 && re - rs > (unsigned)LANES64_ROW_T;
+                //      carried in a register.  One edge at a time: batches of 2 / 4 edges with their reads
+                //      in flight (r03x) and giving long chunks to the whole wave as a row recurrence (r03ae)
+                //      measured slower -- the push is throughput-bound across the resident waves.
                 unsigned kcarry = FRESH;
-                for (unsigned j = rs; j < (rowc ? rs : re); j++) {
+                for (unsigned j = rs; j < re; j++) {
                     const uint64_t sm = L.rec[j].smask;
                     const unsigned cj = L.rec[j].cpos;
                     const unsigned kj = (j == rs || (cj & CP_WS)) ? FRESH : kcarry;
@@ -2116,7 +1790,7 @@ tokenize_kernel(KernArgs ka) {
 #ifndef PUSH32
 #define PUSH32 0   // A/B knob: 1 = the span mask walked as two 32-bit halves (one v_ffbl and 32-bit arithmetic per edge)
 #endif
-                    if (PUSH32 && PUSH_B == 1) {
+                    if (PUSH32) {
 #pragma unroll
                         for (int hh = 0; hh < 2; hh++) {
                             uint32_t m32 = hh == 0 ? ((uint32_t)sm & ~1u) : (uint32_t)(sm >> 32);
@@ -2130,55 +1804,11 @@ tokenize_kernel(KernArgs ka) {
                         }
                         continue;
                     }
-                    uint64_t m = sm & ~1ull;
-                    while (m) {
-                        unsigned dd[PUSH_B];
-                        bool hv[PUSH_B];
-#pragma unroll
-                        for (int q = 0; q < PUSH_B; q++) {
-                            hv[q] = m != 0;
-                            dd[q] = hv[q] ? (unsigned)__builtin_ctzll(m) : 0u;
-                            m &= m - 1ull;   // (m = 0 stays 0)
-                        }
-                        uint2 f[PUSH_B];
-#pragma unroll
-                        for (int q = 0; q < PUSH_B; q++) f[q] = fin2[j + 1u + dd[q]];   // <= re: no token crosses a cut
-#pragma unroll
-                        for (int q = 0; q < PUSH_B; q++) upd(f[q], dd[q]);
-#pragma unroll
-                        for (int q = 0; q < PUSH_B; q++)
-                            if (hv[q]) fin2[j + 1u + dd[q]] = f[q];
-                    }
-                }
-                // ---- the long chunks, one after another, each over all lanes: lane d holds candidate
-                //      j = i-1-d with its state in row form ((cost+1) << 16 | G) and its span mask;
-                //      the chunk's first boundary is a fresh start (a cut), ends of words restart
-                for (uint64_t lm = ballot(rowc); lm; lm &= lm - 1ull) {
-                    const unsigned q = (unsigned)__builtin_ctzll(lm);
-                    const unsigned ra = __builtin_amdgcn_readlane(rs, q), rb = __builtin_amdgcn_readlane(re, q);
-                    constexpr unsigned ST0 = 0x10000u;
-                    const uint64_t m0 = L.rec[ra].smask;
-                    unsigned mlo = lane == 0 ? (unsigned)m0 : 0u, mhi = lane == 0 ? (unsigned)(m0 >> 32) : 0u;
-                    unsigned st = lane == 0 ? ST0 : 0u;
-                    unsigned cpj = lane == 0 ? (L.rec[ra].cpos & 0x7FFFu) : 0u;
-                    for (unsigned i = ra + 1u; i <= rb; i++) {
-                        const unsigned cur = L.rec[i].cpos;
-                        const uint64_t mi = L.rec[i].smask;
-                        const unsigned cpi = cur & 0x7FFFu;
-                        const unsigned span = cpi - cpj;
-                        const unsigned gj = st & 0x7FFFu;
-                        const unsigned kv = (st | 0x7FFFu) - (gj > span ? gj : span);
-                        const unsigned bit = (lane < 32u ? (mlo >> lane) : (mhi >> (lane - 32u))) & 1u;
-                        const unsigned key = bit ? kv : 0xFFFFFFFFu;
-                        const unsigned r = wave_min_u32(key);
-                        const uint64_t gmb = ballot(key == r);
-                        const uint64_t emb = ballot((key ^ r) < 0x8000u);
-                        if (lane == 0) fin2[i] = make_uint2((unsigned)__builtin_ctzll(gmb) | ((unsigned)__builtin_ctzll(emb) << 8), r);
-                        const bool wend = (cur & CP_WS) != 0;
-                        st = wave_shift_in(st, wend ? ST0 : (r ^ 0x7FFFu) + 0x10000u);
-                        cpj = wave_shift_in(cpj, cpi);
-                        mlo = wave_shift_in(mlo, (unsigned)mi);
-                        mhi = wave_shift_in(mhi, (unsigned)(mi >> 32));
+                    for (uint64_t m = sm & ~1ull; m; m &= m - 1ull) {
+                        const unsigned dd = (unsigned)__builtin_ctzll(m);
+                        uint2 f = fin2[j + 1u + dd];   // <= re: no token crosses a cut
+                        upd(f, dd);
+                        fin2[j + 1u + dd] = f;
                     }
                 }
                 if (DPT_STOP == 26) return;   // diagnostic: + the recurrence
@@ -2227,25 +1857,17 @@ tokenize_kernel(KernArgs ka) {
                     if constexpr (G == 16) {
                         forward_lanes();
                         lane_mode = true;
-#ifdef DPT_LANEDBG
-                        if (lane == 0) atomicAdd(&g_lanedbg[16 * 16 + 1], 1u);
-#endif
-                    } else if constexpr (!BIG && LANES64) {
+                    } else if constexpr (!BIG) {
                         forward_lanes64();
                         lane_mode = DPT_STOP >= 25 && DPT_STOP <= 27;   // stop builds: no C0/C1 over unfinished fin[]
                     } else {
                         forward(F_{}, C2_{});
                     }
                 } else if (uncapped) forward(F_{}, C1_{}); else forward(F_{}, C0_{});
-#ifdef DPT_LANEDBG
-                if (capb && lane == 0) atomicAdd(&g_lanedbg[16 * 16], 1u);
-#endif
             }
         }
         wave_sync();
-        if constexpr (PF_NEXT == 1 && G == 16 && !BIG) asm volatile("s_waitcnt vmcnt(0)" : : "v"(pfv));
         STAMP(2);
-        PRIO_PHASE(2);
 
         // ---------------------------------------------------------- C0: per-window token counts and validity
         KREFRESH();
@@ -2310,10 +1932,6 @@ tokenize_kernel(KernArgs ka) {
 
         // ---------------------------------------------------------- C1: selection, one lane per word
         KREFRESH();
-#if DPT_DOUBLE == 3
-        for (int rep_ = 0; rep_ < 2; rep_++) {
-            if (rep_) wave_sync();
-#endif
         if (DPT_RUN_B && !lane_mode) {
             unsigned pre[NG + 1], tokpre[NG + 1], inv_g[NG];
             pre[0] = 0; tokpre[0] = 0;
@@ -2365,20 +1983,11 @@ tokenize_kernel(KernArgs ka) {
                 }
             }
         }
-#if DPT_DOUBLE == 3
-        }
-#endif
         wave_sync();
-        if constexpr (PF_NEXT == 2 && G == 16 && !BIG) asm volatile("s_waitcnt vmcnt(0)" : : "v"(pfv));
         STAMP(3);
-        PRIO_PHASE(3);
 
         // ---------------------------------------------------------- C2: ids (lanes over all slots' tokens)
         KREFRESH();
-#if DPT_DOUBLE == 4
-        for (int rep_ = 0; rep_ < 2; rep_++) {
-            if (rep_) wave_sync();
-#endif
         if (DPT_RUN_C2) {
             unsigned pre[NG + 1], na_g[NG];
             uint64_t obase[NG];       // staging element of the window's first token, per slot
@@ -2422,13 +2031,7 @@ tokenize_kernel(KernArgs ka) {
             // the stored bytes once a round would overflow it (walk_pending); a longer one is walked
             // below by the refill walker.
             constexpr bool BULK = G == 16 && !BIG;
-#ifndef C2_PAIR16
-#define C2_PAIR16 1   // A/B knob: 0 = the bulk pass reads the root children / root table (slots4)
-#endif
-#ifndef PEND_CAP
-#define PEND_CAP 64   // residual tokens a wave's pending row holds (A/B knob; the scratch row has 64 entries)
-#endif
-            static_assert(PEND_CAP >= 1 && PEND_CAP <= 64, "pending row");
+            constexpr unsigned PEND_CAP = 64;   // residual tokens a wave's pending row holds (its scratch row)
             unsigned wbeg = 0, wend = total;
             // the list of tokens left for the walkers: in the rec[].cpos halves (dead in C2) -- G = 16:
             // entry i in group i / 256's rec[i % 256]; G = 64 (one slot): rec[i]
@@ -2438,9 +2041,6 @@ tokenize_kernel(KernArgs ka) {
                 else
                     return grp(0).rec[i].cpos;
             };
-#ifndef C2_HASH
-#define C2_HASH 1   // A/B knob: 0 = every token the bulk pass leaves goes to the walkers
-#endif
             // hash pass over n tokens (token number of entry i: src(i)): a token of at most
             // TOKHASH_MAX_BYTES expanded bytes without a newline atom gets its id from ONE bucket load
             // of the token hash table (dpt_internal.h); the others are listed, in order, at the front of
@@ -2448,25 +2048,20 @@ tokenize_kernel(KernArgs ka) {
             auto hash_pass = [&](unsigned n, auto src) -> unsigned {
                 const uint8_t *hbase = reinterpret_cast<const uint8_t *>(tv.pair16) + TOKHASH_OFFSET;
                 const TokHashHeader hh = *reinterpret_cast<const TokHashHeader *>(hbase);
-                if (!C2_HASH || !hh.max_probe) {
+                if (!hh.max_probe) {
                     for (unsigned i = lane; i < n; i += 64u) list_ref(i) = (uint16_t)src(i);
                     return n;
                 }
                 const __amdgpu_buffer_rsrc_t hr = __builtin_amdgcn_make_buffer_rsrc(
                     (void *)(hbase + sizeof(TokHashHeader)), (short)0, (int)((hh.mask + 1u) * 16u), 0x00020000);
-#ifndef C2_NL
-#define C2_NL 0   // A/B knob: 1 = one-atom newline tokens take the header's id without a lookup (neutral on
-                  // cfg4, -0.5 % on cfg5: profiles/r03_ab.log r03aa)
-#endif
-#ifndef HP_U
-#define HP_U 2   // A/B knob: token rounds of 64 per hash-pass iteration (their loads before any store: a load
-                 // waits for every older store of the wave)
-#endif
+                // token rounds of 64 per iteration, their loads before any store (a load waits for every
+                // older store of the wave; 1 or 4 rounds measured slower, r03)
+                constexpr int HP_U = 2;
                 unsigned r2 = 0;
                 for (unsigned i0 = 0; i0 < n; i0 += 64u * HP_U) {
                     unsigned tt[HP_U], hh2[HP_U], fpv[HP_U];
                     uint64_t oqv[HP_U];
-                    bool hs[HP_U], inr[HP_U], nlv[HP_U];
+                    bool hs[HP_U], inr[HP_U];
 #pragma unroll
                     for (int u = 0; u < HP_U; u++) {
                         const unsigned i = i0 + 64u * (unsigned)u + lane;
@@ -2484,8 +2079,6 @@ tokenize_kernel(KernArgs ka) {
                         const unsigned p0 = L.aoff[jj];
                         const unsigned nbytes = (typename GL::Idx)(L.aoff[j1] - p0);
                         const unsigned fa = (raw ? 1u : 0u) & q.fw & (unsigned)(jj == 0);
-                        // a non-first '\n' atom alone is the token "<0x0A>": its id from the header
-                        const bool nl1 = C2_NL && raw && in && nbytes == 1 && !fa && hh.nl_id1 && L.bytes[p0] == '\n';
                         uint32_t h = 0, fp = 0;
                         bool hashed;
                         if constexpr (G == 16) {
@@ -2496,8 +2089,7 @@ tokenize_kernel(KernArgs ka) {
                         } else {   // 64-lane rows (BLOOM-scale vocabularies): keys of up to 64 bytes
                             hashed = in && token_hash_long<CH>(L.bytes, p0, nbytes, raw, fa, hh.seed, h, fp);
                         }
-                        tt[u] = t; hh2[u] = h & hh.mask; fpv[u] = fp; oqv[u] = q.ob + k; hs[u] = hashed || nl1; inr[u] = in;
-                        nlv[u] = nl1;
+                        tt[u] = t; hh2[u] = h & hh.mask; fpv[u] = fp; oqv[u] = q.ob + k; hs[u] = hashed; inr[u] = in;
                     }
                     // every round's first probe, then the rare further probes, then the stores
                     int32_t idv[HP_U];
@@ -2505,7 +2097,6 @@ tokenize_kernel(KernArgs ka) {
                     for (int u = 0; u < HP_U; u++) {
                         const auto e = __builtin_amdgcn_raw_buffer_load_b128(hr, hh2[u] * 16u, 0, 0);
                         idv[u] = e[0] == fpv[u] ? (int32_t)e[1] : (e[2] == fpv[u] ? (int32_t)e[3] : INT32_MIN);
-                        idv[u] = nlv[u] ? (int32_t)(hh.nl_id1 - 1u) : idv[u];
                     }
 #pragma unroll
                     for (int u = 0; u < HP_U; u++) {
@@ -2524,7 +2115,6 @@ tokenize_kernel(KernArgs ka) {
 #pragma unroll
                     for (int u = 0; u < HP_U; u++) {
                         if (hs[u]) {
-                            if (DPT_NOSTORE & 2) continue;   // diagnostic
                             if (n16) a.staging16[oqv[u]] = (int16_t)idv[u];
                             else a.staging[oqv[u]] = idv[u];
                         }
@@ -2543,17 +2133,12 @@ tokenize_kernel(KernArgs ka) {
             if constexpr (BULK) {
                 const bool i16 = n16;
                 unsigned r = 0;
-#ifndef C2_DEFER
-#define C2_DEFER 0   // A/B knob: the bulk pass's int16 stores after all its lookups (see below): the held ids
-                     // spill -- cfg2 -4.1 %, cfg4 +1.9 % (profiles/r03_ab.log)
-#endif
                 // The bulk pass over every selected token, 4 per lane per round of 256.  int16 ids from the
                 // pair table: all the window-set's lookups first, then all its stores -- a load waits for
                 // every OLDER vector-memory op of the wave, stores included (MI355X_MICROARCH.md: vmcnt
                 // counts loads and stores together, in issue order), so a store between two rounds of
-                // lookups put a store's full latency on every round.
-                uint32_t kmask = 0;   // bit 4 * round + u: token 256 * round + 64 * u + lane is a bulk token
-                uint32_t pvs[8];      // its id: 16-bit half (u & 1) of pvs[2 * round + u / 2]
+                // lookups put a store's full latency on every round.  (Every round's lookups before any
+                // store held the ids in registers and spilled: cfg2 -4.1 %, r03.)
                 auto bulk_round = [&](unsigned t0, int32_t (&ix)[4], unsigned (&kind)[4], uint64_t (&oq)[4]) {
 #pragma unroll
                     for (int u = 0; u < 4; u++) {
@@ -2578,7 +2163,7 @@ tokenize_kernel(KernArgs ka) {
                                               ((unsigned)(b0 == ' ') | (unsigned)(b0 == '\n') | (q.fw & (unsigned)(jj == 0)) |
                                                ((unsigned)(nbytes == 2u) & ((unsigned)(b1 == ' ') | (unsigned)(b1 == '\n'))));
                         const unsigned bulk = (unsigned)in & (unsigned)(nbytes - 1u <= 1u) & (expd ^ 1u);
-                        if constexpr (SW == 1 && C2_PAIR16)   // int16 ids: the 128-KB pair table (L1-resident for ASCII)
+                        if constexpr (SW == 1)   // int16 ids: the 128-KB pair table (L1-resident for ASCII)
                             ix[u] = bulk ? (int32_t)(nbytes == 1u ? 65536u + b0 : (b0 << 8) + b1) : 0;
                         else
                             ix[u] = bulk ? (nbytes == 1u ? tv.root_base + (int32_t)b0 : (int32_t)(tv.n_slots + (b0 << 8) + b1)) : 0;
@@ -2590,49 +2175,18 @@ tokenize_kernel(KernArgs ka) {
                         r += (unsigned)__builtin_popcountll(m);
                     }
                 };
-                if constexpr (SW == 1 && C2_PAIR16 && C2_DEFER) {
-                    static_assert(NG * CH <= 1024, "four rounds of 256 tokens cover a window set");
-#pragma unroll
-                    for (int rd = 0; rd < 4; rd++) {
-                        if (256u * (unsigned)rd < total) {
-                            int32_t ix[4];
-                            unsigned kind[4];
-                            uint64_t oq[4];
-                            bulk_round(256u * (unsigned)rd, ix, kind, oq);
-                            int16_t pv[4];
-#pragma unroll
-                            for (int u = 0; u < 4; u++) {
-                                pv[u] = tv.pair16[ix[u]];
-                                kmask |= (kind[u] ? 1u : 0u) << (4 * rd + u);
-                            }
-                            pvs[2 * rd] = (uint32_t)(uint16_t)pv[0] | ((uint32_t)(uint16_t)pv[1] << 16);
-                            pvs[2 * rd + 1] = (uint32_t)(uint16_t)pv[2] | ((uint32_t)(uint16_t)pv[3] << 16);
-                        }
-                    }
-                    // the stores: token t of slot g goes to staging element obase[g] + (t - pre[g])
-#pragma unroll
-                    for (int q2 = 0; q2 < 16; q2++) {
-                        if ((kmask >> q2) & 1u) {
-                            const unsigned t = 256u * (unsigned)(q2 >> 2) + 64u * (unsigned)(q2 & 3) + lane;
-                            uint64_t ob = obase[0] - pre[0];
-#pragma unroll
-                            for (int k = 1; k < NG; k++) ob = t >= pre[k] ? obase[k] - pre[k] : ob;
-                            a.staging16[ob + t] = (int16_t)(pvs[q2 >> 1] >> (16 * (q2 & 1)));
-                        }
-                    }
-                }
-                for (unsigned t0 = 0; t0 < total && !(SW == 1 && C2_PAIR16 && C2_DEFER); t0 += 64u * 4u) {
+                for (unsigned t0 = 0; t0 < total; t0 += 64u * 4u) {
                     int32_t ix[4];
                     unsigned kind[4];   // 0: not here, 1 / 2: a token of that many bytes
                     uint64_t oq[4];
                     bulk_round(t0, ix, kind, oq);
-                    if constexpr (SW == 1 && C2_PAIR16) {
+                    if constexpr (SW == 1) {
                         int16_t pv[4];
 #pragma unroll
                         for (int u = 0; u < 4; u++) pv[u] = tv.pair16[ix[u]];
 #pragma unroll
                         for (int u = 0; u < 4; u++)
-                            if (kind[u] && !(DPT_NOSTORE & 1)) a.staging16[oq[u]] = pv[u];
+                            if (kind[u]) a.staging16[oq[u]] = pv[u];
                         continue;
                     }
                     int4 ent[4];
@@ -2651,7 +2205,6 @@ tokenize_kernel(KernArgs ka) {
                 }
                 wave_sync();
                 STAMP(5);
-                if (KREF_MORE) KREFRESH();
                 if (DPT_C2STOP == 1) r = 0;   // diagnostic: the bulk pass only
                 if (r > 0) {
                     r = hash_pass(r, [&](unsigned i) -> unsigned { return list_ref(i); });
@@ -2699,7 +2252,6 @@ tokenize_kernel(KernArgs ka) {
                     wave_sync();
                 }
             }
-            if (KREF_MORE) KREFRESH();
             auto tok_at = [&](unsigned i) -> unsigned { return list_ref(i); };
             // One token walk per lane; a lane whose token is resolved writes the id and takes the
             // next token (ballot + mbcnt), so each iteration is one trie step for 64 tokens.  A
@@ -2727,12 +2279,9 @@ tokenize_kernel(KernArgs ka) {
                 T.out = q.ob + k;
                 return T;
             };
-#ifndef C2_WALKS
-#define C2_WALKS 1
-#endif
-            // C2_WALKS token walks per lane (tokens lane, lane + 64, ... first), so that many trie
-            // loads are in flight per lane in every iteration
-            constexpr int NW = C2_WALKS;
+            // NW token walks per lane (tokens lane, lane + 64, ... first), so that many trie loads are
+            // in flight per lane in every iteration
+            constexpr int NW = 1;
             bool active[NW];
             Tok C[NW];
             int32_t node[NW], nb[NW];
@@ -2792,9 +2341,6 @@ tokenize_kernel(KernArgs ka) {
                 }
             }
         }
-#if DPT_DOUBLE == 4
-        }
-#endif
         wave_sync();
         STAMP(7);
 
@@ -2825,7 +2371,6 @@ tokenize_kernel(KernArgs ka) {
         }
         wave_sync();
         STAMP(4);
-        PRIO_PHASE(4);
     }
     if constexpr (G == 16 && !BIG)
         if (n_pend) walk_pending(n_pend);
@@ -2846,18 +2391,11 @@ tokenize_kernel(KernArgs ka) {
 // (dpt_dp_host_far); from byte PART_CTR_OFFSET the first pass's partition counters and their used-up
 // mask (dpt_internal.h).
 constexpr unsigned CTR_ARENA64 = 4, CTR_LASTNEED64 = 5, CTR_FAR64 = 6, CTR_LASTFAR64 = 7;
-#ifndef FIN_THREADS
-#define FIN_THREADS 512   // threads per finish block (>= FIN_BATCH): all of them copy
-#endif
-#ifndef SCAN_THREADS
-#define SCAN_THREADS 1024   // threads of the batch-scan block
-#endif
-#ifndef FIN_TARGET_BLOCKS
-#define FIN_TARGET_BLOCKS 2048   // small batches: each batch's copy is split over slices until the grid has this many blocks
-#endif
-#ifndef FIN_MAX_SLICES
-#define FIN_MAX_SLICES 8
-#endif
+constexpr unsigned FIN_U = 16;                // loads in flight per thread of the copy
+constexpr unsigned FIN_THREADS = 512;         // threads per finish block (>= FIN_BATCH): all of them copy
+constexpr unsigned SCAN_THREADS = 1024;       // threads of the batch-scan block
+constexpr uint64_t FIN_TARGET_BLOCKS = 2048;  // small batches: each batch's copy is split over slices until the grid has this many blocks
+constexpr uint64_t FIN_MAX_SLICES = 8;
 
 // 64-bit inclusive add-scan over the wave (ds_bpermute shifts)
 __device__ __forceinline__ uint64_t wave_incl_scan_add64(uint64_t v, unsigned lane) {
@@ -3034,9 +2572,6 @@ __global__ void __launch_bounds__(FIN_THREADS) finish_kernel(FinishArgs f) {
         }
     }
     const uint64_t k_beg = total * sl / f.slices, k_end = total * (sl + 1) / f.slices;
-#ifndef FIN_U
-#define FIN_U 16
-#endif
     constexpr unsigned U = FIN_U;
     // the string of this thread's first id: the last string whose start is <= it (binary search;
     // then monotone in k)
@@ -3080,9 +2615,7 @@ __global__ void __launch_bounds__(64) reset_kernel(uint32_t *ctr) {
 // Token-count histogram: LDS-privatised int64 bins, one LDS atomic per string for its count bin
 // (peeling distinct bins per wave with ballots measured slower: 36 vs 30 us on cfg2); statuses --
 // nearly all 0, so per-lane atomics would serialise 64-way on one bin -- by one ballot per value.
-#ifndef HIST_THREADS
-#define HIST_THREADS 1024
-#endif
+constexpr unsigned HIST_THREADS = 1024;
 __global__ void __launch_bounds__(HIST_THREADS) hist_kernel(const uint64_t *__restrict__ id_off, const int32_t *__restrict__ status,
                                                    uint64_t n_str, unsigned long long *hist, uint32_t n_bins) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long lh[];
@@ -3236,9 +2769,9 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
             b.hist_zero = reinterpret_cast<unsigned long long *>(p.hist);   // (the finish pass adds to it)
             b.n_hist = p.hist_bins + 8u;
         }
-#ifndef FALLBACK_DIV
-#define FALLBACK_DIV 4   // the fallback passes' grids: 1/FALLBACK_DIV of a full one (usually they find no work)
-#endif
+        // the fallback passes' grids: 1/FALLBACK_DIV of a full one (usually they find no work; 16 / 64
+        // within noise, r03ah)
+        constexpr unsigned FALLBACK_DIV = 4;
         // (n_units caps the grid: one block per FALLBACK_DIV CUs; the retry list is rare and short)
         uint64_t fb_units = (uint64_t)(p.max_blocks / 64) / FALLBACK_DIV;
         fb_units = fb_units < p.n_str ? fb_units : p.n_str;
@@ -3309,9 +2842,7 @@ size_t wsl_scratch_bytes(unsigned max_blocks) {
 hipError_t launch_histogram(const uint64_t *id_off, const int32_t *status, uint64_t n_str, int64_t *hist,
                             uint32_t n_bins, hipStream_t stream) {
     if (n_str == 0) return hipSuccess;
-#ifndef HIST_BLOCKS
-#define HIST_BLOCKS 256
-#endif
+    constexpr uint64_t HIST_BLOCKS = 256;
     uint64_t blocks = (n_str + HIST_THREADS - 1) / HIST_THREADS;
     if (blocks > HIST_BLOCKS) blocks = HIST_BLOCKS;   // each block adds its bins to the global ones once
     hipLaunchKernelGGL(hist_kernel, dim3((unsigned)blocks), dim3(HIST_THREADS), (n_bins + 8) * sizeof(unsigned long long), stream,
@@ -3340,11 +2871,6 @@ hipError_t kernel_init() {
 int small_window_bytes() { return SMALL_CH; }
 int big_window_bytes() { return BIG_CH; }
 
-#ifdef DPT_LANEDBG
-extern "C" int dpt_debug_lanes(unsigned *out) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lanedbg), sizeof(unsigned) * (16 * 16 + 4)) == hipSuccess ? 0 : -1;
-}
-#endif
 #ifdef DPT_STAMPS
 extern "C" int dpt_debug_stamps(unsigned long long *out, int reset) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
