@@ -44,9 +44,16 @@ struct dpt_ctx {
                                       // counter at byte 32, ..., the first pass's partition counters at byte 256
     uint8_t *wsl_scratch = nullptr;   // word lists of the 256-byte pass (dpt::wsl_scratch_bytes)
     uint4 *pend = nullptr;            // pending residual tokens of the 256-byte pass (dpt::pend_scratch_bytes)
-    unsigned long long *flags = nullptr;   // batch sums, then (from cap_flags / 2) batch prefixes: one each per 256 strings
-    uint64_t cap_flags = 0;
-    int flag_parity = 0;   // which half of flags holds the batch sums (all zero between calls); see fin_fold
+    // per 256-string batch, two parity regions R0, R1 of {batch sums, self-copy prefixes + flags, copied
+    // counts} (3 x cap_batches u64 each), then the batch prefixes of the scan path (cap_batches): the
+    // call of parity P uses R_P and -- fold and self-copy calls -- zeroes R_(1-P) for the next one (the
+    // parity flips); between calls R_parity is all zero.  See dpt_internal.h fin_fold and SC_*.
+    unsigned long long *flags = nullptr;
+    uint64_t cap_batches = 0;
+    int flag_parity = 0;
+    uint2 *cq = nullptr;              // self-copy queues (dpt::cq_scratch_bytes)
+    unsigned long long *last_sc = nullptr;   // the last call's region when it self-copied (dpt_ctx_copy_stats) ...
+    uint64_t last_sc_nb = 0;                 // ... and its batches
     unsigned max_blocks = 0;
     // host path: one device buffer in (text | offsets | cut) and one out (id_off | status | capped |
     // counters | ids | edges), each mirrored by a pinned host buffer so every copy is one async DMA
@@ -152,12 +159,18 @@ int ensure_workspace(dpt_ctx *c, const dpt_vocab *v, uint64_t n_bytes, uint64_t 
         cap2 /= 2;
         c->cap_str = cap < cap2 ? cap : cap2;
     }
-    if (2 * ((n_str + dpt::FIN_BATCH - 1) / dpt::FIN_BATCH) > c->cap_flags || !c->flags) {
-        // two arrays of one entry per batch (sums | prefixes at cap_flags / 2), at one per 64 strings
-        const uint64_t want = 2 * ((n_str + 63) / 64 > 1 ? (n_str + 63) / 64 : 1);
-        if ((e = grow(&c->flags, &c->cap_flags, want)) != hipSuccess) return hip_fail(e, "hipMalloc(flags)");
-        // the batch sums start at zero; every call's batch_scan_kernel zeroes them again
-        if ((e = hipMemset(c->flags, 0, c->cap_flags * sizeof(unsigned long long))) != hipSuccess) return hip_fail(e, "hipMemset(flags)");
+    const uint64_t nbat = (n_str + dpt::FIN_BATCH - 1) / dpt::FIN_BATCH;
+    if (nbat > c->cap_batches || !c->flags) {
+        // (+25 % on growth; the regions start at zero and every call leaves the next one's zeroed)
+        uint64_t capb = nbat > 1 ? nbat : 1;
+        if (c->cap_batches) capb += capb / 4;
+        if (c->flags) (void)hipFree(c->flags);
+        c->flags = nullptr;
+        c->cap_batches = 0;
+        c->flag_parity = 0;
+        if ((e = hipMalloc((void **)&c->flags, 7 * capb * sizeof(unsigned long long))) != hipSuccess) return hip_fail(e, "hipMalloc(flags)");
+        if ((e = hipMemset(c->flags, 0, 7 * capb * sizeof(unsigned long long))) != hipSuccess) return hip_fail(e, "hipMemset(flags)");
+        c->cap_batches = capb;
         fresh = true;
     }
     if (!c->wsl_scratch) {
@@ -167,6 +180,10 @@ int ensure_workspace(dpt_ctx *c, const dpt_vocab *v, uint64_t n_bytes, uint64_t 
     if (!c->pend) {
         e = hipMalloc((void **)&c->pend, dpt::pend_scratch_bytes(c->max_blocks));
         if (e != hipSuccess) return hip_fail(e, "hipMalloc(pend)");
+    }
+    if (!c->cq) {
+        e = hipMalloc((void **)&c->cq, dpt::cq_scratch_bytes(c->max_blocks));
+        if (e != hipSuccess) return hip_fail(e, "hipMalloc(cq)");
     }
     if (!c->retry_count) {
         // zeroed once here; every call's finish kernel resets it for the next call
@@ -438,7 +455,7 @@ int dpt_ctx_destroy(dpt_ctx *c) {
     if (!c) return DPT_OK;
     DeviceGuard g(c->device);
     void *ps[] = {c->staging32, c->staging16, c->arena, c->counts, c->retry_list, c->retry_count, c->wsl_scratch,
-                  c->pend, c->flags, c->d_in, c->d_out};
+                  c->pend, c->cq, c->flags, c->d_in, c->d_out};
     for (void *p : ps)
         if (p) (void)hipFree(p);
     if (c->p_in) (void)hipHostFree(c->p_in);
@@ -465,10 +482,30 @@ int dpt_ctx_workspace_bytes(const dpt_ctx *c, uint64_t *device_path, uint64_t *h
     if (!c) return fail(DPT_E_ARG, "null ctx");
     if (device_path)
         *device_path = c->cap16 * 2 + c->cap32 * 4 + c->arena_cap * ARENA_PER_BYTE + c->cap_str * (8 + 2 * 4) +
-                       c->cap_flags * 8 + (c->wsl_scratch ? dpt::wsl_scratch_bytes(c->max_blocks) : 0) +
+                       c->cap_batches * 7 * 8 + (c->wsl_scratch ? dpt::wsl_scratch_bytes(c->max_blocks) : 0) +
                        (c->pend ? dpt::pend_scratch_bytes(c->max_blocks) : 0) +
+                       (c->cq ? dpt::cq_scratch_bytes(c->max_blocks) : 0) +
                        (c->retry_count ? dpt::CTR_ALLOC_BYTES : 0);
     if (host_path) *host_path = c->cap_in + c->cap_out;
+    return DPT_OK;
+}
+
+int dpt_ctx_copy_stats(dpt_ctx *c, uint64_t *copied, uint64_t *batches_ofs, uint64_t *n_batches) {
+    if (!c || !copied || !batches_ofs || !n_batches) return fail(DPT_E_ARG, "null argument");
+    *copied = *batches_ofs = *n_batches = 0;
+    if (!c->last_sc || !c->last_sc_nb) return DPT_OK;
+    DeviceGuard g(c->device);
+    const uint64_t nb = c->last_sc_nb, cb = c->cap_batches;
+    std::vector<unsigned long long> inc(nb);
+    std::vector<uint32_t> cp(nb);
+    hipError_t e = hipMemcpy(inc.data(), c->last_sc + cb, nb * 8, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(cp.data(), c->last_sc + 2 * cb, nb * 4, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return hip_fail(e, "D2H copy stats");
+    for (uint64_t b = 0; b < nb; b++) {
+        *copied += cp[b];
+        *batches_ofs += (inc[b] & dpt::SC_OFS) ? 1 : 0;
+    }
+    *n_batches = nb;
     return DPT_OK;
 }
 
@@ -522,9 +559,21 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
     p.wsl_scratch = c->wsl_scratch;
     p.long_span = v->stats.max_cp > 64 ? 1 : 0;
     p.max_tok_bytes = v->stats.max_bytes;
-    p.flags_half = c->cap_flags / 2;
-    p.flags = c->flags + (c->flag_parity ? p.flags_half : 0);
-    p.bpre = c->flags + (c->flag_parity ? 0 : p.flags_half);
+    {
+        const uint64_t cb = c->cap_batches;
+        unsigned long long *r = c->flags + (c->flag_parity ? 3 * cb : 0);
+        p.flags = r;
+        p.inc = r + cb;
+        p.copied = reinterpret_cast<uint32_t *>(r + 2 * cb);
+        p.zero_other = c->flags + (c->flag_parity ? 0 : 3 * cb);
+        p.zero_n = 3 * cb;
+        p.bpre = c->flags + 6 * cb;
+        p.cq = c->cq;
+        // self-copy: CSR calls of enough batches without edge outputs or length-only DPs
+        const char *sce = getenv("DPT_SELF_COPY");   // (A/B switch: "0" = off; read per call)
+        p.self_copy = !(sce && !strcmp(sce, "0")) && !padded && !edges && !(mode_flags & (DPT_FLAG_UNCAPPED | DPT_FLAG_LEN_ONLY)) &&
+                      (n_str + dpt::FIN_BATCH - 1) / dpt::FIN_BATCH >= dpt::SC_MIN_BATCHES;
+    }
     p.max_blocks = c->max_blocks;
     p.arena = c->arena;
     p.arena_cap = c->arena_cap;
@@ -564,10 +613,13 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
     hipError_t e = dpt::launch_encode(p, st, evp);
     if (e != hipSuccess) {
         (void)hipMemsetAsync(c->retry_count, 0, dpt::CTR_ALLOC_BYTES, st);   // the scan kernel did not reset them
-        (void)hipMemsetAsync(c->flags, 0, c->cap_flags * sizeof(unsigned long long), st);   // nor zero the batch sums
+        (void)hipMemsetAsync(c->flags, 0, 7 * c->cap_batches * sizeof(unsigned long long), st);   // nor zero the batch arrays
+        c->flag_parity = 0;
         return hip_fail(e, "encode launch");
     }
-    if (!padded && dpt::fin_fold(n_str)) c->flag_parity ^= 1;   // the finish pass zeroed the other half
+    if (!padded && (dpt::fin_fold(n_str) || p.self_copy)) c->flag_parity ^= 1;   // the finish pass zeroed the other region
+    c->last_sc = p.self_copy ? p.flags : nullptr;
+    c->last_sc_nb = p.self_copy ? (n_str + dpt::FIN_BATCH - 1) / dpt::FIN_BATCH : 0;
     return DPT_OK;
 }
 

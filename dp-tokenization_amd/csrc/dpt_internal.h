@@ -33,8 +33,13 @@ struct EncodeLaunch {
     uint32_t max_tok_bytes;  // longest vocabulary token, bytes
     unsigned long long *flags;   // per FIN_BATCH-string batch: the sum of its counts, added by the tokenize passes as
                                  //   strings finish; batch_scan_kernel zeroes it for the next call
-    unsigned long long *bpre;    // per batch: its exclusive id prefix (batch_scan_kernel); the other of the two arrays
-    uint64_t flags_half;         // entries of each array (flags, bpre)
+    unsigned long long *bpre;    // per batch: its exclusive id prefix (batch_scan_kernel)
+    unsigned long long *inc;     // per batch (self-copy): SC_* flags + inclusive id prefix
+    uint32_t *copied;            // per batch (self-copy): strings the first pass copied into place
+    unsigned long long *zero_other;   // fold / self-copy calls: the other parity's region, zeroed for the next call ...
+    uint64_t zero_n;             // ... (u64 entries)
+    bool self_copy;              // the first pass copies its strings' ids into the CSR arrays (dpt_kernels.hip)
+    uint2 *cq;                   // self-copy: per wave, CQ_CAP queued {string, count}
     unsigned max_blocks;
     int variant;             // KERNEL_* below
     bool padded;             // dpt_encode_padded: staging = the caller's ids, counts = the caller's; no finish pass
@@ -78,6 +83,18 @@ __host__ __device__ inline bool fin_fold(uint64_t n_str) {
     return nb > 1 && nb <= FIN_FOLD_MAX;
 }
 constexpr unsigned FIN_MAX_BINS = 1024;   // histogram bins the finish pass folds in (more: the separate pass)
+
+// Batch sums (EncodeLaunch::flags): the count sum in bits 0..39 (a batch holds < 2^40 ids: 256 strings of
+// < 4 GiB); in self-copy calls the first pass also counts, per batch, its strings finished there
+// (bits 40..48) and those routed to a later pass (bits 49..57) -- one atomic add per string.
+constexpr unsigned BS_FIN_SHIFT = 40, BS_ROUTE_SHIFT = 49;
+constexpr unsigned long long BS_SUM_MASK = (1ull << BS_FIN_SHIFT) - 1;
+// Self-copy (dpt_kernels.hip): per batch, the inclusive id prefix (bits 0..55) once known (SC_PUB), the
+// right to write the batch's id_off entries (SC_CLAIM) and their being written (SC_OFS).
+constexpr unsigned long long SC_PUB = 1ull << 63, SC_CLAIM = 1ull << 62, SC_OFS = 1ull << 61;
+constexpr unsigned long long SC_VAL_MASK = (1ull << 56) - 1;
+constexpr unsigned CQ_CAP = 32;            // strings a wave's copy queue holds
+constexpr uint64_t SC_MIN_BATCHES = 8;     // calls of fewer batches take the finish pass's copy alone
 constexpr size_t PART_CTR_OFFSET = 256;
 constexpr size_t CTR_ALLOC_BYTES = PART_CTR_OFFSET + (NPART_MAX + 1) * PART_STRIDE * 4;
 
@@ -182,6 +199,7 @@ void launch_long(const LongLaunch &p, hipStream_t stream, hipEvent_t ev_stop = n
 hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t ev[2]);
 size_t wsl_scratch_bytes(unsigned max_blocks);
 size_t pend_scratch_bytes(unsigned max_blocks);
+size_t cq_scratch_bytes(unsigned max_blocks);
 hipError_t launch_histogram(const uint64_t *id_off, const int32_t *status, uint64_t n_str, int64_t *hist,
                             uint32_t n_bins, hipStream_t stream);
 hipError_t kernel_init();

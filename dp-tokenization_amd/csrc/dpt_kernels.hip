@@ -114,6 +114,18 @@ __device__ __forceinline__ unsigned wave_shift_in(unsigned x, unsigned in) {
     return (unsigned)__builtin_amdgcn_update_dpp((int)in, (int)x, 0x138, 0xF, 0xF, false);
 }
 
+// 64-bit inclusive add-scan over the wave (ds_bpermute shifts)
+__device__ __forceinline__ uint64_t wave_incl_scan_add64(uint64_t v, unsigned lane) {
+#pragma unroll
+    for (unsigned k = 1; k < 64; k <<= 1) {
+        const int src = (int)((lane >= k ? lane - k : lane) << 2);
+        const unsigned lo = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)(unsigned)v);
+        const unsigned hi = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)(unsigned)(v >> 32));
+        v += lane >= k ? (((uint64_t)hi << 32) | lo) : 0ull;
+    }
+    return v;
+}
+
 __device__ __forceinline__ unsigned uni(unsigned x) { return __builtin_amdgcn_readfirstlane(x); }
 __device__ __forceinline__ uint64_t uni64(uint64_t x) {
     return ((uint64_t)uni((unsigned)(x >> 32)) << 32) | uni((unsigned)x);
@@ -255,6 +267,7 @@ struct SlotState {
     uint32_t abase;
     uint16_t wlen, n_atoms, n_words;
     uint8_t active, status, inval, capb;   // capb: some atom of the window is not a token by itself (the cap can bind)
+    uint8_t qh, qt;                        // SS[0] only: the wave's copy-queue head and tail (self-copy; mod 256)
 };
 static_assert(sizeof(SlotState) == 48, "slot state layout");
 
@@ -331,6 +344,13 @@ struct EncodeArgs {
     int mode;                   // DPT_MODE_* | DPT_FLAG_*
     unsigned long long *hist_zero;   // 2048-byte pass, fin_fold calls with DPT_HIST_OVERWRITE: the histogram to
     uint32_t n_hist;                 //   zero before the finish pass adds to it (the scan kernel's duty otherwise)
+    // self-copy (first pass of CSR calls; inc == nullptr: off): see sc_step in tokenize_kernel
+    unsigned long long *inc;    // per batch: SC_PUB | SC_CLAIM | SC_OFS | inclusive id prefix
+    uint32_t *copied;           // per batch: strings copied into place
+    uint2 *cq;                  // per wave: CQ_CAP queued {string, count} (ring; head / tail in SS[0].qh / qt)
+    uint32_t *route_c;          // ~(first batch holding a string routed to a later pass), 0: none (atomicMax)
+    uint64_t *id_off;
+    int32_t *ids;
 };
 
 #ifdef DPT_STAMPS
@@ -701,11 +721,30 @@ __device__ bool prep_window(GroupLDS<CH, G> &L, uint8_t *gw, const WinRegs<CH> &
 
 constexpr unsigned NPART = 16;   // first-pass work partitions (<= NPART_MAX)
 static_assert(NPART >= 1 && NPART <= NPART_MAX, "NPART");
+// First-pass partition p of npart over n strings: the FIN_BATCH-string chunks c with c % npart == p,
+// in order.  part_size: its strings; part_string: the string at partition-local index v (< part_size).
+// (32-bit arithmetic: a call has fewer than 2^31 strings)
+__device__ __forceinline__ unsigned part_size(unsigned n, unsigned npart, unsigned p) {
+    const unsigned nch = (n + FIN_BATCH - 1) / FIN_BATCH;
+    if (nch <= p) return 0;
+    // (uniform: readfirstlane keeps the VALU-lowered division out of an SGPR copy ROCm 7.2 rejects)
+    const unsigned cnt = __builtin_amdgcn_readfirstlane((nch - 1 - p) / npart) + 1;   // chunks of p
+    const unsigned last = p + (cnt - 1) * npart;               // its last chunk
+    return cnt * FIN_BATCH - (last == nch - 1 ? nch * FIN_BATCH - n : 0);   // (only the batch's last chunk is short)
+}
+__device__ __forceinline__ unsigned part_string(unsigned npart, unsigned p, unsigned v) {
+    return ((v / FIN_BATCH) * npart + p) * FIN_BATCH + v % FIN_BATCH;
+}
 constexpr unsigned A_REFILL = 32;     // phase A: idle lanes needed before a batched refill (1/8/16/32 within 2 %)
 constexpr unsigned A_REFILL64 = 32;   // the same for the 64-lane kernels (8 / 1: neutral / -0.5 %, r03aa)
 #ifndef DPT_STOP     // diagnostic builds only (wrong results): 1 = prep only, 21 = + A0, 2 = + A, 25 / 26 / 27 =
                      // + lane-mode B's cut points / recurrence / transfer scan + fix-up, 3 = + B/C0/C1
 #define DPT_STOP 9
+#endif
+#ifdef DPT_NO_SC     // A/B builds only: the first pass without its self-copy code (the host's DPT_SELF_COPY=0 leaves it in)
+constexpr bool SC_ON = false;
+#else
+constexpr bool SC_ON = true;
 #endif
 #ifndef DPT_C2STOP   // diagnostic builds only (wrong results): C2 stops after its bulk pass (1) / hash pass (2)
 #define DPT_C2STOP 0
@@ -737,6 +776,156 @@ __device__ __forceinline__ TrieView tv_of(ConstKernArgs *kp) {
 }
 // (the 16-lane instantiations: the 64-lane ones do not spill, and measured 1.7 % slower with it)
 #define KREFRESH() do { if constexpr (G == 16) asm volatile("" : "+s"(kp)); } while (0)
+
+// ---- self-copy (first pass of CSR calls, a.inc != nullptr).  The finish pass used to copy every
+// staged id into the CSR arrays after this kernel (0.33 ms, 13 % of a cfg2 step, half its HBM
+// traffic).  Here the wave that finished a string copies its ids itself once the string's offset is
+// known: the string waits in the wave's copy queue (a.cq, CQ_CAP entries) until its FIN_BATCH-string
+// batch is complete and the ids of every earlier batch are counted, which happens about a round
+// later since the partitions advance through the batch side by side.  Cross-wave data goes through
+// agent-scope atomics only (MI355X: per-XCD L2s are not coherent; no release fence is needed):
+//   * a finishing string stores its count (ld_agent / st_agent: sc1) and, after the store drained,
+//     adds 1 << BS_FIN_SHIFT | count to its batch sum (a routed string adds 1 << BS_ROUTE_SHIFT);
+//   * the first wave that finds a batch complete and the id prefix before it computable -- the
+//     nearest published prefix back plus the sums of the complete batches after it (a decoupled
+//     look-back) -- claims it (atomicOr SC_PUB | SC_CLAIM | inclusive prefix), writes the batch's
+//     id_off entries from its strings' counts, drains, and sets SC_OFS;
+//   * a queued string whose batch has SC_OFS is copied from the wave's own staging (its own stores:
+//     only the L1 could be stale, so the loads are sc1) to ids[id_off[s+1] - count ..].
+// Strings whose batch or an earlier one holds a string routed to a later pass, and strings that do
+// not fit the queue, stay for the finish pass (it copies every batch not fully copied here).
+// The id_off[s+1] of a string is the CSR offset (tokenizer_utils.py:76-79: ids concatenated per string).
+// (Cold code, kept out of line: inlined into the tokenize loop it cost 8 SGPR + 8 VGPR spills.)
+__device__ __forceinline__ unsigned long long sc_ld(const unsigned long long *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long sc_readlane64(unsigned long long v, unsigned l) {
+    return ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), l) << 32) |
+           (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, l);
+}
+template <typename A>
+__device__ __forceinline__ unsigned sc_size(const A &a, unsigned b) {
+    const uint64_t rem = a.n_str - (uint64_t)b * FIN_BATCH;
+    return rem < FIN_BATCH ? (unsigned)rem : FIN_BATCH;
+}
+// E = the ids of the batches before b.  1: known; 0: a batch in between has strings still running;
+// -1: one holds a string routed to a later pass (no batch from there on is copied in this pass)
+template <typename A>
+__device__ __forceinline__ int sc_prefix(const A &a, unsigned b, unsigned lane, unsigned long long &E) {
+    unsigned long long acc = 0;
+    for (unsigned top = b; top > 0; top = top > 64u ? top - 64u : 0u) {
+        const int k = (int)top - 1 - (int)lane;
+        unsigned long long pv = SC_PUB, sv = 0;   // k < 0: before the first batch, prefix 0
+        if (k >= 0) {
+            pv = sc_ld(&a.inc[k]);
+            sv = sc_ld(&a.bsum[k]);
+        }
+        const uint64_t pm = ballot((pv & SC_PUB) != 0);
+        const unsigned l0 = pm ? (unsigned)__builtin_ctzll(pm) : 64u;   // the nearest published
+        const bool below = lane < l0;
+        const unsigned rt = (unsigned)(sv >> BS_ROUTE_SHIFT) & 0x1FFu, fin = (unsigned)(sv >> BS_FIN_SHIFT) & 0x1FFu;
+        if (ballot(below && rt != 0)) return -1;
+        if (ballot(below && fin != sc_size(a, (unsigned)max(k, 0)))) return 0;
+        const unsigned long long part_sum = below ? (sv & BS_SUM_MASK) : 0ull;
+        acc += sc_readlane64(wave_incl_scan_add64(part_sum, lane), 63);
+        if (l0 < 64u) {
+            E = acc + (sc_readlane64(pv, l0) & SC_VAL_MASK);
+            return 1;
+        }
+    }
+    E = acc;
+    return 1;
+}
+// batch b's id_off entries: 1 written (SC_OFS), 0 not yet, -1 not in this pass
+template <typename A>
+__device__ __forceinline__ int sc_publish(const A &a, unsigned b, unsigned lane) {
+    if (const unsigned rc = uni(__hip_atomic_load(a.route_c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)); rc && b >= ~rc) return -1;
+    const unsigned long long v = uni64(sc_ld(&a.inc[b]));
+    if (v & SC_OFS) return 1;
+    if (v & SC_CLAIM) return 0;   // another wave is writing them
+    const unsigned long long sv = uni64(sc_ld(&a.bsum[b]));
+    if ((sv >> BS_ROUTE_SHIFT) & 0x1FFu) return -1;
+    const unsigned nsz = sc_size(a, b);
+    if (((sv >> BS_FIN_SHIFT) & 0x1FFu) != nsz) return 0;
+    unsigned long long E = 0;
+    const int r = b ? sc_prefix(a, b, lane, E) : 1;
+    if (r <= 0) return r;
+    unsigned long long old = 0;
+    if (lane == 0) old = atomicOr(&a.inc[b], SC_PUB | SC_CLAIM | (E + (sv & BS_SUM_MASK)));
+    old = sc_readlane64(old, 0);
+    if (old & SC_CLAIM) return (old & SC_OFS) ? 1 : 0;
+    // this wave writes them: string s0 + i ends at E + the counts of strings s0 .. s0 + i
+    const uint64_t s0 = (uint64_t)b * FIN_BATCH;
+    unsigned long long c[4], t = 0;
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const unsigned i = 4u * lane + (unsigned)u;
+        c[u] = i < nsz ? sc_ld(reinterpret_cast<const unsigned long long *>(a.counts) + s0 + i) : 0ull;
+        t += c[u];
+    }
+    unsigned long long run = E + wave_incl_scan_add64(t, lane) - t;
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const unsigned i = 4u * lane + (unsigned)u;
+        run += c[u];
+        if (i < nsz)
+            __hip_atomic_store(reinterpret_cast<unsigned long long *>(a.id_off) + s0 + i + 1, run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the entries are out before SC_OFS says so
+    if (lane == 0) atomicOr(&a.inc[b], SC_OFS);
+    return 1;
+}
+// The copy queue's n entries from qh: publish the head's batch if it can be, then the length of the run
+// of entries from the head whose batches have their id_off written (~0u: drop the queue, a string
+// before them went to a later pass).
+__device__ __noinline__ unsigned sc_ready(ConstKernArgs *kp, unsigned qh, unsigned n, unsigned lane) {
+    const auto &a = kp->ea;
+    uint2 e = make_uint2(0u, 0u);
+    if (lane < n) e = a.cq[(size_t)blockIdx.x * CQ_CAP + ((qh + lane) % CQ_CAP)];
+    const unsigned b = e.x / FIN_BATCH;
+    unsigned long long st = SC_OFS;
+    if (lane < n) st = sc_ld(&a.inc[b]);
+    uint64_t ready = ballot(lane < n && (st & SC_OFS) != 0);
+    if (!(ready & 1ull)) {
+        const unsigned bh = __builtin_amdgcn_readlane(b, 0);
+        const int r = sc_publish(a, bh, lane);
+        if (r < 0) return ~0u;
+        if (r > 0) ready |= ballot(lane < n && b == bh);
+    }
+    const unsigned npop = ~ready ? (unsigned)__builtin_ctzll(~ready) : 64u;   // the ready run from the head
+    return npop < n ? npop : n;
+}
+// copy the queue's npop entries from qh: string s's cnt staged ids (this wave's own stores, read sc1: only
+// this CU's L1 could hold a stale line another wave read) to ids[id_off[s+1] - cnt ..]
+__device__ __noinline__ void sc_copy_run(ConstKernArgs *kp, unsigned qh, unsigned npop, unsigned lane, uint64_t base_off, bool w16) {
+    const auto &a = kp->ea;
+    for (unsigned q = 0; q < npop; q++) {
+        const uint2 e = a.cq[(size_t)blockIdx.x * CQ_CAP + ((qh + q) % CQ_CAP)];
+        const unsigned s = uni(e.x), cnt = uni(e.y);
+        const uint64_t o0 = uni64(sc_ld(reinterpret_cast<const unsigned long long *>(a.id_off) + s + 1)) - cnt;
+        const uint64_t src = a.str_off[s] - base_off;
+        const uint8_t *sb = w16 ? reinterpret_cast<const uint8_t *>(a.staging16 + src) : reinterpret_cast<const uint8_t *>(a.staging + src);
+        const unsigned al = (unsigned)((uintptr_t)sb & 3u);   // (a dword-aligned resource base)
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)(sb - al), (short)0, (int)(al + cnt * (w16 ? 2u : 4u)), 0x00020000);
+        int32_t *dst = a.ids + o0;
+        for (unsigned k0 = 0; k0 < cnt; k0 += 256u) {
+            int32_t v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const unsigned k = k0 + 64u * (unsigned)u + lane;
+                // aux 16: sc1 (past cnt the range check reads 0)
+                v[u] = w16 ? (int32_t)(int16_t)__builtin_amdgcn_raw_buffer_load_b16(r, al + 2u * k, 0, 16)
+                           : (int32_t)__builtin_amdgcn_raw_buffer_load_b32(r, al + 4u * k, 0, 16);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const unsigned k = k0 + 64u * (unsigned)u + lane;
+                if (k < cnt) dst[k] = v[u];
+            }
+        }
+        if (lane == 0) atomicAdd(&a.copied[s / FIN_BATCH], 1u);
+    }
+}
 
 // SW: staged id width 0 = by a.staging16, 1 = int16, 2 = int32; RAW: DPT_MODE_RAW as a compile-time
 // constant (its expansions and word starts fold away in the other modes' code and vice versa -- the
@@ -773,27 +962,32 @@ tokenize_kernel(KernArgs ka) {
     const bool raw = mode == 0;
     const bool uncapped = (a.mode & DPT_FLAG_UNCAPPED) != 0;   // f2: inspect_tokenizer's inf-initialised DP
     const bool len_only = (a.mode & (DPT_FLAG_UNCAPPED | DPT_FLAG_LEN_ONLY)) != 0;
-    // Strings are handed out by npart device counters, one per contiguous partition of the batch
-    // (strings [p n/npart, (p+1) n/npart) -- each counter in its own 256-byte line): a wave claims as
-    // many strings as it has free slots from its current partition (starting on blockIdx mod npart)
-    // and, when a claim reaches the partition's end, marks the partition in a shared mask and moves
-    // to the next unmarked one.  Round 1's single counter (one same-address atomic per refill) bound
-    // the whole kernel: a prep-only build ran 2.91 of the full build's 2.99 ms, every wave queued
-    // behind ~5.6k others' atomics (profiles/r02_phase_diag.txt).  No string is claimed ahead of a
-    // free slot: strings held in reserve by one wave left others idle at the end of multi-window
-    // batches (cfg4 4.35 -> 4.56 ms with 4-string claims).
+    // Strings are handed out by npart device counters (each in its own 256-byte line).  Partition p
+    // holds the FIN_BATCH-string chunks p, p + npart, p + 2 npart, ... of the batch, in that order
+    // (part_size / part_string): the partitions advance through the batch side by side, so strings
+    // finish roughly in batch order and the CSR offsets of a finished string become known about a
+    // round later (the first pass copies its own strings' ids into place: self_copy below).  A
+    // wave claims as many strings as it has free slots from its current partition (starting on
+    // blockIdx mod npart) and, when a claim reaches the partition's end, marks the partition in a
+    // shared mask and moves to the next unmarked one.  Round 1's single counter (one same-address
+    // atomic per refill) bound the whole kernel: a prep-only build ran 2.91 of the full build's 2.99
+    // ms, every wave queued behind ~5.6k others' atomics (profiles/r02_phase_diag.txt).  No string is
+    // claimed ahead of a free slot: strings held in reserve by one wave left others idle at the end
+    // of multi-window batches (cfg4 4.35 -> 4.56 ms with 4-string claims).
     const unsigned npart = BIG ? 1u : (unsigned)min((uint64_t)NPART, max((uint64_t)1, n_work / 4096u));
     unsigned part = BIG ? 0u : blockIdx.x % npart;
     bool exhausted = false, claimed_all = false;
     unsigned n_pend = 0;   // 16-lane first pass: residual tokens waiting in the wave's pending row
-    // one claim of up to req strings (uniform): [nb, ne), possibly empty once every partition is used up
-    auto claim = [&](unsigned req, uint64_t &nb, uint64_t &ne) {
+    // one claim of up to req strings (uniform): partition-local [nb, ne) of partition cp, possibly
+    // empty once every partition is used up
+    auto claim = [&](unsigned req, uint64_t &nb, uint64_t &ne, unsigned &cp) {
         for (;;) {
             uint32_t *ctr = BIG ? a.work_next : a.part_ctr + part * PART_STRIDE;
-            const uint64_t lo = BIG ? 0u : n_work * part / npart, hi = BIG ? n_work : n_work * (part + 1) / npart;
+            const uint64_t hi = BIG ? n_work : part_size((unsigned)n_work, npart, part);
             unsigned b = 0;
             if (lane == 0) b = atomicAdd(ctr, req);
-            nb = lo + __builtin_amdgcn_readlane(b, 0);
+            cp = __builtin_amdgcn_readfirstlane(part);
+            nb = __builtin_amdgcn_readlane(b, 0);
             ne = nb < hi ? (nb + req < hi ? nb + req : hi) : nb;
             if (nb + req >= hi) {   // the partition is used up (by this claim or earlier ones)
                 if (BIG) {
@@ -861,9 +1055,33 @@ tokenize_kernel(KernArgs ka) {
             else a.staging[out] = id;
         }
     };
+
+    // ---- self-copy: see sc_ready / sc_copy_run above
+    auto sc_step = [&]() -> unsigned {   // strings copied (uniform)
+        const unsigned qh = uni(SS[0].qh), qt = uni(SS[0].qt);
+        const unsigned n = (qt - qh) & 0xFFu;
+        if (!n) return 0;
+        const unsigned npop = sc_ready(kp, qh, n, lane);
+        if (npop == ~0u) {   // a string before them went to a later pass: the finish pass copies the queue's strings
+            if (lane == 0) SS[0].qh = (uint8_t)qt;
+            return 0;
+        }
+        if (!npop) return 0;
+        if constexpr (G == 16 && !BIG)
+            if (n_pend) {   // the strings' residual ids are still in the pending row
+                walk_pending(n_pend);
+                n_pend = 0;
+            }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's staging stores are out
+        sc_copy_run(kp, qh, npop, lane, base_off, SW == 1 || (SW == 0 && a.staging16 != nullptr));
+        if (lane == 0) SS[0].qh = (uint8_t)(qh + npop);
+        return npop;
+    };
+    auto st_agent = [](unsigned long long *p, unsigned long long v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
     STAMP_DECL
 
     if (lane < (unsigned)NG) SS[lane].active = 0;
+    if (lane == 0) { SS[0].qh = 0; SS[0].qt = 0; }
     wave_sync();
 
     for (;;) {
@@ -884,13 +1102,14 @@ tokenize_kernel(KernArgs ka) {
                 while (rem && !claimed_all) {
                     const unsigned n_need = (unsigned)__builtin_popcount(rem);
                     uint64_t nb = 0, ne = 0;
-                    claim(n_need, nb, ne);
+                    unsigned cp = 0;
+                    claim(n_need, nb, ne, cp);
                     const unsigned got = (unsigned)(ne - nb);
                     if (lane < (unsigned)NG && ((rem >> lane) & 1u)) {
                         const unsigned k = (unsigned)__builtin_popcount(rem & ((1u << lane) - 1u));
                         if (k < got) {
                             const uint64_t idx = nb + k;
-                            const uint64_t s = BIG ? (uint64_t)a.work_list[idx] : idx;
+                            const uint64_t s = BIG ? (uint64_t)a.work_list[idx] : part_string(npart, cp, (unsigned)idx);
                             const uint64_t o0 = a.str_off[s], o1 = a.str_off[s + 1];
                             SlotState &S = SS[lane];
                             S.s = (uint32_t)s; S.sb = o0 - base_off; S.slen = (uint32_t)(o1 - o0); S.pos = 0; S.active = 1;
@@ -943,9 +1162,22 @@ tokenize_kernel(KernArgs ka) {
                         lst[atomicAdd(cnt, 1u)] = (uint32_t)s;
                     }
                     a.status[s] = (int32_t)status;
-                    a.counts[s] = 0;
                     if (a.capped) a.capped[s] = status == 2 ? 0 : -1;
                     S.active = 0;
+                    if (!BIG && SC_ON && a.inc) {   // self-copy: finished with no ids (empty), or routed to a later pass
+                        const unsigned b = (unsigned)(s / FIN_BATCH);
+                        if (status == 3) {
+                            atomicAdd(&a.bsum[b], 1ull << BS_ROUTE_SHIFT);
+                            atomicMax(a.route_c, ~b);
+                        } else {
+                            st_agent(reinterpret_cast<unsigned long long *>(a.counts) + s, 0ull);
+                            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                            atomicAdd(&a.bsum[b], 1ull << BS_FIN_SHIFT);
+                            atomicAdd(&a.copied[b], 1u);
+                        }
+                    } else {
+                        a.counts[s] = 0;
+                    }
                 }
                 refill = true;
             }
@@ -2346,6 +2578,8 @@ tokenize_kernel(KernArgs ka) {
 
         // ---------------------------------------------------------- advance slots, finish strings
         KREFRESH();
+        bool fq = false;            // self-copy: a string with ids finished here (queued below)
+        unsigned fq_s = 0, fq_n = 0;
         if (lane < (unsigned)NG) {
             SlotState &S = SS[lane];
             if (S.active && S.n_atoms > 0 && S.status == 0 && (S.inval & 2)) {
@@ -2353,6 +2587,10 @@ tokenize_kernel(KernArgs ka) {
                 // unbounded pass redoes the whole string (and writes its status and count)
                 a.long_list[atomicAdd(a.long_count, 1u)] = S.s;
                 S.active = 0;
+                if (!BIG && SC_ON && a.inc) {   // self-copy: routed to a later pass
+                    atomicAdd(&a.bsum[S.s / FIN_BATCH], 1ull << BS_ROUTE_SHIFT);
+                    atomicMax(a.route_c, ~(S.s / FIN_BATCH));
+                }
             } else if (S.active && S.n_atoms > 0) {
                 S.capsum += S.wtok;
                 if (S.status == 0 && S.inval) S.status = 1;
@@ -2361,19 +2599,64 @@ tokenize_kernel(KernArgs ka) {
                 S.abase += S.n_atoms;
                 if (S.pos >= S.slen) {
                     const uint64_t s = S.s;
+                    const uint64_t cnt = S.status == 0 ? (uint64_t)S.ntok : 0ull;
                     a.status[s] = (int32_t)S.status;
-                    a.counts[s] = S.status == 0 ? (uint64_t)S.ntok : 0ull;
-                    if (a.bsum && S.status == 0 && S.ntok) atomicAdd(&a.bsum[s / FIN_BATCH], (unsigned long long)S.ntok);
                     if (a.capped) a.capped[s] = S.status == 3 ? -1 : (int32_t)S.capsum;
                     S.active = 0;
+                    if (!BIG && SC_ON && a.inc) {
+                        // the count, drained, then the batch sum: a wave that sees the batch complete
+                        // reads every count of it (sc_publish)
+                        st_agent(reinterpret_cast<unsigned long long *>(a.counts) + s, cnt);
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        atomicAdd(&a.bsum[s / FIN_BATCH], (1ull << BS_FIN_SHIFT) | cnt);
+                        if (!cnt) atomicAdd(&a.copied[s / FIN_BATCH], 1u);   // nothing to copy
+                        fq = cnt != 0;
+                        fq_s = (unsigned)s;
+                        fq_n = (unsigned)cnt;
+                    } else {
+                        a.counts[s] = cnt;
+                        if (a.bsum && cnt) atomicAdd(&a.bsum[s / FIN_BATCH], (unsigned long long)cnt);
+                    }
                 }
             }
         }
         wave_sync();
+        if (!BIG && SC_ON && a.inc) {
+            // queue the strings that finished with ids (the rest of a full queue stays for the finish pass),
+            // then one step of the queue
+            const uint64_t fm = ballot(fq);
+            if (fm) {
+                const unsigned qh = uni(SS[0].qh), qt = uni(SS[0].qt);
+                const unsigned room = CQ_CAP - ((qt - qh) & 0xFFu);
+                const unsigned rk = __builtin_amdgcn_mbcnt_hi((unsigned)(fm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)fm, 0u));
+                if (fq && rk < room) a.cq[(size_t)blockIdx.x * CQ_CAP + ((qt + rk) % CQ_CAP)] = make_uint2(fq_s, fq_n);
+                const unsigned nq = (unsigned)__builtin_popcountll(fm);
+                if (lane == 0) SS[0].qt = (uint8_t)(qt + (nq < room ? nq : room));
+                wave_sync();
+            }
+            (void)sc_step();
+            wave_sync();
+        }
         STAMP(4);
     }
     if constexpr (G == 16 && !BIG)
-        if (n_pend) walk_pending(n_pend);
+        if (n_pend) {
+            walk_pending(n_pend);
+            n_pend = 0;
+        }
+    if (!BIG && SC_ON && a.inc) {
+        // the queue's last strings: their batches complete as the other waves finish (every string is
+        // claimed by now, by running waves); bounded -- what is left stays for the finish pass
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (uni(SS[0].qh) != uni(SS[0].qt)) {
+            if (sc_step()) {
+                wave_sync();
+                continue;
+            }
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) break;   // 200 ms at 100 MHz
+            __builtin_amdgcn_s_sleep(8);
+        }
+    }
     STAMP_FLUSH;
 #undef a
 #undef tv
@@ -2396,18 +2679,6 @@ constexpr unsigned FIN_THREADS = 512;         // threads per finish block (>= FI
 constexpr unsigned SCAN_THREADS = 1024;       // threads of the batch-scan block
 constexpr uint64_t FIN_TARGET_BLOCKS = 2048;  // small batches: each batch's copy is split over slices until the grid has this many blocks
 constexpr uint64_t FIN_MAX_SLICES = 8;
-
-// 64-bit inclusive add-scan over the wave (ds_bpermute shifts)
-__device__ __forceinline__ uint64_t wave_incl_scan_add64(uint64_t v, unsigned lane) {
-#pragma unroll
-    for (unsigned k = 1; k < 64; k <<= 1) {
-        const int src = (int)((lane >= k ? lane - k : lane) << 2);
-        const unsigned lo = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)(unsigned)v);
-        const unsigned hi = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)(unsigned)(v >> 32));
-        v += lane >= k ? (((uint64_t)hi << 32) | lo) : 0ull;
-    }
-    return v;
-}
 
 // inclusive add-scan over a block of NT threads; *total = the block's sum.  Uses s_w[NT / 64] and
 // ends with the block synchronised (s_w reusable after it).
@@ -2461,11 +2732,11 @@ __global__ void __launch_bounds__(SCAN_THREADS) batch_scan_kernel(uint64_t n_str
     const uint64_t per = (nb + SCAN_THREADS - 1) / SCAN_THREADS;
     const uint64_t c0 = (uint64_t)tid * per < nb ? (uint64_t)tid * per : nb, c1 = c0 + per < nb ? c0 + per : nb;
     uint64_t sum = 0;
-    for (uint64_t k = c0; k < c1; k++) sum += bsum[k];
+    for (uint64_t k = c0; k < c1; k++) sum += bsum[k] & BS_SUM_MASK;
     uint64_t total;
     uint64_t run = block_incl_scan_add64<SCAN_THREADS>(sum, s_w, &total) - sum;
     for (uint64_t k = c0; k < c1; k++) {
-        const uint64_t b = bsum[k];
+        const uint64_t b = bsum[k] & BS_SUM_MASK;
         bpre[k] = run;
         bsum[k] = 0;
         run += b;
@@ -2491,6 +2762,8 @@ struct FinishArgs {
     int hist_store;                   // ... stored, not added (DPT_HIST_OVERWRITE in a one-batch call) ...
     const int32_t *status;            // ... with the statuses it counts
     uint32_t n_bins;
+    unsigned long long *inc;          // self-copy calls (finish_kernel<ST, true>): per batch SC_* flags + prefix
+    const uint32_t *copied;           // ... and the strings the first pass copied into place
 };
 
 // CSR offsets and ids: block b takes slice b % slices of batch b / slices.  One count per thread of
@@ -2500,11 +2773,15 @@ struct FinishArgs {
 // per thread.  At 1M strings a batch is one block (3 907 blocks); small calls split each batch's copy
 // so the grid still has ~FIN_TARGET_BLOCKS blocks (a block's copy is a chain of dependent load rounds:
 // 125k strings were 489 blocks of 7 rounds each).
-template <typename ST>
+// SC (self-copy calls): batches the first pass fully copied (SC_OFS and every string copied) only count
+// their histogram; the others take their first id from a look-back -- the nearest published prefix back
+// plus the final batch sums after it -- publish their own, and are copied here as usual.
+template <typename ST, bool SC = false>
 __global__ void __launch_bounds__(FIN_THREADS) finish_kernel(FinishArgs f) {
     __shared__ uint64_t s_rel[FIN_BATCH + 1];   // ids of the batch's strings before string k, + the batch total
     __shared__ uint64_t s_src[FIN_BATCH];       // staging element of each string's first id
     __shared__ uint64_t s_w[FIN_THREADS / 64];
+    __shared__ unsigned s_pub;                  // SC look-back: the nearest published batch, as a distance
     const unsigned tid = threadIdx.x;
     const uint64_t t = blockIdx.x / f.slices;
     const unsigned sl = blockIdx.x % f.slices;
@@ -2517,9 +2794,42 @@ __global__ void __launch_bounds__(FIN_THREADS) finish_kernel(FinishArgs f) {
     const uint64_t src = has ? f.str_off[s0 + tid] - base_off : 0ull;
     uint64_t total;
     uint64_t o0 = 0;   // one batch: its first id is 0
-    if (f.fold) {   // the batch's first id: the sums of the batches before it (t <= FIN_FOLD_MAX)
+    bool done = false;   // SC: the first pass copied the whole batch
+    if constexpr (SC) {
+        for (uint64_t k = (uint64_t)blockIdx.x * FIN_THREADS + tid; k < f.fold_n; k += (uint64_t)gridDim.x * FIN_THREADS)
+            f.fold_zero[k] = 0;   // the other parity's arrays, for the next call
+        const unsigned long long iv = __hip_atomic_load(&f.inc[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t nsz = f.n_str - s0 < FIN_BATCH ? f.n_str - s0 : FIN_BATCH;
+        done = (iv & SC_OFS) && f.copied[t] == nsz;
+        if (!done) {
+            // look-back: the ids before batch t = the nearest published inclusive prefix + the sums after it
+            uint64_t acc = 0;
+            for (uint64_t top = t;;) {
+                const int64_t k = (int64_t)top - 1 - (int64_t)tid;
+                unsigned long long pv = SC_PUB;   // k < 0: before the first batch, prefix 0
+                if (k >= 0) pv = __hip_atomic_load(&f.inc[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (tid == 0) s_pub = FIN_THREADS;
+                __syncthreads();
+                if (pv & SC_PUB) atomicMin(&s_pub, tid);
+                __syncthreads();
+                const unsigned l0 = s_pub;
+                uint64_t part = 0, sum = 0;
+                if (tid < l0 && k >= 0) part = f.fold[k] & BS_SUM_MASK;
+                (void)block_incl_scan_add64<FIN_THREADS>(part, s_w, &sum);
+                acc += sum;
+                if (l0 < FIN_THREADS) {
+                    if (tid == l0) s_w[0] = pv & SC_VAL_MASK;   // (s_w is free again after the scan)
+                    __syncthreads();
+                    o0 = acc + s_w[0];
+                    __syncthreads();
+                    break;
+                }
+                top -= FIN_THREADS;   // (top > FIN_THREADS here: k < 0 counts as published)
+            }
+        }
+    } else if (f.fold) {   // the batch's first id: the sums of the batches before it (t <= FIN_FOLD_MAX)
         uint64_t ps = 0;
-        for (uint64_t k = tid; k < t; k += FIN_THREADS) ps += f.fold[k];
+        for (uint64_t k = tid; k < t; k += FIN_THREADS) ps += f.fold[k] & BS_SUM_MASK;
         (void)block_incl_scan_add64<FIN_THREADS>(ps, s_w, &o0);
         for (uint64_t k = (uint64_t)blockIdx.x * FIN_THREADS + tid; k < f.fold_n; k += (uint64_t)gridDim.x * FIN_THREADS)
             f.fold_zero[k] = 0;
@@ -2562,6 +2872,14 @@ __global__ void __launch_bounds__(FIN_THREADS) finish_kernel(FinishArgs f) {
             else if (lh[b]) atomicAdd(&f.hist[b], lh[b]);
         }
     }
+    if (SC && done) {   // the first pass wrote the batch's offsets and ids
+        if (t == 0 && tid == 0 && sl == 0) {
+            f.id_off[0] = 0;
+            reset_counters(f.ctr);
+        }
+        return;
+    }
+    if (SC && sl == 0 && tid == 0) atomicOr(&f.inc[t], SC_PUB | (o0 + total));   // for the later batches' look-backs
     if (sl == 0) {
         if (has) f.id_off[s0 + tid + 1] = o0 + incl;
         if (t == 0 && tid == 0) {
@@ -2720,6 +3038,10 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     a.pend = p.pend; a.ws_node = p.ws_node; a.ws_base = p.ws_base; a.ws_id = p.ws_id;
     a.long_span = p.long_span;
     a.hist_zero = nullptr; a.n_hist = 0;
+    // self-copy (the host decides: CSR calls of >= SC_MIN_BATCHES batches without edges or length-only DPs)
+    a.inc = p.self_copy ? p.inc : nullptr; a.copied = p.copied; a.cq = p.cq;
+    a.route_c = p.retry_count + 5;   // (counter block uint32 [5]: reset_counters zeroes it)
+    a.id_off = p.id_off; a.ids = p.ids;
     TrieView tv{p.slots, p.slot_ids, p.slots4, p.root_base, p.n_slots, p.pair16};
     const bool wide = (p.mode & DPT_MODE_MASK) == DPT_MODE_ATOMS;   // atoms of up to 8 bytes
     const bool raw = (p.mode & DPT_MODE_MASK) == DPT_MODE_RAW;
@@ -2765,7 +3087,8 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
         EncodeArgs b = a;
         b.work_list = p.retry_list; b.work_count = p.retry_count;
         b.work_next = p.retry_count + 2;
-        if (!p.padded && fin_fold(p.n_str) && p.hist && p.hist_overwrite && p.hist_bins >= 2 && p.hist_bins <= FIN_MAX_BINS) {
+        if (!p.padded && (fin_fold(p.n_str) || p.self_copy) && p.hist && p.hist_overwrite && p.hist_bins >= 2 &&
+            p.hist_bins <= FIN_MAX_BINS) {
             b.hist_zero = reinterpret_cast<unsigned long long *>(p.hist);   // (the finish pass adds to it)
             b.n_hist = p.hist_bins + 8u;
         }
@@ -2804,14 +3127,16 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     const uint64_t nb = (p.n_str + FIN_BATCH - 1) / FIN_BATCH;
     FinishArgs f;
     f.bsum = nullptr; f.ctr = nullptr; f.fold = nullptr; f.fold_zero = nullptr; f.fold_n = 0;
-    const bool fold = fin_fold(p.n_str);
+    f.inc = p.inc; f.copied = p.copied;
+    const bool sc = p.self_copy;
+    const bool fold = !sc && fin_fold(p.n_str);
     const bool fold_hist = p.hist && p.hist_bins >= 2 && p.hist_bins <= FIN_MAX_BINS;
     f.hist = fold_hist ? reinterpret_cast<unsigned long long *>(p.hist) : nullptr;
     f.status = p.status;
     f.n_bins = p.hist_bins;
     f.hist_store = (fold_hist && p.hist_overwrite && nb <= 1) ? 1 : 0;
-    unsigned long long *hz = (fold_hist && p.hist_overwrite && nb > 1 && !fold) ? f.hist : nullptr;
-    if (fold) { f.fold = p.flags; f.fold_zero = p.bpre; f.fold_n = p.flags_half; f.ctr = p.retry_count; }
+    unsigned long long *hz = (fold_hist && p.hist_overwrite && nb > 1 && !fold && !sc) ? f.hist : nullptr;
+    if (fold || sc) { f.fold = p.flags; f.fold_zero = p.zero_other; f.fold_n = p.zero_n; f.ctr = p.retry_count; }
     else if (nb > 1) hipLaunchKernelGGL(batch_scan_kernel, dim3(1), dim3(SCAN_THREADS), 0, stream, p.n_str, p.flags, p.bpre, p.retry_count,
                                         hz, p.hist_bins + 8u);
     else { f.bsum = p.flags; f.ctr = p.retry_count; }
@@ -2821,8 +3146,14 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     uint64_t sls = (FIN_TARGET_BLOCKS + nb - 1) / nb;
     f.slices = (unsigned)(sls < 1 ? 1 : (sls > FIN_MAX_SLICES ? FIN_MAX_SLICES : sls));
     const uint64_t fb = nb * f.slices;
-    if (p.staging16) hipLaunchKernelGGL(finish_kernel<int16_t>, dim3((unsigned)fb), dim3(FIN_THREADS), 0, stream, f);
-    else hipLaunchKernelGGL(finish_kernel<int32_t>, dim3((unsigned)fb), dim3(FIN_THREADS), 0, stream, f);
+    if (sc) {
+        if (p.staging16) hipLaunchKernelGGL((finish_kernel<int16_t, true>), dim3((unsigned)fb), dim3(FIN_THREADS), 0, stream, f);
+        else hipLaunchKernelGGL((finish_kernel<int32_t, true>), dim3((unsigned)fb), dim3(FIN_THREADS), 0, stream, f);
+    } else if (p.staging16) {
+        hipLaunchKernelGGL(finish_kernel<int16_t>, dim3((unsigned)fb), dim3(FIN_THREADS), 0, stream, f);
+    } else {
+        hipLaunchKernelGGL(finish_kernel<int32_t>, dim3((unsigned)fb), dim3(FIN_THREADS), 0, stream, f);
+    }
     if (p.hist && !fold_hist) {   // too many bins for the finish pass's LDS: the separate pass
         hipError_t eh = hipGetLastError();
         if (eh != hipSuccess) return eh;
@@ -2834,6 +3165,7 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
 }
 
 size_t pend_scratch_bytes(unsigned max_blocks) { return (size_t)max_blocks * 64 * sizeof(uint4); }
+size_t cq_scratch_bytes(unsigned max_blocks) { return (size_t)max_blocks * CQ_CAP * sizeof(uint2); }
 
 size_t wsl_scratch_bytes(unsigned max_blocks) {
     return (size_t)max_blocks * 4 * GroupLDS<SMALL_CH, 16>::WSL_STRIDE;   // NG x stride covers both G at CH = 256

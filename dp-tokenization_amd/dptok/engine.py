@@ -421,6 +421,15 @@ class Encoder:
         check(_lib.lib().dpt_ctx_long_need(self.handle, ctypes.byref(a), ctypes.byref(b)), "dpt_ctx_long_need")
         return a.value, b.value
 
+    def copy_stats(self) -> Tuple[int, int, int]:
+        """(strings the last call's first pass copied into the CSR arrays itself, batches whose offsets
+        it wrote, the call's 256-string batches) -- all 0 when it did not self-copy; call after the
+        encode's stream has completed (dpt_ctx_copy_stats)."""
+        a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        check(_lib.lib().dpt_ctx_copy_stats(self.handle, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)),
+              "dpt_ctx_copy_stats")
+        return a.value, b.value, c.value
+
     def set_histogram(self, hist_ptr: int, n_bins: int, overwrite: bool = False) -> None:
         """Fold the token-count histogram into the next encode on this engine (dpt_ctx_set_histogram_ex:
         its finish pass adds to hist, device int64[n_bins + 8], or with ``overwrite`` replaces it -- the

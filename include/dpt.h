@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define DPT_ABI_VERSION 2
+#define DPT_ABI_VERSION 3
 
 /* return codes */
 #define DPT_OK 0
@@ -113,6 +113,13 @@ int dpt_ctx_workspace_bytes(const dpt_ctx *c, uint64_t *device_path, uint64_t *h
  * strings its unbounded pass took (*need) and the arena's capacity (*cap).  need > cap: the strings that
  * did not fit have status DPT_STATUS_TOO_LONG -- reserve long_bytes >= need and call again. */
 int dpt_ctx_long_need(dpt_ctx *c, uint64_t *need, uint64_t *cap);
+/* ABI 3.  After the ctx's last dpt_encode / dpt_encode_host has completed (synchronise its stream
+ * first): the strings whose ids the first tokenize pass copied into the CSR arrays itself (*copied,
+ * strings without ids included; the finish pass copies the others), the 256-string batches whose
+ * offsets it wrote (*batches_ofs) and the call's batches (*n_batches).  All 0 when the call did not
+ * self-copy (fewer than 8 batches, dpt_encode_padded / dpt_dp_host*, or DPT_SELF_COPY=0 in the
+ * environment -- an A/B switch read per call). */
+int dpt_ctx_copy_stats(dpt_ctx *c, uint64_t *copied, uint64_t *batches_ofs, uint64_t *n_batches);
 
 /*
  * Tokenize n_str strings, CSR-packed: string s is text[str_off[s]-str_off[0] .. str_off[s+1]-str_off[0]),

@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     for name in _declared():
         assert hasattr(L, name), name
     assert set(_declared()) == set(_lib.EXPORTED)
-    assert L.dpt_abi_version() == 2
+    assert L.dpt_abi_version() == 3
 
 
 def test_errors_without_device_or_args():

@@ -1,14 +1,29 @@
 """CPU model of the tokenize kernel's work distribution (dpt_kernels.hip tokenize_kernel, the
-`claim` lambda and the refill loop): npart = min(NPART, max(1, n / 4096)) partition counters over
-contiguous string ranges, claims of as many strings as the wave has free slots (1..4), a used-up
-mask; each wave starts on partition blockIdx mod npart and moves to the next unmarked partition
-after a claim reaches its partition's end.  Under random interleavings of the waves' atomics every
-string is handed out exactly once and every wave stops."""
+`claim` lambda and the refill loop): npart = min(NPART, max(1, n / 4096)) partition counters,
+partition p holding the 256-string chunks p, p + npart, ... (part_size / part_string), claims of
+as many strings as the wave has free slots (1..4), a used-up mask; each wave starts on partition
+blockIdx mod npart and moves to the next unmarked partition after a claim reaches its partition's
+end.  Under random interleavings of the waves' atomics every string is handed out exactly once and
+every wave stops."""
 import random
 
 import pytest
 
 NPART = 16
+CHUNK = 256   # FIN_BATCH
+
+
+def part_size(n, npart, p):
+    nch = (n + CHUNK - 1) // CHUNK
+    if nch <= p:
+        return 0
+    cnt = (nch - 1 - p) // npart + 1
+    last = p + (cnt - 1) * npart
+    return cnt * CHUNK - (nch * CHUNK - n if last == nch - 1 else 0)
+
+
+def part_string(npart, p, v):
+    return ((v // CHUNK) * npart + p) * CHUNK + v % CHUNK
 
 
 def run(n_work, n_waves, seed):
@@ -24,9 +39,9 @@ def run(n_work, n_waves, seed):
         nonlocal mask
         while True:
             p = wv["part"]
-            lo, hi = n_work * p // npart, n_work * (p + 1) // npart
+            hi = part_size(n_work, npart, p)
             b = ctr[p]; ctr[p] += req                 # atomicAdd
-            nb = lo + b
+            nb = b
             ne = min(nb + req, hi) if nb < hi else nb
             claimed_all = False
             if nb + req >= hi:
@@ -40,7 +55,7 @@ def run(n_work, n_waves, seed):
                     pick = hi_free if hi_free else free
                     wv["part"] = (pick & -pick).bit_length() - 1
             if ne > nb or claimed_all:
-                return list(range(nb, ne)), claimed_all
+                return [part_string(npart, p, v) for v in range(nb, ne)], claimed_all
 
     live = list(range(n_waves))
     while live:
@@ -54,7 +69,18 @@ def run(n_work, n_waves, seed):
     return got
 
 
-@pytest.mark.parametrize("n_work,n_waves", [(1, 1), (3, 64), (4095, 50), (4096 * 16 + 3, 300), (100003, 700), (70000, 5632)])
+@pytest.mark.parametrize("n_work,n_waves", [(1, 1), (3, 64), (4095, 50), (4096 * 16 + 3, 300), (100003, 700), (70000, 5632),
+                                             (256 * 16 * 5 + 256, 400), (256 * 16 * 5 - 1, 400)])
 def test_every_string_exactly_once(n_work, n_waves):
     for seed in range(3):
         assert run(n_work, n_waves, seed) == [1] * n_work
+
+
+def test_partitions_tile_the_batch():
+    # part_string maps each partition's local indices onto disjoint string sets covering [0, n)
+    for n in [1, 255, 256, 257, 4096, 65535, 65536, 65537, 256 * 16 * 7 + 100, 1000000]:
+        npart = min(NPART, max(1, n // 4096))
+        seen = []
+        for p in range(npart):
+            seen += [part_string(npart, p, v) for v in range(part_size(n, npart, p))]
+        assert sorted(seen) == list(range(n)), n

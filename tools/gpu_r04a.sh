@@ -6,8 +6,9 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 B=dp-tokenization_amd/csrc/build
-H=dp-tokenization_amd/dptok/libdpt.so
-out=gpurun_out/r04a; mkdir -p $out
+H=dp-tokenization_amd/csrc/build/var_base/libdpt.so   # (the r04a source built without the self-copy code)
+export DPT_SELF_COPY=0
+out=gpurun_out/r04a; mkdir -p $out/phase
 CTRS="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_INSTS_VALU"
 timeout -k 10 300 python3 tools/prof_driver.py 200000 1 s2orc gen-only || exit 1
 for wl in "ascii 1000000" "s2orc 200000"; do
