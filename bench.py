@@ -431,6 +431,9 @@ def main():
         dt = float(t.item())
     ms_stage, launches = enc.profile_read()
     enc.profile(False)
+    # the last timed call's self-copy (dpt_ctx_copy_stats): strings its first pass copied into the CSR
+    # arrays itself, batches whose offsets it wrote (the finish pass copied the rest)
+    sc_copied, sc_batches, sc_nb = enc.copy_stats()
 
     # secondary: the encode alone through dpt_encode_padded (ids left at each string's byte offset,
     # per-string counts; no finish pass, no histogram) -- reported beside `value`, never as it
@@ -542,6 +545,8 @@ def main():
                          "alg_bytes_staged_width": alg_staged, "staged_id_bytes": id_bytes,
                          "frac_staged_width": alg_staged / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
             "cpu_baseline": cpu,
+            "self_copy": {"strings_copied_by_first_pass": sc_copied, "strings": M, "batches_with_offsets": sc_batches,
+                          "batches": sc_nb, "enabled": os.environ.get("DPT_SELF_COPY", "1") != "0"},
             "padded_layout": {"api": "dpt_encode_padded (ids at each string's byte offset + per-string counts, no CSR pass); encode only, no histogram",
                               "ms_per_step": dtp / args.steps * 1e3, "bytes_per_s": bytes_all * args.steps / dtp,
                               "counts_and_status_equal_csr": padded_same},

@@ -9,6 +9,7 @@
 #include <string.h>
 
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/dpt.h"
@@ -208,13 +209,23 @@ std::vector<uint32_t> build_token_hash(const uint8_t *blob, const uint64_t *off,
     struct Key { uint32_t w[dpt::TOKHASH_MAX_BYTES_LONG / 4]; uint32_t len; int32_t id; };
     std::vector<Key> keys;
     keys.reserve(n);
+    // entries of equal bytes: one key, the last entry's id (dict semantics, as the trie: dpt_vocab.cpp) --
+    // two keys of one byte string would share a fingerprint and no seed could build the table
+    std::unordered_map<std::string, size_t> seen;
+    seen.reserve(n);
     for (uint32_t t = 0; t < n; t++) {
         const uint64_t len = off[t + 1] - off[t];
         if (len == 0 || len > dpt::TOKHASH_MAX_BYTES_LONG) continue;
+        const int32_t id = ids ? ids[t] : (int32_t)t;
+        const auto ins = seen.emplace(std::string(reinterpret_cast<const char *>(blob + (off[t] - off[0])), (size_t)len), keys.size());
+        if (!ins.second) {
+            keys[ins.first->second].id = id;
+            continue;
+        }
         Key k;
         memset(k.w, 0, sizeof(k.w));
         k.len = (uint32_t)len;
-        k.id = ids ? ids[t] : (int32_t)t;
+        k.id = id;
         memcpy(k.w, blob + (off[t] - off[0]), len);   // little-endian dwords, zero past the token
         keys.push_back(k);
     }
@@ -520,12 +531,23 @@ int dpt_ctx_long_need(dpt_ctx *c, uint64_t *need, uint64_t *cap) {
     return DPT_OK;
 }
 
+// dev_call: dpt_encode itself (the call an armed histogram belongs to, dpt_ctx_set_histogram_ex); the
+// host path and dpt_encode_padded leave it armed
 static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uint8_t *text, uint64_t n_bytes,
                        const uint64_t *str_off, const uint8_t *cut_mask, uint64_t n_str, int32_t *ids, uint64_t ids_cap,
                        uint64_t *id_off, int32_t *status, int32_t *capped_len, uint64_t *edges, void *hip_stream,
-                       uint64_t *far = nullptr, uint64_t far_cap = 0, uint64_t *padded_counts = nullptr) {
+                       uint64_t *far = nullptr, uint64_t far_cap = 0, uint64_t *padded_counts = nullptr,
+                       bool dev_call = false) {
     const int mode = mode_flags & DPT_MODE_MASK;
     if (!c || !v) return fail(DPT_E_ARG, "null ctx or vocab");
+    // the armed histogram is this call's whatever happens below (one call only, failed ones included)
+    int64_t *hist = dev_call ? c->hist : nullptr;
+    const uint32_t hist_bins = c->hist_bins;
+    const bool hist_overwrite = c->hist_overwrite;
+    if (dev_call) {
+        c->hist = nullptr;
+        c->hist_overwrite = false;
+    }
     if (mode != DPT_MODE_RAW && mode != DPT_MODE_PRESPLIT && mode != DPT_MODE_ATOMS) return fail(DPT_E_ARG, "bad mode");
     if (mode_flags & ~(DPT_MODE_MASK | DPT_FLAG_UNCAPPED | DPT_FLAG_LEN_ONLY)) return fail(DPT_E_ARG, "bad flags");
     const bool padded = padded_counts != nullptr;
@@ -582,11 +604,9 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
     p.staging16 = v->ids16 ? c->staging16 : nullptr;
     p.padded = padded;
     p.pend = c->pend;
-    p.hist = padded ? nullptr : c->hist;   // (dpt_encode_padded has no offsets to count)
-    p.hist_bins = c->hist_bins;
-    p.hist_overwrite = c->hist_overwrite;
-    c->hist = nullptr;                     // one call only
-    c->hist_overwrite = false;
+    p.hist = hist;
+    p.hist_bins = hist_bins;
+    p.hist_overwrite = hist_overwrite;
     if (padded) {   // the ids go straight to their final place (int32), the counts to the caller's array
         p.staging = ids;
         p.staging16 = nullptr;
@@ -628,7 +648,7 @@ int dpt_encode(dpt_ctx *c, const dpt_vocab *v, int mode, const uint8_t *text, ui
                uint64_t *id_off, int32_t *status, int32_t *capped_len, void *hip_stream) {
     if (mode & ~DPT_MODE_MASK) return fail(DPT_E_ARG, "flags are for dpt_dp_host");
     return encode_impl(c, v, mode, text, n_bytes, str_off, cut_mask, n_str, ids, ids_cap, id_off, status, capped_len,
-                       nullptr, hip_stream);
+                       nullptr, hip_stream, nullptr, 0, nullptr, true);
 }
 
 int dpt_encode_padded(dpt_ctx *c, const dpt_vocab *v, int mode, const uint8_t *text, uint64_t n_bytes,
@@ -837,7 +857,8 @@ int dpt_dp_host_far(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uint8_
 
 int dpt_token_histogram(const uint64_t *id_off, const int32_t *status, uint64_t n_str, int64_t *hist, uint32_t n_bins,
                         void *hip_stream) {
-    if (!id_off || !hist || (n_str && !status) || n_bins < 2) return fail(DPT_E_ARG, "bad histogram arguments");
+    if (!id_off || !hist || (n_str && !status) || n_bins < 2 || n_bins > DPT_HIST_MAX_BINS)
+        return fail(DPT_E_ARG, "bad histogram arguments (2 <= n_bins <= DPT_HIST_MAX_BINS)");
     hipError_t e = dpt::launch_histogram(id_off, status, n_str, hist, n_bins, (hipStream_t)hip_stream);
     if (e != hipSuccess) return hip_fail(e, "histogram launch");
     return DPT_OK;
@@ -845,7 +866,7 @@ int dpt_token_histogram(const uint64_t *id_off, const int32_t *status, uint64_t 
 
 int dpt_ctx_set_histogram_ex(dpt_ctx *c, int64_t *hist, uint32_t n_bins, int flags) {
     if (!c) return fail(DPT_E_ARG, "null ctx");
-    if (hist && n_bins < 2) return fail(DPT_E_ARG, "n_bins < 2");
+    if (hist && (n_bins < 2 || n_bins > DPT_HIST_MAX_BINS)) return fail(DPT_E_ARG, "n_bins outside 2..DPT_HIST_MAX_BINS");
     if (flags & ~DPT_HIST_OVERWRITE) return fail(DPT_E_ARG, "unknown histogram flags");
     c->hist = hist;
     c->hist_bins = hist ? n_bins : 0;

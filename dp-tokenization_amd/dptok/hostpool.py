@@ -16,13 +16,16 @@ parent thread each.  They start on the first large batch and are reused.  Batche
 """
 from __future__ import annotations
 
+import atexit
 import os
 import pickle
+import select
 import struct
 import subprocess
 import sys
 import threading
-from typing import List, Optional, Sequence
+import time
+from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 
@@ -36,15 +39,28 @@ def send_msg(f, obj) -> None:
     f.flush()
 
 
-def recv_msg(f):
-    h = f.read(_HDR.size)
-    if len(h) < _HDR.size:
-        raise EOFError("worker pipe closed")
-    n = _HDR.unpack(h)[0]
-    b = f.read(n)
-    if len(b) < n:
-        raise EOFError("worker pipe closed")
-    return pickle.loads(b)
+def _read_exact(fd: int, n: int, deadline: Optional[float]) -> bytes:
+    """n bytes from a pipe's file descriptor; TimeoutError past the deadline (time.monotonic())."""
+    parts, got = [], 0
+    while got < n:
+        if deadline is not None:
+            left = deadline - time.monotonic()
+            if left <= 0 or not select.select([fd], [], [], left)[0]:
+                raise TimeoutError("pre-tokenization worker did not answer in time")
+        b = os.read(fd, min(n - got, 1 << 20))
+        if not b:
+            raise EOFError("worker pipe closed")
+        parts.append(b)
+        got += len(b)
+    return b"".join(parts)
+
+
+def recv_msg(f, timeout: Optional[float] = None):
+    """One length-prefixed pickle from a worker's (unbuffered) stdout; timeout: seconds or None."""
+    fd = f.fileno()
+    deadline = None if timeout is None else time.monotonic() + timeout
+    n = _HDR.unpack(_read_exact(fd, _HDR.size, deadline))[0]
+    return pickle.loads(_read_exact(fd, n, deadline))
 
 
 def cpu_share() -> int:
@@ -75,6 +91,10 @@ def concat_packed(parts):
     return (np.concatenate(texts + [z]), np.concatenate(offs), np.concatenate(cuts + [z]), np.concatenate(cnts))
 
 
+# seconds a worker may take per chunk: a base plus a rate far below SentencePiece's (~1 MB/s per core)
+TIMEOUT_BASE_S, TIMEOUT_PER_BYTE_S = 60.0, 1e-5
+
+
 class PretokenizePool:
     def __init__(self, tokenizer, table, encode_ids, procs: Optional[int] = None, min_batch: int = 2048):
         self.tokenizer = tokenizer
@@ -103,15 +123,15 @@ class PretokenizePool:
         env.setdefault("TOKENIZERS_PARALLELISM", "false")   # one process per core already
         for _ in range(self.procs):
             p = subprocess.Popen([sys.executable, "-m", "dptok._pretok_worker"], stdin=subprocess.PIPE,
-                                 stdout=subprocess.PIPE, env=env, cwd=here)
+                                 stdout=subprocess.PIPE, env=env, cwd=here, bufsize=0)
             self._workers.append(p)
         try:
             for p in self._workers:
                 send_msg(p.stdin, (list(sys.path), tok_bytes))
             for p in self._workers:
-                if recv_msg(p.stdout) != "ready":
+                if recv_msg(p.stdout, TIMEOUT_BASE_S) != "ready":
                     raise RuntimeError("pre-tokenization worker failed to start")
-        except (EOFError, OSError, RuntimeError):
+        except (EOFError, OSError, RuntimeError, TimeoutError):
             self.close()
             self._broken = True
             return False
@@ -137,13 +157,16 @@ class PretokenizePool:
                             nxt[0] += 1
                         if i >= k or errors:
                             return
-                        send_msg(p.stdin, list(texts[bounds[i]:bounds[i + 1]]))
-                        kind, val = recv_msg(p.stdout)
+                        chunk = list(texts[bounds[i]:bounds[i + 1]])
+                        send_msg(p.stdin, chunk)
+                        # bounded: a hung worker (e.g. inside the tokenizer's own threads) counts as a dead one
+                        budget = TIMEOUT_BASE_S + TIMEOUT_PER_BYTE_S * sum(len(t) for t in chunk)
+                        kind, val = recv_msg(p.stdout, budget)
                         if kind == "err":
                             errors.append(val)
                             return
                         results[i] = val
-                except (EOFError, OSError) as e:
+                except (EOFError, OSError, TimeoutError) as e:
                     errors.append(e)
 
             th = [threading.Thread(target=feed, args=(p,), daemon=True) for p in self._workers]
@@ -153,7 +176,7 @@ class PretokenizePool:
                 t.join()
             if errors:
                 e = errors[0]
-                if isinstance(e, (EOFError, OSError)):   # a worker died: drop the pool, run in-process
+                if isinstance(e, (EOFError, OSError, TimeoutError)):   # a worker died or hung: drop the pool, run in-process
                     self.close()
                     self._broken = True
                     return self.table.pack(self.encode_ids(texts))
@@ -169,7 +192,7 @@ class PretokenizePool:
         for p in self._workers:
             try:
                 p.wait(timeout=10)
-            except subprocess.TimeoutExpired:
+            except subprocess.TimeoutExpired:   # (a hung worker: its own process only, by its handle)
                 p.kill()
                 p.wait()
             try:
@@ -183,3 +206,31 @@ class PretokenizePool:
             self.close()
         except Exception:
             pass
+
+
+# One pool per tokenizer object: every dp_tokenize_llama(tok, "llama") adapter over the same tokenizer
+# shares its workers (each holds an unpickled tokenizer), and every pool is closed at exit.
+_POOLS: Dict[int, "PretokenizePool"] = {}
+_POOLS_LOCK = threading.Lock()
+
+
+def shared_pool(tokenizer, table, encode_ids, **kw) -> "PretokenizePool":
+    with _POOLS_LOCK:
+        pool = _POOLS.get(id(tokenizer))
+        if pool is None or pool.tokenizer is not tokenizer:   # (an id reused after its tokenizer died)
+            if pool is not None:
+                pool.close()
+            pool = PretokenizePool(tokenizer, table, encode_ids, **kw)
+            _POOLS[id(tokenizer)] = pool   # (keeps the tokenizer alive, so its id stays unique)
+        return pool
+
+
+@atexit.register
+def _close_pools() -> None:
+    with _POOLS_LOCK:
+        for pool in _POOLS.values():
+            try:
+                pool.close()
+            except Exception:
+                pass
+        _POOLS.clear()

@@ -30,7 +30,7 @@ if _HERE not in sys.path:
 
 from dptok import Encoder, Vocab, raise_for_status  # noqa: E402
 from dptok.engine import PieceTable  # noqa: E402
-from dptok.hostpool import PretokenizePool  # noqa: E402
+from dptok.hostpool import shared_pool  # noqa: E402
 
 SPACE_TOKEN = "▁"
 
@@ -117,16 +117,23 @@ def batch_encoder(tokenizer):
             and type(tokenizer).encode is PreTrainedTokenizerBase.encode
             and type(tokenizer)._encode_plus is TokenizersBackend._encode_plus
             and hasattr(tokenizer._tokenizer, "encode_batch_fast")):
+        fast = [True]   # (the private calls below are pinned on transformers 5.x; any other signature: per text)
+
         def encode_batch(texts):
-            pad, trunc, max_len, _ = tokenizer._get_padding_truncation_strategies(padding=False, truncation=None,
-                                                                                  max_length=None)
-            if pad != PaddingStrategy.DO_NOT_PAD or trunc != TruncationStrategy.DO_NOT_TRUNCATE:
-                return [tokenizer.encode(t) for t in texts]
-            tokenizer.set_truncation_and_padding(padding_strategy=pad, truncation_strategy=trunc, max_length=max_len,
-                                                 stride=0, pad_to_multiple_of=None, padding_side=None)
-            if tokenizer._tokenizer.encode_special_tokens != tokenizer.split_special_tokens:
-                tokenizer._tokenizer.encode_special_tokens = tokenizer.split_special_tokens
-            return [e.ids for e in tokenizer._tokenizer.encode_batch_fast(list(texts), add_special_tokens=True)]
+            if fast[0]:
+                try:
+                    pad, trunc, max_len, _ = tokenizer._get_padding_truncation_strategies(padding=False, truncation=None,
+                                                                                          max_length=None)
+                    if pad == PaddingStrategy.DO_NOT_PAD and trunc == TruncationStrategy.DO_NOT_TRUNCATE:
+                        tokenizer.set_truncation_and_padding(padding_strategy=pad, truncation_strategy=trunc,
+                                                             max_length=max_len, stride=0, pad_to_multiple_of=None,
+                                                             padding_side=None)
+                        if tokenizer._tokenizer.encode_special_tokens != tokenizer.split_special_tokens:
+                            tokenizer._tokenizer.encode_special_tokens = tokenizer.split_special_tokens
+                        return [e.ids for e in tokenizer._tokenizer.encode_batch_fast(list(texts), add_special_tokens=True)]
+                except (TypeError, AttributeError):
+                    fast[0] = False   # from now on the library's public encode, per text
+            return [tokenizer.encode(t) for t in texts]
         return encode_batch
     return lambda texts: [tokenizer.encode(t) for t in texts]
 
@@ -150,7 +157,7 @@ def dp_tokenize_llama(llama_tokenizer, pretokenize_option="llama"):
         pretokenize = pretokenize_with_llama(llama_tokenizer, vocab_bidict)
         pieces = PieceTable(t2i)
         encode_ids = batch_encoder(llama_tokenizer)
-        host = PretokenizePool(llama_tokenizer, pieces, encode_ids)   # worker processes for large batches
+        host = shared_pool(llama_tokenizer, pieces, encode_ids)   # worker processes for large batches (one per tokenizer)
 
         def encode_many(texts: Sequence[str]) -> List[List[int]]:
             # SentencePiece runs on the host (third-party); the pieces -> words merge is array

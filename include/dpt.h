@@ -194,13 +194,17 @@ int dpt_dp_host_far(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uint8_
  * Token-count histogram (device pointers): hist[0..n_bins) counts strings by
  * #ids (last bin = overflow), then hist[n_bins+0] = total ids, hist[n_bins+1] =
  * total strings, hist[n_bins+2+k] = strings with status k (k = 0..4).
- * hist must hold n_bins + 8 int64 and is ACCUMULATED into (zero it first).
+ * hist must hold n_bins + 8 int64 and is ACCUMULATED into (zero it first).  2 <= n_bins <= DPT_HIST_MAX_BINS
+ * (the bins are counted in LDS).
  */
+#define DPT_HIST_MAX_BINS 16384
 int dpt_token_histogram(const uint64_t *id_off, const int32_t *status, uint64_t n_str,
                         int64_t *hist, uint32_t n_bins, void *hip_stream);
 
 /*
  * Fold the token-count histogram of dpt_token_histogram into the NEXT dpt_encode call on this ctx
+ * (dpt_encode only: dpt_encode_host, dpt_encode_padded and dpt_dp_host* leave it armed; a dpt_encode
+ * that fails still consumes it)
  * (its finish pass: no separate launch, no re-read of the offsets and statuses): hist (device
  * pointer, n_bins + 8 int64, layout and accumulate semantics of dpt_token_histogram) is added to
  * once, stream-ordered with that call.  hist NULL cancels.  n_bins above 1024 uses the separate

@@ -149,3 +149,56 @@ def test_pretokenize_pool_equals_in_process(kind, tokenizers_):
         assert all(np.array_equal(a, b) for a, b in zip(got, ref))
     finally:
         pool.close()
+
+
+def test_batch_encoder_falls_back_on_private_api_change(tokenizers_, monkeypatch):
+    """the tokenizers fast path calls private transformers APIs; if their signature changes,
+    the batch encoder switches to the public per-text encode instead of raising."""
+    from packages.tokenizer_utils import batch_encoder
+    tok = tokenizers_["hf"]
+    texts = ["hello world", " a\nb", "", "OptimalLengthTokenization"]
+    ref = [tok.encode(t) for t in texts]
+    enc = batch_encoder(tok)
+
+    class Backend:   # the Rust backend, with a changed batch signature
+        def __init__(self, t):
+            object.__setattr__(self, "_t", t)
+
+        def __getattr__(self, k):
+            return getattr(self._t, k)
+
+        def __setattr__(self, k, v):
+            setattr(self._t, k, v)
+
+        def encode_batch_fast(self, *a, **k):
+            raise TypeError("unexpected keyword argument")
+    monkeypatch.setattr(tok, "_tokenizer", Backend(tok._tokenizer))
+    assert enc(texts) == ref
+    assert enc(texts) == ref   # (permanently per text now)
+
+
+def test_worker_recv_times_out():
+    """a pre-tokenization worker that never answers counts as a dead one (bounded wait)."""
+    import os
+    import time
+    from dptok.hostpool import recv_msg
+    r, w = os.pipe()
+    try:
+        f = os.fdopen(r, "rb", buffering=0)
+        t0 = time.monotonic()
+        with pytest.raises(TimeoutError):
+            recv_msg(f, 0.3)
+        assert time.monotonic() - t0 < 5
+    finally:
+        os.close(w)
+        f.close()
+
+
+def test_one_pool_per_tokenizer(tokenizers_):
+    """adapters over the same tokenizer share one worker pool."""
+    from dptok.engine import PieceTable
+    from dptok.hostpool import shared_pool
+    from packages.tokenizer_utils import batch_encoder
+    tok = tokenizers_["sp"]
+    table, enc = PieceTable(dict(tok.get_vocab())), batch_encoder(tok)
+    assert shared_pool(tok, table, enc) is shared_pool(tok, table, enc)
