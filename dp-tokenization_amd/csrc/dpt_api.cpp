@@ -537,7 +537,7 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
                        const uint64_t *str_off, const uint8_t *cut_mask, uint64_t n_str, int32_t *ids, uint64_t ids_cap,
                        uint64_t *id_off, int32_t *status, int32_t *capped_len, uint64_t *edges, void *hip_stream,
                        uint64_t *far = nullptr, uint64_t far_cap = 0, uint64_t *padded_counts = nullptr,
-                       bool dev_call = false) {
+                       bool dev_call = false, uint64_t *ctr_snap = nullptr, bool no_fallback = false) {
     const int mode = mode_flags & DPT_MODE_MASK;
     if (!c || !v) return fail(DPT_E_ARG, "null ctx or vocab");
     // the armed histogram is this call's whatever happens below (one call only, failed ones included)
@@ -607,6 +607,8 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
     p.hist = hist;
     p.hist_bins = hist_bins;
     p.hist_overwrite = hist_overwrite;
+    p.ctr_snap = ctr_snap;
+    p.no_fallback = no_fallback;
     if (padded) {   // the ids go straight to their final place (int32), the counts to the caller's array
         p.staging = ids;
         p.staging16 = nullptr;
@@ -664,6 +666,38 @@ static int rerun_too_long(dpt_ctx *c, const dpt_vocab *v, int mode, const uint8_
                           const uint8_t *cut_mask, uint64_t n_str, int32_t *ids, uint64_t ids_cap, uint64_t *id_off,
                           int32_t *status, int32_t *capped_len);
 
+// Host path calls up to this many input bytes check whether any string needs the fallback passes.
+constexpr uint64_t NO_FALLBACK_CHECK_BYTES = 16384;
+
+// True when no string of a RAW / PRESPLIT call can leave the first pass (dpt_kernels.hip tokenize_kernel):
+// every word fits one 256-byte window (consecutive word starts -- byte 0, then ' ' in RAW mode or a cut
+// byte on a non-continuation byte in PRESPLIT mode -- at most 256 bytes apart, the last one at most 256
+// bytes before the string's end) and every atom (a code point: a byte and its continuation bytes) has at
+// most 4 bytes.  (Vocabularies with tokens of more than 64 code points are not checked: the caller.)
+static bool no_fallback_needed(int mode, const uint8_t *text, const uint64_t *str_off, const uint8_t *cut,
+                               uint64_t n_str) {
+    if (mode != DPT_MODE_RAW && mode != DPT_MODE_PRESPLIT) return false;
+    const uint64_t base = str_off[0];
+    for (uint64_t i = 0; i < n_str; i++) {
+        const uint64_t a = str_off[i] - base, b = str_off[i + 1] - base;
+        uint64_t ws = a;        // the current word's start
+        unsigned cont = 0;      // continuation bytes after the current atom's first byte
+        for (uint64_t k = a; k < b; k++) {
+            const uint8_t x = text[k];
+            const bool is_cont = k > a && (x & 0xC0) == 0x80;   // (the string's first byte starts an atom)
+            cont = is_cont ? cont + 1 : 0;
+            if (cont > 3) return false;   // an atom of over 4 bytes
+            const bool wstart = k > a && (mode == DPT_MODE_RAW ? x == ' ' : (cut[k] != 0 && !is_cont));
+            if (wstart) {
+                if (k - ws > 256) return false;
+                ws = k;
+            }
+        }
+        if (b - ws > 256) return false;
+    }
+    return true;
+}
+
 static int encode_host_impl(dpt_ctx *c, const dpt_vocab *v, int mode, const uint8_t *text, uint64_t n_bytes,
                             const uint64_t *str_off, const uint8_t *cut_mask, uint64_t n_str, int32_t *ids,
                             uint64_t ids_cap, uint64_t *id_off, int32_t *status, int32_t *capped_len,
@@ -711,19 +745,23 @@ static int encode_host_impl(dpt_ctx *c, const dpt_vocab *v, int mode, const uint
     uint64_t *d_edges = edges ? reinterpret_cast<uint64_t *>(c->d_out + o_edges) : nullptr;
     uint64_t *d_far = want_far ? reinterpret_cast<uint64_t *>(c->d_out + o_far) : nullptr;
     const uint64_t *p_idoff = reinterpret_cast<const uint64_t *>(c->p_out);
-    // small batches: everything in one copy (ids up to the n_bytes bound); large: the head, then the ids
+    // small batches: everything in one copy (ids up to the n_bytes bound); large: the head, then the ids.
+    // The counter block's first 64 bytes ride in d_out's counter slot (the finish pass's reset copies
+    // them there), so one copy brings them back.
     const bool one_copy = 4 * n_bytes <= (4ull << 20);
+    // Small calls skip the 2048-byte and unbounded passes' dispatches when no string can need them
+    // (no_fallback_needed): a per-string dp_tokenize call's launch chain loses two of its four kernels.
+    const bool no_fb = n_bytes <= NO_FALLBACK_CHECK_BYTES && !edges && v->stats.max_cp <= 64 &&
+                       no_fallback_needed(mode & DPT_MODE_MASK, text, str_off, cut ? cut_mask : nullptr, n_str);
     bool overflow = false;   // some strings got status 3 (arena full): they alone run again below
     for (int attempt = 0;; attempt++) {
         int rc = encode_impl(c, v, mode, c->d_in, n_bytes, reinterpret_cast<const uint64_t *>(c->d_in + o_off),
                              cut ? c->d_in + o_cut : nullptr, n_str, d_ids, n_bytes ? n_bytes : 1, d_idoff, d_status,
-                             d_capped, d_edges, st, d_far, far_cap);
+                             d_capped, d_edges, st, d_far, far_cap, nullptr, false,
+                             reinterpret_cast<uint64_t *>(c->d_out + o_ctr), no_fb);
         if (rc) return rc;
-        if ((e = hipMemcpyAsync(c->p_out, c->d_out, one_copy ? out_bytes : o_ctr, hipMemcpyDeviceToHost, st)) != hipSuccess)
+        if ((e = hipMemcpyAsync(c->p_out, c->d_out, one_copy ? out_bytes : o_ctr + COUNTER_BYTES, hipMemcpyDeviceToHost, st)) != hipSuccess)
             return hip_fail(e, "D2H");
-        // after the block copy, which spans the (unused) counter slot of d_out
-        if ((e = hipMemcpyAsync(c->p_out + o_ctr, c->retry_count, COUNTER_BYTES, hipMemcpyDeviceToHost, st)) != hipSuccess)
-            return hip_fail(e, "D2H counters");
         if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(e, "sync");
         uint64_t used = 0;
         if (n_str) memcpy(&used, c->p_out + o_ctr + 40, sizeof(used));   // the call's claimed bytes (finish_kernel)

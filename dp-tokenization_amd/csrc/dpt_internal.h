@@ -40,6 +40,8 @@ struct EncodeLaunch {
     uint64_t zero_n;             // ... (u64 entries)
     bool self_copy;              // the first pass copies its strings' ids into the CSR arrays (dpt_kernels.hip)
     uint2 *cq;                   // self-copy: per wave, CQ_CAP queued {string, count}
+    uint64_t *ctr_snap;          // nullable (host path): the counter block's first 64 bytes, copied here by its reset
+    bool no_fallback;            // the host checked that no string needs the 2048-byte or unbounded pass: skip them
     unsigned max_blocks;
     int variant;             // KERNEL_* below
     bool padded;             // dpt_encode_padded: staging = the caller's ids, counts = the caller's; no finish pass

@@ -2702,12 +2702,16 @@ __device__ __forceinline__ uint64_t block_incl_scan_add64(uint64_t v, uint64_t *
 
 // Reset the counter block for the next call (the claimed arena bytes and far pairs stay readable as
 // the call's "last need" / "last far").
-__device__ __forceinline__ void reset_counters(uint32_t *ctr) {
+// snap (nullable): the block's first 64 bytes as the host reads them after the call (the host path's
+// one device-to-host copy carries them, instead of a copy of the counter block of its own)
+__device__ __forceinline__ void reset_counters(uint32_t *ctr, uint64_t *snap = nullptr) {
     uint64_t *c64 = reinterpret_cast<uint64_t *>(ctr);
     c64[CTR_LASTNEED64] = c64[CTR_ARENA64];
     c64[CTR_ARENA64] = 0;
     c64[CTR_LASTFAR64] = c64[CTR_FAR64];
     c64[CTR_FAR64] = 0;
+    if (snap)
+        for (unsigned q = 0; q < 8; q++) snap[q] = c64[q];
     ctr[0] = 0; ctr[1] = 0; ctr[2] = 0; ctr[3] = 0; ctr[4] = 0; ctr[5] = 0; ctr[6] = 0;
     uint32_t *pc = ctr + PART_CTR_OFFSET / 4;
     for (unsigned q = 0; q <= NPART; q++) pc[q * PART_STRIDE] = 0;   // the partition counters and the mask
@@ -2722,7 +2726,8 @@ __device__ __forceinline__ void reset_counters(uint32_t *ctr) {
 // copy before its look-back, so each block took its batches one after another.
 __global__ void __launch_bounds__(SCAN_THREADS) batch_scan_kernel(uint64_t n_str, unsigned long long *bsum,
                                                                   unsigned long long *bpre, uint32_t *ctr,
-                                                                  unsigned long long *hist_zero, uint32_t n_hist) {
+                                                                  unsigned long long *hist_zero, uint32_t n_hist,
+                                                                  uint64_t *ctr_snap) {
     // DPT_HIST_OVERWRITE: the histogram the finish pass adds to starts from zero (stream order)
     if (hist_zero)
         for (uint32_t b = threadIdx.x; b < n_hist; b += SCAN_THREADS) hist_zero[b] = 0;
@@ -2741,7 +2746,7 @@ __global__ void __launch_bounds__(SCAN_THREADS) batch_scan_kernel(uint64_t n_str
         bsum[k] = 0;
         run += b;
     }
-    if (tid == 0) reset_counters(ctr);
+    if (tid == 0) reset_counters(ctr, ctr_snap);
 }
 
 struct FinishArgs {
@@ -2764,6 +2769,7 @@ struct FinishArgs {
     uint32_t n_bins;
     unsigned long long *inc;          // self-copy calls (finish_kernel<ST, true>): per batch SC_* flags + prefix
     const uint32_t *copied;           // ... and the strings the first pass copied into place
+    uint64_t *ctr_snap;               // nullable: the counter block's first 64 bytes before the reset (reset_counters)
 };
 
 // CSR offsets and ids: block b takes slice b % slices of batch b / slices.  One count per thread of
@@ -2875,7 +2881,7 @@ __global__ void __launch_bounds__(FIN_THREADS) finish_kernel(FinishArgs f) {
     if (SC && done) {   // the first pass wrote the batch's offsets and ids
         if (t == 0 && tid == 0 && sl == 0) {
             f.id_off[0] = 0;
-            reset_counters(f.ctr);
+            reset_counters(f.ctr, f.ctr_snap);
         }
         return;
     }
@@ -2886,7 +2892,7 @@ __global__ void __launch_bounds__(FIN_THREADS) finish_kernel(FinishArgs f) {
             f.id_off[0] = 0;
             // without the scan kernel: its other duties (every tokenize pass is done)
             if (f.bsum) f.bsum[0] = 0;   // one-batch call (fold calls zero the other array instead)
-            if (f.ctr) reset_counters(f.ctr);
+            if (f.ctr) reset_counters(f.ctr, f.ctr_snap);
         }
     }
     const uint64_t k_beg = total * sl / f.slices, k_end = total * (sl + 1) / f.slices;
@@ -3098,7 +3104,11 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
         // (n_units caps the grid: one block per FALLBACK_DIV CUs; the retry list is rare and short)
         uint64_t fb_units = (uint64_t)(p.max_blocks / 64) / FALLBACK_DIV;
         fb_units = fb_units < p.n_str ? fb_units : p.n_str;
-        if (wide) launch_tok<BIG_CH, 64, true, true>(b, tv, fb_units ? fb_units : 1, p.max_blocks / 64, stream);
+        // (skipped when the host showed no string needs them -- small host-path calls: two dispatches
+        // of a per-string dp_tokenize call -- unless they time the call or zero its histogram)
+        const bool fallback = !p.no_fallback || ev || b.hist_zero;
+        if (!fallback) {
+        } else if (wide) launch_tok<BIG_CH, 64, true, true>(b, tv, fb_units ? fb_units : 1, p.max_blocks / 64, stream);
         else if (raw) launch_tok<BIG_CH, 64, true, false, 0, true>(b, tv, fb_units ? fb_units : 1, p.max_blocks / 64, stream);
         else launch_tok<BIG_CH, 64, true, false>(b, tv, fb_units ? fb_units : 1, p.max_blocks / 64, stream);
         // the unbounded pass over whatever the windowed passes could not hold (usually nothing:
@@ -3116,7 +3126,7 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
         const uint64_t lcap = (uint64_t)(p.max_blocks / 16) / FALLBACK_DIV;
         const uint64_t lb = p.n_str < lcap ? p.n_str : lcap;
         l.blocks = (unsigned)(lb ? lb : 1);
-        launch_long(l, stream, ev ? ev[1] : nullptr);
+        if (fallback) launch_long(l, stream, ev ? ev[1] : nullptr);
     }
     if (p.padded) {   // dpt_encode_padded: the ids are in place; only the counters need their reset
         hipLaunchKernelGGL(reset_kernel, dim3(1), dim3(64), 0, stream, p.retry_count);
@@ -3127,7 +3137,7 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     const uint64_t nb = (p.n_str + FIN_BATCH - 1) / FIN_BATCH;
     FinishArgs f;
     f.bsum = nullptr; f.ctr = nullptr; f.fold = nullptr; f.fold_zero = nullptr; f.fold_n = 0;
-    f.inc = p.inc; f.copied = p.copied;
+    f.inc = p.inc; f.copied = p.copied; f.ctr_snap = p.ctr_snap;
     const bool sc = p.self_copy;
     const bool fold = !sc && fin_fold(p.n_str);
     const bool fold_hist = p.hist && p.hist_bins >= 2 && p.hist_bins <= FIN_MAX_BINS;
@@ -3138,7 +3148,7 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     unsigned long long *hz = (fold_hist && p.hist_overwrite && nb > 1 && !fold && !sc) ? f.hist : nullptr;
     if (fold || sc) { f.fold = p.flags; f.fold_zero = p.zero_other; f.fold_n = p.zero_n; f.ctr = p.retry_count; }
     else if (nb > 1) hipLaunchKernelGGL(batch_scan_kernel, dim3(1), dim3(SCAN_THREADS), 0, stream, p.n_str, p.flags, p.bpre, p.retry_count,
-                                        hz, p.hist_bins + 8u);
+                                        hz, p.hist_bins + 8u, p.ctr_snap);
     else { f.bsum = p.flags; f.ctr = p.retry_count; }
     f.staging = p.staging16 ? (const void *)p.staging16 : (const void *)p.staging;
     f.str_off = p.str_off; f.counts = p.counts; f.n_str = p.n_str; f.id_off = p.id_off; f.ids = p.ids;
