@@ -45,6 +45,9 @@
 #include <type_traits>
 
 #include "dpt_internal.h"
+// the unbounded pass (namespace dpt::lng): one translation unit with fallback_kernel, which runs it
+// in the same launch as the 2048-byte pass
+#include "dpt_long.hip"
 
 namespace dpt {
 
@@ -274,8 +277,15 @@ static_assert(sizeof(SlotState) == 48, "slot state layout");
 template <int CH, int G>
 constexpr int group_lds_bytes() { return (int)((sizeof(GroupLDS<CH, G>) + 15) & ~size_t(15)); }
 
+// A wave's LDS: per slot g its group's arrays, then its SlotState -- slot g at g * group_stride.  The
+// 16-lane kernel's stride (1856 B = 464 dwords, 16 mod 32) puts the two DPP rows of a 32-lane LDS lane group
+// (slots 0 / 1, 2 / 3) half a bank row apart: lane-mode B and C1 step through chunks 17 atoms apart, and
+// two slots 452 dwords apart (the arrays back to back, then the slot states) made most of those reads
+// 2-way bank conflicts; interleaved, the same bytes are conflict-free.
 template <int CH, int G>
-constexpr int block_lds_bytes() { return (64 / G) * (group_lds_bytes<CH, G>() + (int)sizeof(SlotState)); }
+constexpr int group_stride() { return group_lds_bytes<CH, G>() + (int)sizeof(SlotState); }
+template <int CH, int G>
+constexpr int block_lds_bytes() { return (64 / G) * group_stride<CH, G>(); }
 
 // ------------------------------------------------------------------ trie access
 
@@ -930,9 +940,11 @@ __device__ __noinline__ void sc_copy_run(ConstKernArgs *kp, unsigned qh, unsigne
 // SW: staged id width 0 = by a.staging16, 1 = int16, 2 = int32; RAW: DPT_MODE_RAW as a compile-time
 // constant (its expansions and word starts fold away in the other modes' code and vice versa -- the
 // 16-lane kernel sits at its register limit)
+// The body of tokenize_kernel (and of fallback_kernel's 2048-byte blocks); bid: the block's index
+// among the blocks running it.  The kernel arguments start with a KernArgs (read through the kernarg
+// segment pointer, KREFRESH).
 template <int CH, int G, bool BIG, bool WIDE, int SW = 0, bool RAW = false>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CH == 256 && G == 16) ? WPE16 : ((CH == 256 && G == 64) ? WPE64 : 1))))
-tokenize_kernel(KernArgs ka) {
+__device__ __forceinline__ void tokenize_body(const unsigned bid) {
     ConstKernArgs *kp = (ConstKernArgs *)__builtin_amdgcn_kernarg_segment_ptr();
 #define a (kp->ea)
 #define tv (tv_of(kp))
@@ -941,10 +953,11 @@ tokenize_kernel(KernArgs ka) {
     using GR = Group<G>;
     using M = typename GR::M;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    SlotState *const SS = reinterpret_cast<SlotState *>(smem + NG * group_lds_bytes<CH, G>());
-    auto grp = [&](unsigned g) -> GL & { return *reinterpret_cast<GL *>(smem + g * group_lds_bytes<CH, G>()); };
+    constexpr unsigned GSTR = (unsigned)group_stride<CH, G>();
+    auto SSr = [&](unsigned g) -> SlotState & { return *reinterpret_cast<SlotState *>(smem + g * GSTR + group_lds_bytes<CH, G>()); };
+    auto grp = [&](unsigned g) -> GL & { return *reinterpret_cast<GL *>(smem + g * GSTR); };
     auto wsl_of = [&](unsigned g) -> uint8_t * {
-        return GL::WSLG ? a.wsl_scratch + ((size_t)blockIdx.x * NG + g) * GL::WSL_STRIDE : nullptr;
+        return GL::WSLG ? a.wsl_scratch + ((size_t)bid * NG + g) * GL::WSL_STRIDE : nullptr;
     };
 
     const unsigned lane = lane_id();
@@ -952,7 +965,7 @@ tokenize_kernel(KernArgs ka) {
     const unsigned d = lane % G;         // my back distance - 1
     const uint64_t n_work = BIG ? (uint64_t)(*a.work_count) : a.n_str;
     if constexpr (BIG)
-        if (a.hist_zero && blockIdx.x == 0)
+        if (a.hist_zero && bid == 0)
             for (uint32_t b = lane; b < a.n_hist; b += 64u) a.hist_zero[b] = 0;
     if (BIG && n_work == 0) return;   // no retries: no counter traffic
     const uint64_t base_off = a.str_off[0];
@@ -975,7 +988,7 @@ tokenize_kernel(KernArgs ka) {
     // claimed ahead of a free slot: strings held in reserve by one wave left others idle at the end
     // of multi-window batches (cfg4 4.35 -> 4.56 ms with 4-string claims).
     const unsigned npart = BIG ? 1u : (unsigned)min((uint64_t)NPART, max((uint64_t)1, n_work / 4096u));
-    unsigned part = BIG ? 0u : blockIdx.x % npart;
+    unsigned part = BIG ? 0u : bid % npart;
     bool exhausted = false, claimed_all = false;
     unsigned n_pend = 0;   // 16-lane first pass: residual tokens waiting in the wave's pending row
     // one claim of up to req strings (uniform): partition-local [nb, ne) of partition cp, possibly
@@ -1019,7 +1032,7 @@ tokenize_kernel(KernArgs ka) {
     auto walk_pending = [&](unsigned P) {
         wave_sync();   // the entries other lanes stored
         if (lane < P) {
-            const uint4 e = a.pend[(uint64_t)blockIdx.x * 64u + lane];
+            const uint4 e = a.pend[(uint64_t)bid * 64u + lane];
             const uint64_t out = (uint64_t)e.x | ((uint64_t)(e.y & 0xFFFFu) << 32);
             const unsigned len = (e.y >> 16) & 0xFFu;
             const bool fi = raw && ((e.y >> 24) & 1u);
@@ -1058,12 +1071,12 @@ tokenize_kernel(KernArgs ka) {
 
     // ---- self-copy: see sc_ready / sc_copy_run above
     auto sc_step = [&]() -> unsigned {   // strings copied (uniform)
-        const unsigned qh = uni(SS[0].qh), qt = uni(SS[0].qt);
+        const unsigned qh = uni(SSr(0).qh), qt = uni(SSr(0).qt);
         const unsigned n = (qt - qh) & 0xFFu;
         if (!n) return 0;
         const unsigned npop = sc_ready(kp, qh, n, lane);
         if (npop == ~0u) {   // a string before them went to a later pass: the finish pass copies the queue's strings
-            if (lane == 0) SS[0].qh = (uint8_t)qt;
+            if (lane == 0) SSr(0).qh = (uint8_t)qt;
             return 0;
         }
         if (!npop) return 0;
@@ -1074,14 +1087,14 @@ tokenize_kernel(KernArgs ka) {
             }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's staging stores are out
         sc_copy_run(kp, qh, npop, lane, base_off, SW == 1 || (SW == 0 && a.staging16 != nullptr));
-        if (lane == 0) SS[0].qh = (uint8_t)(qh + npop);
+        if (lane == 0) SSr(0).qh = (uint8_t)(qh + npop);
         return npop;
     };
     auto st_agent = [](unsigned long long *p, unsigned long long v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
     STAMP_DECL
 
-    if (lane < (unsigned)NG) SS[lane].active = 0;
-    if (lane == 0) { SS[0].qh = 0; SS[0].qt = 0; }
+    if (lane < (unsigned)NG) SSr(lane).active = 0;
+    if (lane == 0) { SSr(0).qh = 0; SSr(0).qt = 0; }
     wave_sync();
 
     for (;;) {
@@ -1094,7 +1107,7 @@ tokenize_kernel(KernArgs ka) {
         for (;;) {
             unsigned need = 0;
 #pragma unroll
-            for (int g = 0; g < NG; g++) need |= uni(SS[g].active) ? 0u : (1u << g);
+            for (int g = 0; g < NG; g++) need |= uni(SSr(g).active) ? 0u : (1u << g);
             if (need && !exhausted) {
                 // claims until every free slot has a string or every partition is used up (a claim
                 // that reaches a partition's end may return fewer strings than asked)
@@ -1111,7 +1124,7 @@ tokenize_kernel(KernArgs ka) {
                             const uint64_t idx = nb + k;
                             const uint64_t s = BIG ? (uint64_t)a.work_list[idx] : part_string(npart, cp, (unsigned)idx);
                             const uint64_t o0 = a.str_off[s], o1 = a.str_off[s + 1];
-                            SlotState &S = SS[lane];
+                            SlotState &S = SSr(lane);
                             S.s = (uint32_t)s; S.sb = o0 - base_off; S.slen = (uint32_t)(o1 - o0); S.pos = 0; S.active = 1;
                             S.status = o1 == o0 ? 2u : 0u;  // pretokenize_raw('') == [[]] -> IndexError
                             S.ntok = 0; S.capsum = 0; S.abase = 0;
@@ -1124,21 +1137,21 @@ tokenize_kernel(KernArgs ka) {
             }
             unsigned todo = 0;
 #pragma unroll
-            for (int g = 0; g < NG; g++) todo |= (uni(SS[g].active) && !((prepared >> g) & 1u)) ? (1u << g) : 0u;
+            for (int g = 0; g < NG; g++) todo |= (uni(SSr(g).active) && !((prepared >> g) & 1u)) ? (1u << g) : 0u;
             if (!todo) break;
             WinRegs<CH> W[NG];
 #pragma unroll
             for (int g = 0; g < NG; g++) {
                 if (!((todo >> g) & 1u)) continue;
-                const uint64_t sb = uni64(SS[g].sb);
-                load_window<CH>(W[g], a.text + sb, raw ? nullptr : a.cut_mask + sb, uni64(SS[g].pos), uni64(SS[g].slen), raw, lane);
+                const uint64_t sb = uni64(SSr(g).sb);
+                load_window<CH>(W[g], a.text + sb, raw ? nullptr : a.cut_mask + sb, uni64(SSr(g).pos), uni64(SSr(g).slen), raw, lane);
             }
             bool refill = false;
 #pragma unroll
             for (int g = 0; g < NG; g++) {
                 if (!((todo >> g) & 1u)) continue;
                 GL &L = grp(g);
-                SlotState &S = SS[g];
+                SlotState &S = SSr(g);
                 const uint64_t slen = uni64(S.slen), pos = uni64(S.pos);
                 unsigned status = uni(S.status);
                 unsigned wlen = 0, na = 0, nw = 0;
@@ -1184,7 +1197,7 @@ tokenize_kernel(KernArgs ka) {
             wave_sync();
             if (!refill || exhausted) break;
         }
-        if (lane < (unsigned)NG && !((prepared >> lane) & 1u)) { SS[lane].n_atoms = 0; SS[lane].n_words = 0; SS[lane].capb = 0; }
+        if (lane < (unsigned)NG && !((prepared >> lane) & 1u)) { SSr(lane).n_atoms = 0; SSr(lane).n_words = 0; SSr(lane).capb = 0; }
         wave_sync();
         if (busy == 0) break;
         STAMP(0);
@@ -1204,7 +1217,7 @@ tokenize_kernel(KernArgs ka) {
                 if (raw) {
 #pragma unroll
                     for (int g = 0; g < NG; g++) {
-                        const unsigned wl = uni(SS[g].n_atoms) > 0 ? uni(SS[g].wlen) : 0u;
+                        const unsigned wl = uni(SSr(g).n_atoms) > 0 ? uni(SSr(g).wlen) : 0u;
                         const uint32_t *b32 = reinterpret_cast<const uint32_t *>(grp(g).bytes);
                         const uint32_t w0 = 4u * lane < wl ? b32[lane] : 0u;
                         const unsigned nv = wl > 4u * lane ? min(wl - 4u * lane, 4u) : 0u;   // valid bytes in w0
@@ -1215,10 +1228,10 @@ tokenize_kernel(KernArgs ka) {
             }
             unsigned nstart[NG];   // walker starts per slot: all atoms, or A0's marked ones
 #pragma unroll
-            for (int g = 0; g < NG; g++) nstart[g] = uni(SS[g].n_atoms);
+            for (int g = 0; g < NG; g++) nstart[g] = uni(SSr(g).n_atoms);
             unsigned fwmask = 0;   // slots whose window starts the string (raw: '▁' + first atom)
 #pragma unroll
-            for (int g = 0; g < NG; g++) fwmask |= (uni(SS[g].pos) == 0 ? 1u : 0u) << g;
+            for (int g = 0; g < NG; g++) fwmask |= (uni(SSr(g).pos) == 0 ? 1u : 0u) << g;
             // One walk per lane.  Walk state: start atom j, the LDS byte offset of its slot's group,
             // atoms matched so far (len), the trie node, the expanded bytes left of the current atom
             // (seq, cnt) and its descriptor (info).  Finished walks take the next start (ballot +
@@ -1245,7 +1258,7 @@ tokenize_kernel(KernArgs ka) {
             auto start_gj = [&](unsigned gs, unsigned jj) {
                 j = jj;
                 gsel = gs;
-                lbase = gs * (unsigned)group_lds_bytes<CH, G>();
+                lbase = gs * GSTR;
                 const GL &L = *reinterpret_cast<const GL *>(smem + lbase);
                 info = ainfo_get(L, j, raw && ((fwmask >> gs) & 1u));
                 seq = atom_from_info<CH, WIDE>(L.bytes, info, raw, cnt);
@@ -1276,9 +1289,9 @@ tokenize_kernel(KernArgs ka) {
 #pragma unroll
                     for (int g = 0; g < NG; g++) {
                         if (!((a0mask >> g) & 1u)) continue;
-                        const unsigned wl = uni(SS[g].wlen);
-                        const bool first = uni(SS[g].pos) == 0;
-                        const unsigned gbase = (unsigned)g * (unsigned)group_lds_bytes<CH, G>();
+                        const unsigned wl = uni(SSr(g).wlen);
+                        const bool first = uni(SSr(g).pos) == 0;
+                        const unsigned gbase = (unsigned)g * GSTR;
                         const uint32_t *b32 = reinterpret_cast<const uint32_t *>(grp(g).bytes);
                         const unsigned k0 = 4u * lane;
                         // bytes k0 .. k0+7 (past the window: masked by wl below)
@@ -1338,7 +1351,7 @@ tokenize_kernel(KernArgs ka) {
                                 __hip_atomic_fetch_and(&r32[k0 + 1u + u], ~((((tk1 >> u) & 1u) << 16) | (((t2e >> u) & 1u) << 17)),
                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         }
-                        if (ballot(nocap) && lane == 0) SS[g].capb = 1;
+                        if (ballot(nocap) && lane == 0) SSr(g).capb = 1;
                         // the slot's marked atoms, in order, into its fin[] (free until phase B)
                         const unsigned mg = (mark >> (4 * g)) & 15u;
                         const unsigned c = (unsigned)__builtin_popcount(mg);
@@ -1388,11 +1401,11 @@ tokenize_kernel(KernArgs ka) {
 #pragma unroll
                         for (int g = 0; g < NG; g++) base = (gs == (unsigned)g) ? fpre[g] : base;
                         fgs = gs;
-                        fl = gs * (unsigned)group_lds_bytes<CH, G>();
+                        fl = gs * GSTR;
                         const GL &L = *reinterpret_cast<const GL *>(smem + fl);
                         const unsigned jj = L.fin[uu - base].v;
                         fj = jj;
-                        fwl = SS[gs].wlen;
+                        fwl = SSr(gs).wlen;
                         const unsigned b0 = L.bytes[jj];
                         isr = 0; one = 0; pc = 0;
                         if (((fwmask >> gs) & 1u) && jj == 0) {   // '\u2581' + b0: one atom
@@ -1593,7 +1606,7 @@ tokenize_kernel(KernArgs ka) {
             // the slots whose walk found an atom that is no token by itself
 #pragma unroll
             for (int g = 0; g < NG; g++)
-                if (ballot((capm >> g) & 1u) && lane == 0) SS[g].capb = 1;
+                if (ballot((capm >> g) & 1u) && lane == 0) SSr(g).capb = 1;
         }
         wave_sync();
         STAMP(1);
@@ -1603,10 +1616,10 @@ tokenize_kernel(KernArgs ka) {
         bool lane_mode = false;   // B ran per chunk and did C0 and C1 itself (G = 16, capless, no edges)
         if (DPT_RUN_B) {
             GL &L = grp(mg);
-            const unsigned na = SS[mg].n_atoms;
+            const unsigned na = SSr(mg).n_atoms;
             unsigned imax = 0;
 #pragma unroll
-            for (int g = 0; g < NG; g++) imax = max(imax, uni(SS[g].n_atoms));
+            for (int g = 0; g < NG; g++) imax = max(imax, uni(SSr(g).n_atoms));
             // Steps past a slot's own n_atoms (up to the wave's imax <= CH) compute garbage that
             // lands in fin[] entries nobody reads, so the loop body has no per-slot guard.
             // Recording the edges (f1) and the uncapped DP (f2) are hoisted out as loop versions.
@@ -1659,7 +1672,7 @@ tokenize_kernel(KernArgs ka) {
                             L.fin[i].v = (uint8_t)(dg | (de << 4));
                             L.rec[i].smask = Wfin<G>::pack(r);   // rec[i] was consumed at step i-1
                             if constexpr (edges)
-                                if (i <= na) a.edges[SS[mg].sb + SS[mg].abase + i - 1] = es & 0xFFFFu;
+                                if (i <= na) a.edges[SSr(mg).sb + SSr(mg).abase + i - 1] = es & 0xFFFFu;
                         }
                         const bool wend = (int16_t)cur < 0;     // CP_WS: word starts and the window end
                         wsh = wend ? (i << 16) : wsh;
@@ -1700,7 +1713,7 @@ tokenize_kernel(KernArgs ka) {
                             L.fin[i].d = dg | (de << 8);
                             L.fin[i].w = Wfin<G>::pack(r);
                             if constexpr (edges)
-                                if (i <= na) a.edges[SS[0].sb + SS[0].abase + i - 1] = emb;
+                                if (i <= na) a.edges[SSr(0).sb + SSr(0).abase + i - 1] = emb;
                         }
                         const bool wend = (cur & CP_WS) != 0;
                         ws = wend ? i : ws;
@@ -1871,7 +1884,7 @@ tokenize_kernel(KernArgs ka) {
                 tb += (unsigned)__builtin_amdgcn_update_dpp(0, (int)tb, 0x112, 0xF, 0xF, false);
                 tb += (unsigned)__builtin_amdgcn_update_dpp(0, (int)tb, 0x114, 0xF, 0xF, false);
                 tb += (unsigned)__builtin_amdgcn_update_dpp(0, (int)tb, 0x118, 0xF, 0xF, false);
-                if (d == 15) SS[mg].wtok = tb;
+                if (d == 15) SSr(mg).wtok = tb;
                 tb -= T;
                 // P1's L*: from rec[re] when its word ends at re, else from the right (the first
                 // word end of the next chunk that has one)
@@ -1884,7 +1897,7 @@ tokenize_kernel(KernArgs ka) {
                 // (DPP reads outside any branch: a lane masked off in EXEC reads as 0)
                 const unsigned lsn = (unsigned)__builtin_amdgcn_update_dpp(0, (int)lsr, 0x101, 0xF, 0xF, false);
                 const unsigned ls1 = re_ws ? gre : (lsn & 15u) + 1u;
-                const bool walk = !len_only && SS[mg].status == 0;   // per row (not uniform)
+                const bool walk = !len_only && SSr(mg).status == 0;   // per row (not uniform)
                 const bool left_of_q = gre < ls1;
                 unsigned n1 = 0;   // tokens of P1
                 unsigned afin = 0, lsm = ls1;   // after the walk: A and L* of the last piece
@@ -2081,7 +2094,7 @@ tokenize_kernel(KernArgs ka) {
             using C2_ = std::integral_constant<int, 2>;
             unsigned capb = 0;
 #pragma unroll
-            for (int g = 0; g < NG; g++) capb |= uni(SS[g].capb);
+            for (int g = 0; g < NG; g++) capb |= uni(SSr(g).capb);
             if (a.edges) {
                 if (!capb) forward(T_{}, C2_{}); else if (uncapped) forward(T_{}, C1_{}); else forward(T_{}, C0_{});
             } else {
@@ -2109,7 +2122,7 @@ tokenize_kernel(KernArgs ka) {
                 // the word list (word -> first atom, then the window end) from the word-start bits
 #pragma unroll
                 for (int g = 0; g < NG; g++) {
-                    const unsigned na = uni(SS[g].n_atoms);
+                    const unsigned na = uni(SSr(g).n_atoms);
                     if (na == 0) continue;
                     const GL &L = grp(g);
                     uint8_t *gw = wsl_of(g);
@@ -2126,7 +2139,7 @@ tokenize_kernel(KernArgs ka) {
             unsigned pre[NG + 1];
             pre[0] = 0;
 #pragma unroll
-            for (int g = 0; g < NG; g++) pre[g + 1] = pre[g] + (uni(SS[g].n_atoms) > 0 ? uni(SS[g].n_words) : 0u);
+            for (int g = 0; g < NG; g++) pre[g + 1] = pre[g] + (uni(SSr(g).n_atoms) > 0 ? uni(SSr(g).n_words) : 0u);
             const unsigned total = pre[NG];
             for (unsigned u0 = 0; u0 < total; u0 += 64) {
                 const unsigned u = u0 + lane;
@@ -2156,7 +2169,7 @@ tokenize_kernel(KernArgs ka) {
                     const unsigned cs = wave_incl_scan_add(mine ? cost : 0u);
                     const unsigned csum = __builtin_amdgcn_readlane(cs, 63);
                     const unsigned anyinv = (ballot(mine && inv) != 0 ? 1u : 0u) | (ballot(mine && lng) != 0 ? 2u : 0u);
-                    if (lane == 0) { SS[k].wtok += csum; SS[k].inval |= anyinv; }
+                    if (lane == 0) { SSr(k).wtok += csum; SSr(k).inval |= anyinv; }
                 }
             }
         }
@@ -2169,10 +2182,10 @@ tokenize_kernel(KernArgs ka) {
             pre[0] = 0; tokpre[0] = 0;
 #pragma unroll
             for (int g = 0; g < NG; g++) {
-                const unsigned nwg = uni(SS[g].n_atoms) > 0 ? uni(SS[g].n_words) : 0u;
-                inv_g[g] = uni(SS[g].inval) | (uni(SS[g].status) != 0 ? 1u : 0u);
+                const unsigned nwg = uni(SSr(g).n_atoms) > 0 ? uni(SSr(g).n_words) : 0u;
+                inv_g[g] = uni(SSr(g).inval) | (uni(SSr(g).status) != 0 ? 1u : 0u);
                 pre[g + 1] = pre[g] + nwg;
-                tokpre[g + 1] = tokpre[g] + (nwg ? uni(SS[g].wtok) : 0u);
+                tokpre[g + 1] = tokpre[g] + (nwg ? uni(SSr(g).wtok) : 0u);
             }
             const unsigned total = pre[NG];
             unsigned carry = 0;
@@ -2228,11 +2241,11 @@ tokenize_kernel(KernArgs ka) {
             pre[0] = 0;
 #pragma unroll
             for (int g = 0; g < NG; g++) {
-                const bool gv = !len_only && uni(SS[g].inval) == 0 && uni(SS[g].status) == 0 && uni(SS[g].n_atoms) > 0;
-                pre[g + 1] = pre[g] + (gv ? uni(SS[g].wtok) : 0u);
-                na_g[g] = uni(SS[g].n_atoms);
-                firstmask |= (uni64(SS[g].pos) == 0 ? 1u : 0u) << g;
-                const uint64_t e0 = uni64(SS[g].sb) + uni(SS[g].ntok);
+                const bool gv = !len_only && uni(SSr(g).inval) == 0 && uni(SSr(g).status) == 0 && uni(SSr(g).n_atoms) > 0;
+                pre[g + 1] = pre[g] + (gv ? uni(SSr(g).wtok) : 0u);
+                na_g[g] = uni(SSr(g).n_atoms);
+                firstmask |= (uni64(SSr(g).pos) == 0 ? 1u : 0u) << g;
+                const uint64_t e0 = uni64(SSr(g).sb) + uni(SSr(g).ntok);
                 obase[g] = e0;
             }
             const unsigned total = pre[NG];
@@ -2269,7 +2282,7 @@ tokenize_kernel(KernArgs ka) {
             // entry i in group i / 256's rec[i % 256]; G = 64 (one slot): rec[i]
             auto list_ref = [&](unsigned i) -> uint16_t & {
                 if constexpr (G == 16)
-                    return *reinterpret_cast<uint16_t *>(smem + (i >> 8) * (unsigned)group_lds_bytes<CH, G>() + (i & 255u) * 4u);
+                    return *reinterpret_cast<uint16_t *>(smem + (i >> 8) * GSTR + (i & 255u) * 4u);
                 else
                     return grp(0).rec[i].cpos;
             };
@@ -2302,7 +2315,7 @@ tokenize_kernel(KernArgs ka) {
                         unsigned g = 0;
 #pragma unroll
                         for (int k = 1; k < NG; k++) g += t >= pre[k] ? 1u : 0u;
-                        const GL &L = *reinterpret_cast<const GL *>(smem + g * (unsigned)group_lds_bytes<CH, G>());
+                        const GL &L = *reinterpret_cast<const GL *>(smem + g * GSTR);
                         const C2Slot q = *reinterpret_cast<const C2Slot *>(&L.fin[0]);
                         const unsigned k = in ? t - q.base : 0u;
                         const unsigned jj = (unsigned)L.rec[k].smask;
@@ -2379,7 +2392,7 @@ tokenize_kernel(KernArgs ka) {
                         unsigned g = 0;
 #pragma unroll
                         for (int k = 1; k < NG; k++) g += t >= pre[k] ? 1u : 0u;
-                        const GL &L = *reinterpret_cast<const GL *>(smem + g * (unsigned)group_lds_bytes<CH, G>());
+                        const GL &L = *reinterpret_cast<const GL *>(smem + g * GSTR);
                         const C2Slot q = *reinterpret_cast<const C2Slot *>(&L.fin[0]);
                         const unsigned k = in ? t - q.base : 0u;
                         const unsigned jj = (unsigned)L.rec[k].smask;
@@ -2453,7 +2466,7 @@ tokenize_kernel(KernArgs ka) {
                         unsigned g = 0;
 #pragma unroll
                         for (int k = 1; k < NG; k++) g += t >= pre[k] ? 1u : 0u;
-                        const GL &L = *reinterpret_cast<const GL *>(smem + g * (unsigned)group_lds_bytes<CH, G>());
+                        const GL &L = *reinterpret_cast<const GL *>(smem + g * GSTR);
                         const C2Slot q = *reinterpret_cast<const C2Slot *>(&L.fin[0]);
                         const unsigned k = t - q.base;
                         const unsigned jj = (unsigned)L.rec[k].smask;
@@ -2472,7 +2485,7 @@ tokenize_kernel(KernArgs ka) {
                             walk_pending(n_pend);
                             n_pend = 0;
                         }
-                        if (lane < r) a.pend[(uint64_t)blockIdx.x * 64u + n_pend + lane] = ent;
+                        if (lane < r) a.pend[(uint64_t)bid * 64u + n_pend + lane] = ent;
                         n_pend += r;
                         wend = 0;
                     }
@@ -2500,7 +2513,7 @@ tokenize_kernel(KernArgs ka) {
                 unsigned g = 0;
 #pragma unroll
                 for (int k = 1; k < NG; k++) g += t >= pre[k] ? 1u : 0u;
-                T.lbase = g * (unsigned)group_lds_bytes<CH, G>();
+                T.lbase = g * GSTR;
                 const GL &L = *reinterpret_cast<const GL *>(smem + T.lbase);
                 const C2Slot q = *reinterpret_cast<const C2Slot *>(&L.fin[0]);
                 const unsigned k = t - q.base;
@@ -2581,7 +2594,7 @@ tokenize_kernel(KernArgs ka) {
         bool fq = false;            // self-copy: a string with ids finished here (queued below)
         unsigned fq_s = 0, fq_n = 0;
         if (lane < (unsigned)NG) {
-            SlotState &S = SS[lane];
+            SlotState &S = SSr(lane);
             if (S.active && S.n_atoms > 0 && S.status == 0 && (S.inval & 2)) {
                 // a word of more than G atoms while the vocabulary has longer tokens: the
                 // unbounded pass redoes the whole string (and writes its status and count)
@@ -2626,12 +2639,12 @@ tokenize_kernel(KernArgs ka) {
             // then one step of the queue
             const uint64_t fm = ballot(fq);
             if (fm) {
-                const unsigned qh = uni(SS[0].qh), qt = uni(SS[0].qt);
+                const unsigned qh = uni(SSr(0).qh), qt = uni(SSr(0).qt);
                 const unsigned room = CQ_CAP - ((qt - qh) & 0xFFu);
                 const unsigned rk = __builtin_amdgcn_mbcnt_hi((unsigned)(fm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)fm, 0u));
-                if (fq && rk < room) a.cq[(size_t)blockIdx.x * CQ_CAP + ((qt + rk) % CQ_CAP)] = make_uint2(fq_s, fq_n);
+                if (fq && rk < room) a.cq[(size_t)bid * CQ_CAP + ((qt + rk) % CQ_CAP)] = make_uint2(fq_s, fq_n);
                 const unsigned nq = (unsigned)__builtin_popcountll(fm);
-                if (lane == 0) SS[0].qt = (uint8_t)(qt + (nq < room ? nq : room));
+                if (lane == 0) SSr(0).qt = (uint8_t)(qt + (nq < room ? nq : room));
                 wave_sync();
             }
             (void)sc_step();
@@ -2648,7 +2661,7 @@ tokenize_kernel(KernArgs ka) {
         // the queue's last strings: their batches complete as the other waves finish (every string is
         // claimed by now, by running waves); bounded -- what is left stays for the finish pass
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (uni(SS[0].qh) != uni(SS[0].qt)) {
+        while (uni(SSr(0).qh) != uni(SSr(0).qt)) {
             if (sc_step()) {
                 wave_sync();
                 continue;
@@ -2660,6 +2673,12 @@ tokenize_kernel(KernArgs ka) {
     STAMP_FLUSH;
 #undef a
 #undef tv
+}
+
+template <int CH, int G, bool BIG, bool WIDE, int SW = 0, bool RAW = false>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CH == 256 && G == 16) ? WPE16 : ((CH == 256 && G == 64) ? WPE64 : 1))))
+tokenize_kernel(KernArgs ka) {
+    tokenize_body<CH, G, BIG, WIDE, SW, RAW>(blockIdx.x);
 }
 
 // ------------------------------------------------------------------ compaction
@@ -2977,10 +2996,55 @@ __global__ void __launch_bounds__(HIST_THREADS) hist_kernel(const uint64_t *__re
         if (lh[b]) atomicAdd(&hist[b], lh[b]);
 }
 
+// ------------------------------------------------------------------ the fallback passes in one launch
+
+constexpr int SMALL_CH = 256;   // the first pass's window
+constexpr int BIG_CH = 2048;    // the 2048-byte pass's
+
+// The 2048-byte pass and the unbounded pass as ONE launch (they used to be two, ~5 us each on every call
+// although their lists are usually empty).  Each block takes a ticket: the first n_big tickets run the
+// 2048-byte pass (tokenize_body), the others the unbounded pass (lng::long_body) once every 2048-byte
+// block has finished -- that pass appends to the unbounded pass's list.  The blocks a ticket makes wait
+// wait only for blocks that hold earlier tickets, so are running (no dispatch-order assumption).  The
+// list's entries are published like any inter-workgroup hand-off on MI355X (per-XCD L2s): an agent-scope
+// release by each 2048-byte block that stored any, a relaxed done counter, one acquire on the other side.
+struct FallbackArgs {
+    KernArgs k;              // first: tokenize_body reads it through the kernarg segment pointer
+    lng::Args l;
+    uint32_t *ticket, *big_done;   // counter block uint32 [6] / [1] (reset_counters zeroes them)
+    unsigned n_big;
+};
+
+template <bool WIDE, bool RAW>
+__global__ void __launch_bounds__(64) fallback_kernel(FallbackArgs fa) {
+    const unsigned lane = lane_id();
+    unsigned t = 0;
+    if (lane == 0) t = atomicAdd(fa.ticket, 1u);
+    t = __builtin_amdgcn_readfirstlane(t);
+    if (t < fa.n_big) {
+        const bool work = *fa.k.ea.work_count != 0;
+        tokenize_body<BIG_CH, 64, true, WIDE, 0, RAW>(t);
+        if (work) {   // (long-list entries may have been stored)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        if (lane == 0) atomicAdd(fa.big_done, 1u);
+        return;
+    }
+    // the unbounded pass, after every 2048-byte block (bounded: they are running; 2 s at 100 MHz)
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(fa.big_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < fa.n_big) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) break;   // (never expected; results then stale)
+        __builtin_amdgcn_s_sleep(4);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    lng::long_body(fa.l);
+}
+
 // ------------------------------------------------------------------ launchers
 
-constexpr int SMALL_CH = 256;
-constexpr int BIG_CH = 2048;
+
 
 static_assert(block_lds_bytes<SMALL_CH, 16>() <= 64 * 1024, "small LDS");
 static_assert(block_lds_bytes<SMALL_CH, 64>() <= 64 * 1024, "small LDS");
@@ -3107,10 +3171,6 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
         // (skipped when the host showed no string needs them -- small host-path calls: two dispatches
         // of a per-string dp_tokenize call -- unless they time the call or zero its histogram)
         const bool fallback = !p.no_fallback || ev || b.hist_zero;
-        if (!fallback) {
-        } else if (wide) launch_tok<BIG_CH, 64, true, true>(b, tv, fb_units ? fb_units : 1, p.max_blocks / 64, stream);
-        else if (raw) launch_tok<BIG_CH, 64, true, false, 0, true>(b, tv, fb_units ? fb_units : 1, p.max_blocks / 64, stream);
-        else launch_tok<BIG_CH, 64, true, false>(b, tv, fb_units ? fb_units : 1, p.max_blocks / 64, stream);
         // the unbounded pass over whatever the windowed passes could not hold (usually nothing:
         // its waves read a zero count and exit)
         LongLaunch l;
@@ -3126,7 +3186,23 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
         const uint64_t lcap = (uint64_t)(p.max_blocks / 16) / FALLBACK_DIV;
         const uint64_t lb = p.n_str < lcap ? p.n_str : lcap;
         l.blocks = (unsigned)(lb ? lb : 1);
-        if (fallback) launch_long(l, stream, ev ? ev[1] : nullptr);
+        if (fallback) {   // both passes, one launch (fallback_kernel); the end timestamp rides on it
+            FallbackArgs fa;
+            fa.k = KernArgs{b, tv};
+            fa.l = lng::long_args(l);
+            fa.ticket = p.retry_count + 6;
+            fa.big_done = p.retry_count + 1;
+            fa.n_big = (unsigned)(fb_units ? fb_units : 1);
+            const dim3 grid(fa.n_big + l.blocks);
+            constexpr int lds = block_lds_bytes<BIG_CH, 64>();
+            auto go = [&](auto kern) {
+                if (ev) hipExtLaunchKernelGGL(kern, grid, dim3(64), lds, stream, nullptr, ev[1], 0, fa);
+                else hipLaunchKernelGGL(kern, grid, dim3(64), lds, stream, fa);
+            };
+            if (wide) go(fallback_kernel<true, false>);
+            else if (raw) go(fallback_kernel<false, true>);
+            else go(fallback_kernel<false, false>);
+        }
     }
     if (p.padded) {   // dpt_encode_padded: the ids are in place; only the counters need their reset
         hipLaunchKernelGGL(reset_kernel, dim3(1), dim3(64), 0, stream, p.retry_count);
@@ -3206,6 +3282,9 @@ hipError_t kernel_init() {
     if (e == hipSuccess)
         e = hipFuncSetAttribute(reinterpret_cast<const void *>(&tokenize_kernel<BIG_CH, 64, true, true>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, block_lds_bytes<BIG_CH, 64>());
+    for (const void *k : {reinterpret_cast<const void *>(&fallback_kernel<true, false>), reinterpret_cast<const void *>(&fallback_kernel<false, true>),
+                          reinterpret_cast<const void *>(&fallback_kernel<false, false>)})
+        if (e == hipSuccess) e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, block_lds_bytes<BIG_CH, 64>());
     if (e == hipSuccess) done[dev] = true;
     return e;
 }

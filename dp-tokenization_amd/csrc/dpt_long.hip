@@ -196,7 +196,8 @@ __device__ bool span_is_token(const Args &a, const Str &S, unsigned j, unsigned 
     return false;
 }
 
-__global__ void __launch_bounds__(64) long_kernel(Args a) {
+// (the body of long_kernel and of dpt_kernels.hip fallback_kernel's unbounded-pass blocks)
+__device__ __forceinline__ void long_body(const Args &a) {
     const unsigned lane = lane_id();
     const int mode = a.mode & DPT_MODE_MASK;
     const bool raw = mode == DPT_MODE_RAW;
@@ -553,10 +554,11 @@ __global__ void __launch_bounds__(64) long_kernel(Args a) {
     }
 }
 
-}  // namespace lng
+__global__ void __launch_bounds__(64) long_kernel(Args a) { long_body(a); }
 
-void launch_long(const LongLaunch &p, hipStream_t stream, hipEvent_t ev_stop) {
-    lng::Args a;
+// launch_long's arguments from a LongLaunch
+inline Args long_args(const LongLaunch &p) {
+    Args a;
     a.text = p.text; a.str_off = p.str_off; a.cut_mask = p.cut_mask;
     a.staging = p.staging; a.staging16 = p.staging16; a.counts = p.counts; a.bsum = p.bsum; a.status = p.status; a.capped = p.capped;
     a.rec = reinterpret_cast<uint4 *>(p.arena);
@@ -566,6 +568,13 @@ void launch_long(const LongLaunch &p, hipStream_t stream, hipEvent_t ev_stop) {
     a.edges = p.edges; a.far = p.far; a.far_cap = p.far_cap; a.far_count = p.far_count; a.list = p.list; a.list_count = p.list_count; a.work_next = p.work_next;
     a.slots = p.slots; a.slots4 = p.slots4; a.n_slots = p.n_slots; a.root_base = p.root_base;
     a.max_tok_bytes = p.max_tok_bytes; a.long_span = p.long_span; a.mode = p.mode;
+    return a;
+}
+
+}  // namespace lng
+
+void launch_long(const LongLaunch &p, hipStream_t stream, hipEvent_t ev_stop) {
+    const lng::Args a = lng::long_args(p);
     if (ev_stop)   // the end timestamp of the tokenize passes rides on this dispatch (dpt_ctx_profile)
         hipExtLaunchKernelGGL(lng::long_kernel, dim3(p.blocks), dim3(64), 0, stream, nullptr, ev_stop, 0, a);
     else

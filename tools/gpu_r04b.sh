@@ -6,8 +6,10 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 out=gpurun_out/r04b; mkdir -p $out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_selfcopy.py tests/test_gpu_fold.py -x -v -s --timeout 200 --timeout-method thread > $out/pytest_sc.txt 2>&1 || { tail -40 $out/pytest_sc.txt; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_gpu_selfcopy.py tests/test_gpu_fold.py tests/test_gpu_hostpath.py -x -v -s --timeout 200 --timeout-method thread > $out/pytest_sc.txt 2>&1 || { tail -40 $out/pytest_sc.txt; exit 1; }
 tail -3 $out/pytest_sc.txt
+timeout -k 10 300 python tools/percall.py 2000 > $out/percall.json 2>&1 || { tail -5 $out/percall.json; exit 1; }
+cat $out/percall.json
 for r in 1 2; do
   for sc in 0 1; do
     for args in "--workload cfg2" "--workload cfg2 --strings 125000" "--workload cfg4"; do
