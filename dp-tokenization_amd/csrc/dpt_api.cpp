@@ -52,7 +52,8 @@ struct dpt_ctx {
     unsigned long long *flags = nullptr;
     uint64_t cap_batches = 0;
     int flag_parity = 0;
-    uint2 *cq = nullptr;              // self-copy queues (dpt::cq_scratch_bytes)
+    uint4 *cq = nullptr;              // self-copy queues (dpt::cq_scratch_bytes)
+    uint32_t sc_epoch = 0;            // self-copy calls so far: each call's counts carry the next value
     unsigned long long *last_sc = nullptr;   // the last call's region when it self-copied (dpt_ctx_copy_stats) ...
     uint64_t last_sc_nb = 0;                 // ... and its batches
     unsigned max_blocks = 0;
@@ -593,6 +594,8 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
         p.cq = c->cq;
         // self-copy: CSR calls of enough batches without edge outputs or length-only DPs
         const char *sce = getenv("DPT_SELF_COPY");   // (A/B switch: "0" = off; read per call)
+        if (++c->sc_epoch == 0) c->sc_epoch = 1;   // (a count of the previous call never matches)
+        p.sc_epoch = c->sc_epoch;
         p.self_copy = !(sce && !strcmp(sce, "0")) && !padded && !edges && !(mode_flags & (DPT_FLAG_UNCAPPED | DPT_FLAG_LEN_ONLY)) &&
                       (n_str + dpt::FIN_BATCH - 1) / dpt::FIN_BATCH >= dpt::SC_MIN_BATCHES;
     }

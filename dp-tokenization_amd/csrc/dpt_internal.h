@@ -39,7 +39,8 @@ struct EncodeLaunch {
     unsigned long long *zero_other;   // fold / self-copy calls: the other parity's region, zeroed for the next call ...
     uint64_t zero_n;             // ... (u64 entries)
     bool self_copy;              // the first pass copies its strings' ids into the CSR arrays (dpt_kernels.hip)
-    uint2 *cq;                   // self-copy: per wave, CQ_CAP queued {string, count}
+    uint4 *cq;                   // self-copy: per wave, CQ_CAP queued {string, count, staging element}
+    uint32_t sc_epoch;           // self-copy: the call's tag for its counts (never 0)
     uint64_t *ctr_snap;          // nullable (host path): the counter block's first 64 bytes, copied here by its reset
     bool no_fallback;            // the host checked that no string needs the 2048-byte or unbounded pass: skip them
     unsigned max_blocks;
@@ -96,6 +97,7 @@ constexpr unsigned long long BS_SUM_MASK = (1ull << BS_FIN_SHIFT) - 1;
 constexpr unsigned long long SC_PUB = 1ull << 63, SC_CLAIM = 1ull << 62, SC_OFS = 1ull << 61;
 constexpr unsigned long long SC_VAL_MASK = (1ull << 56) - 1;
 constexpr unsigned CQ_CAP = 32;            // strings a wave's copy queue holds
+constexpr unsigned SC_MIN_QUEUE = 8;       // queued strings before a copy step (a step costs round trips)
 constexpr uint64_t SC_MIN_BATCHES = 8;     // calls of fewer batches take the finish pass's copy alone
 constexpr size_t PART_CTR_OFFSET = 256;
 constexpr size_t CTR_ALLOC_BYTES = PART_CTR_OFFSET + (NPART_MAX + 1) * PART_STRIDE * 4;

@@ -357,7 +357,9 @@ struct EncodeArgs {
     // self-copy (first pass of CSR calls; inc == nullptr: off): see sc_step in tokenize_kernel
     unsigned long long *inc;    // per batch: SC_PUB | SC_CLAIM | SC_OFS | inclusive id prefix
     uint32_t *copied;           // per batch: strings copied into place
-    uint2 *cq;                  // per wave: CQ_CAP queued {string, count} (ring; head / tail in SS[0].qh / qt)
+    uint4 *cq;                  // per wave: CQ_CAP queued {string, count, staging element lo, hi} (ring; head / tail in
+                                //   slot 0's SlotState qh / qt)
+    uint32_t sc_epoch;          // the tag of this call's counts (sc_publish_at); never 0
     uint32_t *route_c;          // ~(first batch holding a string routed to a later pass), 0: none (atomicMax)
     uint64_t *id_off;
     int32_t *ids;
@@ -793,17 +795,18 @@ __device__ __forceinline__ TrieView tv_of(ConstKernArgs *kp) {
 // known: the string waits in the wave's copy queue (a.cq, CQ_CAP entries) until its FIN_BATCH-string
 // batch is complete and the ids of every earlier batch are counted, which happens about a round
 // later since the partitions advance through the batch side by side.  Cross-wave data goes through
-// agent-scope atomics only (MI355X: per-XCD L2s are not coherent; no release fence is needed):
-//   * a finishing string stores its count (ld_agent / st_agent: sc1) and, after the store drained,
-//     adds 1 << BS_FIN_SHIFT | count to its batch sum (a routed string adds 1 << BS_ROUTE_SHIFT);
-//   * the first wave that finds a batch complete and the id prefix before it computable -- the
-//     nearest published prefix back plus the sums of the complete batches after it (a decoupled
-//     look-back) -- claims it (atomicOr SC_PUB | SC_CLAIM | inclusive prefix), writes the batch's
-//     id_off entries from its strings' counts, drains, and sets SC_OFS;
+// agent-scope atomic loads and stores only (MI355X: per-XCD L2s are not coherent; 8-byte granules need
+// no ordering and no release fence):
+//   * a finishing string stores its count TAGGED with the call's epoch, a.sc_epoch << 32 | count
+//     (sc1; a batch is complete when all its counts carry the tag -- no counter, no wait);
+//   * the first wave that finds a batch complete and the previous batch's prefix published claims it
+//     (atomicOr SC_PUB | SC_CLAIM | inclusive id prefix), writes the batch's id_off entries, drains,
+//     and sets SC_OFS; an unpublished previous batch is published first, back to the nearest
+//     published one (a decoupled look-back that also serves batches whose strings no queue holds);
 //   * a queued string whose batch has SC_OFS is copied from the wave's own staging (its own stores:
 //     only the L1 could be stale, so the loads are sc1) to ids[id_off[s+1] - count ..].
-// Strings whose batch or an earlier one holds a string routed to a later pass, and strings that do
-// not fit the queue, stay for the finish pass (it copies every batch not fully copied here).
+// Strings whose batch or an earlier one holds a string routed to a later pass (a.route_c), and strings
+// that do not fit the queue, stay for the finish pass (it copies every batch not fully copied here).
 // The id_off[s+1] of a string is the CSR offset (tokenizer_utils.py:76-79: ids concatenated per string).
 // (Cold code, kept out of line: inlined into the tokenize loop it cost 8 SGPR + 8 VGPR spills.)
 __device__ __forceinline__ unsigned long long sc_ld(const unsigned long long *p) {
@@ -818,62 +821,33 @@ __device__ __forceinline__ unsigned sc_size(const A &a, unsigned b) {
     const uint64_t rem = a.n_str - (uint64_t)b * FIN_BATCH;
     return rem < FIN_BATCH ? (unsigned)rem : FIN_BATCH;
 }
-// E = the ids of the batches before b.  1: known; 0: a batch in between has strings still running;
-// -1: one holds a string routed to a later pass (no batch from there on is copied in this pass)
+// Publish batch b given E = the ids before it: claim it, write its id_off entries, set SC_OFS.  1: its
+// id_off entries are written (here or by another wave), 0: not yet (a string still runs, or another
+// wave writes them), -1: never in this pass.  *incl: the inclusive prefix when known (1, or 0 with PUB).
 template <typename A>
-__device__ __forceinline__ int sc_prefix(const A &a, unsigned b, unsigned lane, unsigned long long &E) {
-    unsigned long long acc = 0;
-    for (unsigned top = b; top > 0; top = top > 64u ? top - 64u : 0u) {
-        const int k = (int)top - 1 - (int)lane;
-        unsigned long long pv = SC_PUB, sv = 0;   // k < 0: before the first batch, prefix 0
-        if (k >= 0) {
-            pv = sc_ld(&a.inc[k]);
-            sv = sc_ld(&a.bsum[k]);
-        }
-        const uint64_t pm = ballot((pv & SC_PUB) != 0);
-        const unsigned l0 = pm ? (unsigned)__builtin_ctzll(pm) : 64u;   // the nearest published
-        const bool below = lane < l0;
-        const unsigned rt = (unsigned)(sv >> BS_ROUTE_SHIFT) & 0x1FFu, fin = (unsigned)(sv >> BS_FIN_SHIFT) & 0x1FFu;
-        if (ballot(below && rt != 0)) return -1;
-        if (ballot(below && fin != sc_size(a, (unsigned)max(k, 0)))) return 0;
-        const unsigned long long part_sum = below ? (sv & BS_SUM_MASK) : 0ull;
-        acc += sc_readlane64(wave_incl_scan_add64(part_sum, lane), 63);
-        if (l0 < 64u) {
-            E = acc + (sc_readlane64(pv, l0) & SC_VAL_MASK);
-            return 1;
-        }
-    }
-    E = acc;
-    return 1;
-}
-// batch b's id_off entries: 1 written (SC_OFS), 0 not yet, -1 not in this pass
-template <typename A>
-__device__ __forceinline__ int sc_publish(const A &a, unsigned b, unsigned lane) {
-    if (const unsigned rc = uni(__hip_atomic_load(a.route_c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)); rc && b >= ~rc) return -1;
-    const unsigned long long v = uni64(sc_ld(&a.inc[b]));
-    if (v & SC_OFS) return 1;
-    if (v & SC_CLAIM) return 0;   // another wave is writing them
-    const unsigned long long sv = uni64(sc_ld(&a.bsum[b]));
-    if ((sv >> BS_ROUTE_SHIFT) & 0x1FFu) return -1;
-    const unsigned nsz = sc_size(a, b);
-    if (((sv >> BS_FIN_SHIFT) & 0x1FFu) != nsz) return 0;
-    unsigned long long E = 0;
-    const int r = b ? sc_prefix(a, b, lane, E) : 1;
-    if (r <= 0) return r;
-    unsigned long long old = 0;
-    if (lane == 0) old = atomicOr(&a.inc[b], SC_PUB | SC_CLAIM | (E + (sv & BS_SUM_MASK)));
-    old = sc_readlane64(old, 0);
-    if (old & SC_CLAIM) return (old & SC_OFS) ? 1 : 0;
-    // this wave writes them: string s0 + i ends at E + the counts of strings s0 .. s0 + i
+__device__ __forceinline__ int sc_publish_at(const A &a, unsigned b, unsigned long long E, unsigned lane,
+                                             unsigned long long &incl) {
     const uint64_t s0 = (uint64_t)b * FIN_BATCH;
+    const unsigned nsz = sc_size(a, b);
+    const unsigned long long tag = (unsigned long long)a.sc_epoch << 32;
     unsigned long long c[4], t = 0;
+    bool missing = false;
 #pragma unroll
     for (int u = 0; u < 4; u++) {
         const unsigned i = 4u * lane + (unsigned)u;
-        c[u] = i < nsz ? sc_ld(reinterpret_cast<const unsigned long long *>(a.counts) + s0 + i) : 0ull;
+        c[u] = i < nsz ? sc_ld(reinterpret_cast<const unsigned long long *>(a.counts) + s0 + i) : tag;
+        missing |= (c[u] & ~0xFFFFFFFFull) != tag;
+        c[u] &= 0xFFFFFFFFull;
         t += c[u];
     }
-    unsigned long long run = E + wave_incl_scan_add64(t, lane) - t;
+    if (ballot(missing)) return 0;
+    const unsigned long long scan = wave_incl_scan_add64(t, lane);
+    incl = E + sc_readlane64(scan, 63);
+    unsigned long long old = 0;
+    if (lane == 0) old = atomicOr(&a.inc[b], SC_PUB | SC_CLAIM | incl);
+    old = sc_readlane64(old, 0);
+    if (old & SC_CLAIM) return (old & SC_OFS) ? 1 : 0;   // another wave writes them
+    unsigned long long run = E + scan - t;   // string s0 + i ends at E + the counts of strings s0 .. s0 + i
 #pragma unroll
     for (int u = 0; u < 4; u++) {
         const unsigned i = 4u * lane + (unsigned)u;
@@ -885,13 +859,37 @@ __device__ __forceinline__ int sc_publish(const A &a, unsigned b, unsigned lane)
     if (lane == 0) atomicOr(&a.inc[b], SC_OFS);
     return 1;
 }
+// Batch b's id_off entries: publish b, and first the unpublished batches before it back to the nearest
+// published one (up to 64 back; else 0, retried later).
+template <typename A>
+__device__ __forceinline__ int sc_publish(const A &a, unsigned b, unsigned lane) {
+    if (const unsigned rc = uni(__hip_atomic_load(a.route_c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)); rc && b >= ~rc) return -1;
+    const unsigned long long v = uni64(sc_ld(&a.inc[b]));
+    if (v & SC_OFS) return 1;
+    if (v & SC_PUB) return 0;   // another wave is writing them
+    // the nearest published batch before b: lane l reads batch b-1-l (before batch 0: prefix 0)
+    const int k = (int)b - 1 - (int)lane;
+    const unsigned long long pv = k >= 0 ? sc_ld(&a.inc[k]) : SC_PUB;
+    const uint64_t pm = ballot((pv & SC_PUB) != 0);
+    if (!pm) return 0;
+    const unsigned l0 = (unsigned)__builtin_ctzll(pm);
+    unsigned long long E = sc_readlane64(pv, l0) & SC_VAL_MASK;
+    for (unsigned q = b - l0; q <= b; q++) {   // batches b - l0 .. b, in order
+        unsigned long long incl = 0;
+        const int r = sc_publish_at(a, q, E, lane, incl);
+        if (q == b) return r;
+        if (r == 0 && !(uni64(sc_ld(&a.inc[q])) & SC_PUB)) return 0;   // q is not complete yet
+        E = r ? incl : (uni64(sc_ld(&a.inc[q])) & SC_VAL_MASK);   // (claimed by another wave: its prefix)
+    }
+    return 0;
+}
 // The copy queue's n entries from qh: publish the head's batch if it can be, then the length of the run
 // of entries from the head whose batches have their id_off written (~0u: drop the queue, a string
 // before them went to a later pass).
-__device__ __noinline__ unsigned sc_ready(ConstKernArgs *kp, unsigned qh, unsigned n, unsigned lane) {
+__device__ __noinline__ unsigned sc_ready(ConstKernArgs *kp, unsigned bid, unsigned qh, unsigned n, unsigned lane) {
     const auto &a = kp->ea;
-    uint2 e = make_uint2(0u, 0u);
-    if (lane < n) e = a.cq[(size_t)blockIdx.x * CQ_CAP + ((qh + lane) % CQ_CAP)];
+    uint4 e = make_uint4(0u, 0u, 0u, 0u);
+    if (lane < n) e = a.cq[(size_t)bid * CQ_CAP + ((qh + lane) % CQ_CAP)];
     const unsigned b = e.x / FIN_BATCH;
     unsigned long long st = SC_OFS;
     if (lane < n) st = sc_ld(&a.inc[b]);
@@ -905,15 +903,21 @@ __device__ __noinline__ unsigned sc_ready(ConstKernArgs *kp, unsigned qh, unsign
     const unsigned npop = ~ready ? (unsigned)__builtin_ctzll(~ready) : 64u;   // the ready run from the head
     return npop < n ? npop : n;
 }
-// copy the queue's npop entries from qh: string s's cnt staged ids (this wave's own stores, read sc1: only
-// this CU's L1 could hold a stale line another wave read) to ids[id_off[s+1] - cnt ..]
-__device__ __noinline__ void sc_copy_run(ConstKernArgs *kp, unsigned qh, unsigned npop, unsigned lane, uint64_t base_off, bool w16) {
+// Copy the queue's npop entries from qh: string s's cnt staged ids (this wave's own stores, read sc1: only
+// this CU's L1 could hold a stale line another wave read) to ids[id_off[s+1] - cnt ..].  Every string's
+// offset load is issued at once, and each string's staging loads before the previous string's stores.
+__device__ __noinline__ void sc_copy_run(ConstKernArgs *kp, unsigned bid, unsigned qh, unsigned npop, unsigned lane, bool w16) {
     const auto &a = kp->ea;
+    uint4 e = make_uint4(0u, 0u, 0u, 0u);
+    unsigned long long o1 = 0;
+    if (lane < npop) {
+        e = a.cq[(size_t)bid * CQ_CAP + ((qh + lane) % CQ_CAP)];
+        o1 = sc_ld(reinterpret_cast<const unsigned long long *>(a.id_off) + e.x + 1);
+    }
     for (unsigned q = 0; q < npop; q++) {
-        const uint2 e = a.cq[(size_t)blockIdx.x * CQ_CAP + ((qh + q) % CQ_CAP)];
-        const unsigned s = uni(e.x), cnt = uni(e.y);
-        const uint64_t o0 = uni64(sc_ld(reinterpret_cast<const unsigned long long *>(a.id_off) + s + 1)) - cnt;
-        const uint64_t src = a.str_off[s] - base_off;
+        const unsigned cnt = __builtin_amdgcn_readlane(e.y, q);
+        const uint64_t src = ((uint64_t)__builtin_amdgcn_readlane(e.w, q) << 32) | (unsigned)__builtin_amdgcn_readlane(e.z, q);
+        const uint64_t o0 = sc_readlane64(o1, q) - cnt;
         const uint8_t *sb = w16 ? reinterpret_cast<const uint8_t *>(a.staging16 + src) : reinterpret_cast<const uint8_t *>(a.staging + src);
         const unsigned al = (unsigned)((uintptr_t)sb & 3u);   // (a dword-aligned resource base)
         const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)(sb - al), (short)0, (int)(al + cnt * (w16 ? 2u : 4u)), 0x00020000);
@@ -933,8 +937,8 @@ __device__ __noinline__ void sc_copy_run(ConstKernArgs *kp, unsigned qh, unsigne
                 if (k < cnt) dst[k] = v[u];
             }
         }
-        if (lane == 0) atomicAdd(&a.copied[s / FIN_BATCH], 1u);
     }
+    if (lane < npop) atomicAdd(&a.copied[e.x / FIN_BATCH], 1u);
 }
 
 // SW: staged id width 0 = by a.staging16, 1 = int16, 2 = int32; RAW: DPT_MODE_RAW as a compile-time
@@ -1070,11 +1074,12 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
     };
 
     // ---- self-copy: see sc_ready / sc_copy_run above
-    auto sc_step = [&]() -> unsigned {   // strings copied (uniform)
+    auto sc_step = [&](bool draining) -> unsigned {   // strings copied (uniform)
         const unsigned qh = uni(SSr(0).qh), qt = uni(SSr(0).qt);
         const unsigned n = (qt - qh) & 0xFFu;
         if (!n) return 0;
-        const unsigned npop = sc_ready(kp, qh, n, lane);
+        if (!draining && n < SC_MIN_QUEUE) return 0;   // (a step costs round trips: every few rounds)
+        const unsigned npop = sc_ready(kp, bid, qh, n, lane);
         if (npop == ~0u) {   // a string before them went to a later pass: the finish pass copies the queue's strings
             if (lane == 0) SSr(0).qh = (uint8_t)qt;
             return 0;
@@ -1086,7 +1091,7 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                 n_pend = 0;
             }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's staging stores are out
-        sc_copy_run(kp, qh, npop, lane, base_off, SW == 1 || (SW == 0 && a.staging16 != nullptr));
+        sc_copy_run(kp, bid, qh, npop, lane, SW == 1 || (SW == 0 && a.staging16 != nullptr));
         if (lane == 0) SSr(0).qh = (uint8_t)(qh + npop);
         return npop;
     };
@@ -1180,13 +1185,11 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                     if (!BIG && SC_ON && a.inc) {   // self-copy: finished with no ids (empty), or routed to a later pass
                         const unsigned b = (unsigned)(s / FIN_BATCH);
                         if (status == 3) {
-                            atomicAdd(&a.bsum[b], 1ull << BS_ROUTE_SHIFT);
+                            a.counts[s] = 0;
                             atomicMax(a.route_c, ~b);
                         } else {
-                            st_agent(reinterpret_cast<unsigned long long *>(a.counts) + s, 0ull);
-                            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                            atomicAdd(&a.bsum[b], 1ull << BS_FIN_SHIFT);
-                            atomicAdd(&a.copied[b], 1u);
+                            st_agent(reinterpret_cast<unsigned long long *>(a.counts) + s, (unsigned long long)a.sc_epoch << 32);
+                            atomicAdd(&a.copied[b], 1u);   // nothing to copy
                         }
                     } else {
                         a.counts[s] = 0;
@@ -1345,7 +1348,8 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                         const unsigned t2e = ((tk2 << 1) & 0xEu) | wave_shift_in((tk2 >> 3) & 1u, 0u);
                         if (ballot((tk1 | t2e) != 0)) {
                             // (lane l's dwords are 4l+1 .. 4l+4: lanes l, l+8, l+16, l+24 of a 32-lane group hit
-                            // one bank; a rotated order spilled VGPRs, r03)
+                            // one bank; a rotated order (r03) and a transposed one -- round q's lane l taking
+                            // end 64q+l+1, its bits gathered by ds_bpermute (r04) -- cost VGPR spills instead)
 #pragma unroll
                             for (int u = 0; u < 4; u++)
                                 __hip_atomic_fetch_and(&r32[k0 + 1u + u], ~((((tk1 >> u) & 1u) << 16) | (((t2e >> u) & 1u) << 17)),
@@ -2593,6 +2597,7 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
         KREFRESH();
         bool fq = false;            // self-copy: a string with ids finished here (queued below)
         unsigned fq_s = 0, fq_n = 0;
+        uint64_t fq_sb = 0;
         if (lane < (unsigned)NG) {
             SlotState &S = SSr(lane);
             if (S.active && S.n_atoms > 0 && S.status == 0 && (S.inval & 2)) {
@@ -2600,10 +2605,7 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                 // unbounded pass redoes the whole string (and writes its status and count)
                 a.long_list[atomicAdd(a.long_count, 1u)] = S.s;
                 S.active = 0;
-                if (!BIG && SC_ON && a.inc) {   // self-copy: routed to a later pass
-                    atomicAdd(&a.bsum[S.s / FIN_BATCH], 1ull << BS_ROUTE_SHIFT);
-                    atomicMax(a.route_c, ~(S.s / FIN_BATCH));
-                }
+                if (!BIG && SC_ON && a.inc) atomicMax(a.route_c, ~(S.s / FIN_BATCH));   // self-copy: routed to a later pass
             } else if (S.active && S.n_atoms > 0) {
                 S.capsum += S.wtok;
                 if (S.status == 0 && S.inval) S.status = 1;
@@ -2616,19 +2618,18 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                     a.status[s] = (int32_t)S.status;
                     if (a.capped) a.capped[s] = S.status == 3 ? -1 : (int32_t)S.capsum;
                     S.active = 0;
+                    if (a.bsum && cnt) atomicAdd(&a.bsum[s / FIN_BATCH], (unsigned long long)cnt);
                     if (!BIG && SC_ON && a.inc) {
-                        // the count, drained, then the batch sum: a wave that sees the batch complete
-                        // reads every count of it (sc_publish)
-                        st_agent(reinterpret_cast<unsigned long long *>(a.counts) + s, cnt);
-                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                        atomicAdd(&a.bsum[s / FIN_BATCH], (1ull << BS_FIN_SHIFT) | cnt);
+                        // the count tagged with the call's epoch: the batch is complete when all its
+                        // counts carry the tag (sc_publish_at)
+                        st_agent(reinterpret_cast<unsigned long long *>(a.counts) + s, ((unsigned long long)a.sc_epoch << 32) | cnt);
                         if (!cnt) atomicAdd(&a.copied[s / FIN_BATCH], 1u);   // nothing to copy
                         fq = cnt != 0;
                         fq_s = (unsigned)s;
                         fq_n = (unsigned)cnt;
+                        fq_sb = S.sb;
                     } else {
                         a.counts[s] = cnt;
-                        if (a.bsum && cnt) atomicAdd(&a.bsum[s / FIN_BATCH], (unsigned long long)cnt);
                     }
                 }
             }
@@ -2642,12 +2643,13 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                 const unsigned qh = uni(SSr(0).qh), qt = uni(SSr(0).qt);
                 const unsigned room = CQ_CAP - ((qt - qh) & 0xFFu);
                 const unsigned rk = __builtin_amdgcn_mbcnt_hi((unsigned)(fm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)fm, 0u));
-                if (fq && rk < room) a.cq[(size_t)bid * CQ_CAP + ((qt + rk) % CQ_CAP)] = make_uint2(fq_s, fq_n);
+                if (fq && rk < room)
+                    a.cq[(size_t)bid * CQ_CAP + ((qt + rk) % CQ_CAP)] = make_uint4(fq_s, fq_n, (uint32_t)fq_sb, (uint32_t)(fq_sb >> 32));
                 const unsigned nq = (unsigned)__builtin_popcountll(fm);
                 if (lane == 0) SSr(0).qt = (uint8_t)(qt + (nq < room ? nq : room));
                 wave_sync();
             }
-            (void)sc_step();
+            (void)sc_step(false);
             wave_sync();
         }
         STAMP(4);
@@ -2662,7 +2664,7 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
         // claimed by now, by running waves); bounded -- what is left stays for the finish pass
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         while (uni(SSr(0).qh) != uni(SSr(0).qt)) {
-            if (sc_step()) {
+            if (sc_step(true)) {
                 wave_sync();
                 continue;
             }
@@ -2815,7 +2817,7 @@ __global__ void __launch_bounds__(FIN_THREADS) finish_kernel(FinishArgs f) {
     const uint64_t s0 = t * FIN_BATCH;
     // the first FIN_BATCH threads hold one string each; every thread copies
     const bool has = tid < FIN_BATCH && tid < f.n_str - s0;
-    const uint64_t c = has ? f.counts[s0 + tid] : 0ull;
+    const uint64_t c = has ? f.counts[s0 + tid] & 0xFFFFFFFFull : 0ull;   // (self-copy calls tag the counts)
     const uint64_t src = has ? f.str_off[s0 + tid] - base_off : 0ull;
     uint64_t total;
     uint64_t o0 = 0;   // one batch: its first id is 0
@@ -3109,7 +3111,7 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     a.long_span = p.long_span;
     a.hist_zero = nullptr; a.n_hist = 0;
     // self-copy (the host decides: CSR calls of >= SC_MIN_BATCHES batches without edges or length-only DPs)
-    a.inc = p.self_copy ? p.inc : nullptr; a.copied = p.copied; a.cq = p.cq;
+    a.inc = p.self_copy ? p.inc : nullptr; a.copied = p.copied; a.cq = p.cq; a.sc_epoch = p.sc_epoch;
     a.route_c = p.retry_count + 5;   // (counter block uint32 [5]: reset_counters zeroes it)
     a.id_off = p.id_off; a.ids = p.ids;
     TrieView tv{p.slots, p.slot_ids, p.slots4, p.root_base, p.n_slots, p.pair16};
@@ -3251,7 +3253,7 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
 }
 
 size_t pend_scratch_bytes(unsigned max_blocks) { return (size_t)max_blocks * 64 * sizeof(uint4); }
-size_t cq_scratch_bytes(unsigned max_blocks) { return (size_t)max_blocks * CQ_CAP * sizeof(uint2); }
+size_t cq_scratch_bytes(unsigned max_blocks) { return (size_t)max_blocks * CQ_CAP * sizeof(uint4); }
 
 size_t wsl_scratch_bytes(unsigned max_blocks) {
     return (size_t)max_blocks * 4 * GroupLDS<SMALL_CH, 16>::WSL_STRIDE;   // NG x stride covers both G at CH = 256
