@@ -8,6 +8,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -53,7 +54,7 @@ struct dpt_ctx {
     uint64_t cap_batches = 0;
     int flag_parity = 0;
     uint4 *cq = nullptr;              // self-copy queues (dpt::cq_scratch_bytes)
-    uint32_t sc_epoch = 0;            // self-copy calls so far: each call's counts carry the next value
+
     unsigned long long *last_sc = nullptr;   // the last call's region when it self-copied (dpt_ctx_copy_stats) ...
     uint64_t last_sc_nb = 0;                 // ... and its batches
     unsigned max_blocks = 0;
@@ -156,6 +157,9 @@ int ensure_workspace(dpt_ctx *c, const dpt_vocab *v, uint64_t n_bytes, uint64_t 
         uint64_t cap = c->cap_str, cap2 = 2 * c->cap_str;
         e = grow(&c->counts, &cap, n_str);
         if (e != hipSuccess) return hip_fail(e, "hipMalloc(counts)");
+        // (zeroed: the self-copy's completeness test reads tagged counts, dpt_kernels.hip sc_publish_at)
+        if ((e = hipMemset(c->counts, 0, cap * sizeof(uint64_t))) != hipSuccess) return hip_fail(e, "hipMemset(counts)");
+        fresh = true;
         e = grow(&c->retry_list, &cap2, 2 * n_str);   // the 2048-byte pass's list, then the unbounded pass's
         if (e != hipSuccess) return hip_fail(e, "hipMalloc(retry_list)");
         cap2 /= 2;
@@ -594,8 +598,12 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
         p.cq = c->cq;
         // self-copy: CSR calls of enough batches without edge outputs or length-only DPs
         const char *sce = getenv("DPT_SELF_COPY");   // (A/B switch: "0" = off; read per call)
-        if (++c->sc_epoch == 0) c->sc_epoch = 1;   // (a count of the previous call never matches)
-        p.sc_epoch = c->sc_epoch;
+        // the tag of this call's counts: unique in the process (a count stored by an earlier call -- of
+        // any ctx: freed workspaces are reused -- never matches; the counts start zeroed, tag 0 unused)
+        static std::atomic<uint32_t> epoch{0};
+        uint32_t ep = ++epoch;
+        if (ep == 0) ep = ++epoch;
+        p.sc_epoch = ep;
         p.self_copy = !(sce && !strcmp(sce, "0")) && !padded && !edges && !(mode_flags & (DPT_FLAG_UNCAPPED | DPT_FLAG_LEN_ONLY)) &&
                       (n_str + dpt::FIN_BATCH - 1) / dpt::FIN_BATCH >= dpt::SC_MIN_BATCHES;
     }
