@@ -545,7 +545,7 @@ def main():
                          "alg_bytes_staged_width": alg_staged, "staged_id_bytes": id_bytes,
                          "frac_staged_width": alg_staged / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
             "cpu_baseline": cpu,
-            "self_copy": {"strings_copied_by_first_pass": sc_copied, "strings": M, "batches_with_offsets": sc_batches,
+            "self_copy": {"strings_copied_by_first_pass": sc_copied, "strings": M, "batches_copied_whole": sc_batches,
                           "batches": sc_nb, "enabled": os.environ.get("DPT_SELF_COPY", "1") != "0"},
             "padded_layout": {"api": "dpt_encode_padded (ids at each string's byte offset + per-string counts, no CSR pass); encode only, no histogram",
                               "ms_per_step": dtp / args.steps * 1e3, "bytes_per_s": bytes_all * args.steps / dtp,

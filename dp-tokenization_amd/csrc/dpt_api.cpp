@@ -29,6 +29,8 @@ struct dpt_vocab {
     dpt_vocab_stats stats{};
 };
 
+static uint64_t flag_words(uint64_t cap_batches) { return cap_batches * (2 * dpt::BS_LINE + 1); }
+
 struct dpt_ctx {
     int device = 0;
     // workspace of the device path (ensure_workspace)
@@ -46,17 +48,17 @@ struct dpt_ctx {
                                       // counter at byte 32, ..., the first pass's partition counters at byte 256
     uint8_t *wsl_scratch = nullptr;   // word lists of the 256-byte pass (dpt::wsl_scratch_bytes)
     uint4 *pend = nullptr;            // pending residual tokens of the 256-byte pass (dpt::pend_scratch_bytes)
-    // per 256-string batch, two parity regions R0, R1 of {batch sums, self-copy prefixes + flags, copied
-    // counts} (3 x cap_batches u64 each), then the batch prefixes of the scan path (cap_batches): the
-    // call of parity P uses R_P and -- fold and self-copy calls -- zeroes R_(1-P) for the next one (the
-    // parity flips); between calls R_parity is all zero.  See dpt_internal.h fin_fold and SC_*.
+    // two parity regions R0, R1 of batch lines (dpt::BS_LINE u64 per 256-string batch: its sum, self-copy
+    // prefix, copied count), then the batch prefixes of the scan path (cap_batches u64): the call of
+    // parity P uses R_P and -- fold and self-copy calls -- zeroes R_(1-P) for the next one (the parity
+    // flips); between calls R_parity is all zero.  See dpt_internal.h fin_fold and BS_LINE.
     unsigned long long *flags = nullptr;
     uint64_t cap_batches = 0;
     int flag_parity = 0;
     uint4 *cq = nullptr;              // self-copy queues (dpt::cq_scratch_bytes)
 
     unsigned long long *last_sc = nullptr;   // the last call's region when it self-copied (dpt_ctx_copy_stats) ...
-    uint64_t last_sc_nb = 0;                 // ... and its batches
+    uint64_t last_sc_nb = 0, last_sc_n = 0;  // ... and its batches and strings
     unsigned max_blocks = 0;
     // host path: one device buffer in (text | offsets | cut) and one out (id_off | status | capped |
     // counters | ids | edges), each mirrored by a pinned host buffer so every copy is one async DMA
@@ -157,7 +159,7 @@ int ensure_workspace(dpt_ctx *c, const dpt_vocab *v, uint64_t n_bytes, uint64_t 
         uint64_t cap = c->cap_str, cap2 = 2 * c->cap_str;
         e = grow(&c->counts, &cap, n_str);
         if (e != hipSuccess) return hip_fail(e, "hipMalloc(counts)");
-        // (zeroed: the self-copy's completeness test reads tagged counts, dpt_kernels.hip sc_publish_at)
+        // (zeroed: the self-copy reads tagged counts, dpt_kernels.hip sc_copy_run)
         if ((e = hipMemset(c->counts, 0, cap * sizeof(uint64_t))) != hipSuccess) return hip_fail(e, "hipMemset(counts)");
         fresh = true;
         e = grow(&c->retry_list, &cap2, 2 * n_str);   // the 2048-byte pass's list, then the unbounded pass's
@@ -174,8 +176,8 @@ int ensure_workspace(dpt_ctx *c, const dpt_vocab *v, uint64_t n_bytes, uint64_t 
         c->flags = nullptr;
         c->cap_batches = 0;
         c->flag_parity = 0;
-        if ((e = hipMalloc((void **)&c->flags, 7 * capb * sizeof(unsigned long long))) != hipSuccess) return hip_fail(e, "hipMalloc(flags)");
-        if ((e = hipMemset(c->flags, 0, 7 * capb * sizeof(unsigned long long))) != hipSuccess) return hip_fail(e, "hipMemset(flags)");
+        if ((e = hipMalloc((void **)&c->flags, flag_words(capb) * sizeof(unsigned long long))) != hipSuccess) return hip_fail(e, "hipMalloc(flags)");
+        if ((e = hipMemset(c->flags, 0, flag_words(capb) * sizeof(unsigned long long))) != hipSuccess) return hip_fail(e, "hipMemset(flags)");
         c->cap_batches = capb;
         fresh = true;
     }
@@ -187,7 +189,7 @@ int ensure_workspace(dpt_ctx *c, const dpt_vocab *v, uint64_t n_bytes, uint64_t 
         e = hipMalloc((void **)&c->pend, dpt::pend_scratch_bytes(c->max_blocks));
         if (e != hipSuccess) return hip_fail(e, "hipMalloc(pend)");
     }
-    if (!c->cq) {
+    if (!c->cq && dpt::self_copy_built()) {
         e = hipMalloc((void **)&c->cq, dpt::cq_scratch_bytes(c->max_blocks));
         if (e != hipSuccess) return hip_fail(e, "hipMalloc(cq)");
     }
@@ -498,7 +500,7 @@ int dpt_ctx_workspace_bytes(const dpt_ctx *c, uint64_t *device_path, uint64_t *h
     if (!c) return fail(DPT_E_ARG, "null ctx");
     if (device_path)
         *device_path = c->cap16 * 2 + c->cap32 * 4 + c->arena_cap * ARENA_PER_BYTE + c->cap_str * (8 + 2 * 4) +
-                       c->cap_batches * 7 * 8 + (c->wsl_scratch ? dpt::wsl_scratch_bytes(c->max_blocks) : 0) +
+                       flag_words(c->cap_batches) * 8 + (c->wsl_scratch ? dpt::wsl_scratch_bytes(c->max_blocks) : 0) +
                        (c->pend ? dpt::pend_scratch_bytes(c->max_blocks) : 0) +
                        (c->cq ? dpt::cq_scratch_bytes(c->max_blocks) : 0) +
                        (c->retry_count ? dpt::CTR_ALLOC_BYTES : 0);
@@ -506,20 +508,22 @@ int dpt_ctx_workspace_bytes(const dpt_ctx *c, uint64_t *device_path, uint64_t *h
     return DPT_OK;
 }
 
-int dpt_ctx_copy_stats(dpt_ctx *c, uint64_t *copied, uint64_t *batches_ofs, uint64_t *n_batches) {
-    if (!c || !copied || !batches_ofs || !n_batches) return fail(DPT_E_ARG, "null argument");
-    *copied = *batches_ofs = *n_batches = 0;
+int dpt_self_copy_available(void) { return dpt::self_copy_built() ? 1 : 0; }
+
+int dpt_ctx_copy_stats(dpt_ctx *c, uint64_t *copied, uint64_t *batches_whole, uint64_t *n_batches) {
+    if (!c || !copied || !batches_whole || !n_batches) return fail(DPT_E_ARG, "null argument");
+    *copied = *batches_whole = *n_batches = 0;
     if (!c->last_sc || !c->last_sc_nb) return DPT_OK;
     DeviceGuard g(c->device);
-    const uint64_t nb = c->last_sc_nb, cb = c->cap_batches;
-    std::vector<unsigned long long> inc(nb);
-    std::vector<uint32_t> cp(nb);
-    hipError_t e = hipMemcpy(inc.data(), c->last_sc + cb, nb * 8, hipMemcpyDeviceToHost);
-    if (e == hipSuccess) e = hipMemcpy(cp.data(), c->last_sc + 2 * cb, nb * 4, hipMemcpyDeviceToHost);
+    const uint64_t nb = c->last_sc_nb;
+    std::vector<unsigned long long> lines(nb * dpt::BS_LINE);
+    hipError_t e = hipMemcpy(lines.data(), c->last_sc, lines.size() * 8, hipMemcpyDeviceToHost);
     if (e != hipSuccess) return hip_fail(e, "D2H copy stats");
     for (uint64_t b = 0; b < nb; b++) {
-        *copied += cp[b];
-        *batches_ofs += (inc[b] & dpt::SC_OFS) ? 1 : 0;
+        const unsigned long long *l = lines.data() + b * dpt::BS_LINE;
+        const uint32_t cp = (uint32_t)l[dpt::BS_COPIED];
+        *copied += cp;
+        *batches_whole += cp == (b + 1 < nb ? dpt::FIN_BATCH : c->last_sc_n - b * dpt::FIN_BATCH) ? 1 : 0;
     }
     *n_batches = nb;
     return DPT_OK;
@@ -587,24 +591,26 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
     p.long_span = v->stats.max_cp > 64 ? 1 : 0;
     p.max_tok_bytes = v->stats.max_bytes;
     {
-        const uint64_t cb = c->cap_batches;
-        unsigned long long *r = c->flags + (c->flag_parity ? 3 * cb : 0);
+        const uint64_t cb = c->cap_batches, rl = cb * dpt::BS_LINE;
+        unsigned long long *r = c->flags + (c->flag_parity ? rl : 0);
         p.flags = r;
-        p.inc = r + cb;
-        p.copied = reinterpret_cast<uint32_t *>(r + 2 * cb);
-        p.zero_other = c->flags + (c->flag_parity ? 0 : 3 * cb);
-        p.zero_n = 3 * cb;
-        p.bpre = c->flags + 6 * cb;
+        p.inc = r + dpt::BS_INC;
+        p.copied = reinterpret_cast<uint32_t *>(r + dpt::BS_COPIED);
+        p.zero_other = c->flags + (c->flag_parity ? 0 : rl);
+        p.zero_n = cb;
+        p.bpre = c->flags + 2 * rl;
         p.cq = c->cq;
         // self-copy: CSR calls of enough batches without edge outputs or length-only DPs
-        const char *sce = getenv("DPT_SELF_COPY");   // (A/B switch: "0" = off; read per call)
+        // (opt-in, read per call: "1" = on.  Measured slower than the finish pass's copy so far: the
+        // copy's round trips stall the latency-bound first pass -- DESIGN.md 9)
+        const char *sce = getenv("DPT_SELF_COPY");
         // the tag of this call's counts: unique in the process (a count stored by an earlier call -- of
         // any ctx: freed workspaces are reused -- never matches; the counts start zeroed, tag 0 unused)
         static std::atomic<uint32_t> epoch{0};
         uint32_t ep = ++epoch;
         if (ep == 0) ep = ++epoch;
         p.sc_epoch = ep;
-        p.self_copy = !(sce && !strcmp(sce, "0")) && !padded && !edges && !(mode_flags & (DPT_FLAG_UNCAPPED | DPT_FLAG_LEN_ONLY)) &&
+        p.self_copy = dpt::self_copy_built() && sce && !strcmp(sce, "1") && !padded && !edges && !(mode_flags & (DPT_FLAG_UNCAPPED | DPT_FLAG_LEN_ONLY)) &&
                       (n_str + dpt::FIN_BATCH - 1) / dpt::FIN_BATCH >= dpt::SC_MIN_BATCHES;
     }
     p.max_blocks = c->max_blocks;
@@ -646,13 +652,14 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
     hipError_t e = dpt::launch_encode(p, st, evp);
     if (e != hipSuccess) {
         (void)hipMemsetAsync(c->retry_count, 0, dpt::CTR_ALLOC_BYTES, st);   // the scan kernel did not reset them
-        (void)hipMemsetAsync(c->flags, 0, 7 * c->cap_batches * sizeof(unsigned long long), st);   // nor zero the batch arrays
+        (void)hipMemsetAsync(c->flags, 0, flag_words(c->cap_batches) * sizeof(unsigned long long), st);   // nor zero the batch lines
         c->flag_parity = 0;
         return hip_fail(e, "encode launch");
     }
     if (!padded && (dpt::fin_fold(n_str) || p.self_copy)) c->flag_parity ^= 1;   // the finish pass zeroed the other region
     c->last_sc = p.self_copy ? p.flags : nullptr;
     c->last_sc_nb = p.self_copy ? (n_str + dpt::FIN_BATCH - 1) / dpt::FIN_BATCH : 0;
+    c->last_sc_n = n_str;
     return DPT_OK;
 }
 

@@ -31,13 +31,13 @@ struct EncodeLaunch {
     uint8_t *wsl_scratch;    // max_blocks x wsl_scratch_bytes(1) bytes
     int long_span;           // vocabulary tokens longer than 64 code points: words over 64 atoms -> unbounded pass
     uint32_t max_tok_bytes;  // longest vocabulary token, bytes
-    unsigned long long *flags;   // per FIN_BATCH-string batch: the sum of its counts, added by the tokenize passes as
-                                 //   strings finish; batch_scan_kernel zeroes it for the next call
-    unsigned long long *bpre;    // per batch: its exclusive id prefix (batch_scan_kernel)
-    unsigned long long *inc;     // per batch (self-copy): SC_* flags + inclusive id prefix
-    uint32_t *copied;            // per batch (self-copy): strings the first pass copied into place
-    unsigned long long *zero_other;   // fold / self-copy calls: the other parity's region, zeroed for the next call ...
-    uint64_t zero_n;             // ... (u64 entries)
+    unsigned long long *flags;   // the batch lines (BS_LINE below): per FIN_BATCH-string batch, the sum of its counts,
+                                 //   added by the tokenize passes as strings finish; zeroed for the next call
+    unsigned long long *bpre;    // per batch (dense): its exclusive id prefix (batch_scan_kernel)
+    unsigned long long *inc;     // flags + BS_INC (self-copy): per batch SC_PUB + inclusive id prefix
+    uint32_t *copied;            // flags + BS_COPIED (self-copy): per batch, strings the first pass copied into place
+    unsigned long long *zero_other;   // fold / self-copy calls: the other parity's batch lines, zeroed for the next call ...
+    uint64_t zero_n;             // ... (batches)
     bool self_copy;              // the first pass copies its strings' ids into the CSR arrays (dpt_kernels.hip)
     uint4 *cq;                   // self-copy: per wave, CQ_CAP queued {string, count, staging element}
     uint32_t sc_epoch;           // self-copy: the call's tag for its counts (never 0)
@@ -87,14 +87,17 @@ __host__ __device__ inline bool fin_fold(uint64_t n_str) {
 }
 constexpr unsigned FIN_MAX_BINS = 1024;   // histogram bins the finish pass folds in (more: the separate pass)
 
-// Batch sums (EncodeLaunch::flags): the count sum in bits 0..39 (a batch holds < 2^40 ids: 256 strings of
-// < 4 GiB); in self-copy calls the first pass also counts, per batch, its strings finished there
-// (bits 40..48) and those routed to a later pass (bits 49..57) -- one atomic add per string.
-constexpr unsigned BS_FIN_SHIFT = 40, BS_ROUTE_SHIFT = 49;
+// Batch lines (EncodeLaunch::flags): one 128-byte line per batch, so the strings finishing in
+// neighbouring batches -- the first pass's partitions run through the batches side by side -- add to
+// different lines (16 batches' sums in one line serialised the adds: +0.05 ms at cfg2, +11 % at 125k
+// strings, profiles/r04d_ab.log).  u64 [BS_SUM]: the count sum in bits 0..39 (a batch holds < 2^40 ids)
+// and, from the first pass, its strings finished there in bits 40.. -- one atomic add per string;
+// [BS_INC] (self-copy): SC_PUB | the batch's inclusive id prefix once known; [BS_COPIED] (u32, self-copy):
+// strings the first pass copied into place.
+constexpr unsigned BS_LINE = 16, BS_INC = 1, BS_COPIED = 2;
+constexpr unsigned BS_FIN_SHIFT = 40;
 constexpr unsigned long long BS_SUM_MASK = (1ull << BS_FIN_SHIFT) - 1;
-// Self-copy (dpt_kernels.hip): per batch, the inclusive id prefix (bits 0..55) once known (SC_PUB), the
-// right to write the batch's id_off entries (SC_CLAIM) and their being written (SC_OFS).
-constexpr unsigned long long SC_PUB = 1ull << 63, SC_CLAIM = 1ull << 62, SC_OFS = 1ull << 61;
+constexpr unsigned long long SC_PUB = 1ull << 63;
 constexpr unsigned long long SC_VAL_MASK = (1ull << 56) - 1;
 constexpr unsigned CQ_CAP = 32;            // strings a wave's copy queue holds
 constexpr unsigned SC_MIN_QUEUE = 8;       // queued strings before a copy step (a step costs round trips)
@@ -204,6 +207,7 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
 size_t wsl_scratch_bytes(unsigned max_blocks);
 size_t pend_scratch_bytes(unsigned max_blocks);
 size_t cq_scratch_bytes(unsigned max_blocks);
+bool self_copy_built();   // the library was built with the first pass's self-copy (make sc)
 hipError_t launch_histogram(const uint64_t *id_off, const int32_t *status, uint64_t n_str, int64_t *hist,
                             uint32_t n_bins, hipStream_t stream);
 hipError_t kernel_init();

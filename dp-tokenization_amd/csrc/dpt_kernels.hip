@@ -335,7 +335,8 @@ struct EncodeArgs {
     int32_t *staging;           // ids staged at (str_off[s]-str_off[0]) + k
     int16_t *staging16;         // non-null: the ids are staged here as int16 instead (half the bytes)
     uint64_t *counts;           // per string
-    unsigned long long *bsum;   // nullable: per FIN_BATCH strings, the sum of their counts (atomics as strings finish)
+    unsigned long long *bsum;   // nullable: the batch lines (dpt_internal.h BS_LINE): per FIN_BATCH strings, the sum of
+                                //   their counts (atomics as strings finish)
     int32_t *status;
     int32_t *capped;            // nullable
     uint32_t *retry_list;       // strings for the 2048-byte pass
@@ -355,11 +356,11 @@ struct EncodeArgs {
     unsigned long long *hist_zero;   // 2048-byte pass, fin_fold calls with DPT_HIST_OVERWRITE: the histogram to
     uint32_t n_hist;                 //   zero before the finish pass adds to it (the scan kernel's duty otherwise)
     // self-copy (first pass of CSR calls; inc == nullptr: off): see sc_step in tokenize_kernel
-    unsigned long long *inc;    // per batch: SC_PUB | SC_CLAIM | SC_OFS | inclusive id prefix
-    uint32_t *copied;           // per batch: strings copied into place
+    unsigned long long *inc;    // per batch (BS_LINE apart): SC_PUB | inclusive id prefix
+    uint32_t *copied;           // per batch (2 BS_LINE apart): strings copied into place
     uint4 *cq;                  // per wave: CQ_CAP queued {string, count, staging element lo, hi} (ring; head / tail in
                                 //   slot 0's SlotState qh / qt)
-    uint32_t sc_epoch;          // the tag of this call's counts (sc_publish_at); never 0
+    uint32_t sc_epoch;          // the tag of this call's counts (sc_copy_run); never 0
     uint32_t *route_c;          // ~(first batch holding a string routed to a later pass), 0: none (atomicMax)
     uint64_t *id_off;
     int32_t *ids;
@@ -367,10 +368,10 @@ struct EncodeArgs {
 
 #ifdef DPT_STAMPS
 // diagnostic build only: cycles per phase summed over waves (never in the product build)
-__device__ unsigned long long g_stamps[8];
-#define STAMP_DECL unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; unsigned long long st_prev = __builtin_amdgcn_s_memtime();
+__device__ unsigned long long g_stamps[10];
+#define STAMP_DECL unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; unsigned long long st_prev = __builtin_amdgcn_s_memtime();
 #define STAMP(k) do { const unsigned long long _t = __builtin_amdgcn_s_memtime(); st_acc[k] += _t - st_prev; st_prev = _t; } while (0)
-#define STAMP_FLUSH do { if (lane == 0) for (int _k = 0; _k < 8; _k++) atomicAdd(&g_stamps[_k], st_acc[_k]); } while (0)
+#define STAMP_FLUSH do { if (lane == 0) for (int _k = 0; _k < 10; _k++) atomicAdd(&g_stamps[_k], st_acc[_k]); } while (0)
 #else
 #define STAMP_DECL
 #define STAMP(k)
@@ -753,10 +754,10 @@ constexpr unsigned A_REFILL64 = 32;   // the same for the 64-lane kernels (8 / 1
                      // + lane-mode B's cut points / recurrence / transfer scan + fix-up, 3 = + B/C0/C1
 #define DPT_STOP 9
 #endif
-#ifdef DPT_NO_SC     // A/B builds only: the first pass without its self-copy code (the host's DPT_SELF_COPY=0 leaves it in)
+#ifdef DPT_SC_BUILD   // the first pass's self-copy (sc_prefix ..): compiled in only on request -- its cold code cost
+constexpr bool SC_ON = true;   // the first pass 1 % even when switched off (profiles/r04h_ab.log), and it is slower
+#else                          // than the finish pass's copy so far
 constexpr bool SC_ON = false;
-#else
-constexpr bool SC_ON = true;
 #endif
 #ifndef DPT_C2STOP   // diagnostic builds only (wrong results): C2 stops after its bulk pass (1) / hash pass (2)
 #define DPT_C2STOP 0
@@ -793,42 +794,95 @@ __device__ __forceinline__ TrieView tv_of(ConstKernArgs *kp) {
 // staged id into the CSR arrays after this kernel (0.33 ms, 13 % of a cfg2 step, half its HBM
 // traffic).  Here the wave that finished a string copies its ids itself once the string's offset is
 // known: the string waits in the wave's copy queue (a.cq, CQ_CAP entries) until its FIN_BATCH-string
-// batch is complete and the ids of every earlier batch are counted, which happens about a round
+// batch is complete and the batches before it are complete or published, which happens about a round
 // later since the partitions advance through the batch side by side.  Cross-wave data goes through
-// agent-scope atomic loads and stores only (MI355X: per-XCD L2s are not coherent; 8-byte granules need
-// no ordering and no release fence):
-//   * a finishing string stores its count TAGGED with the call's epoch, a.sc_epoch << 32 | count
-//     (sc1; a batch is complete when all its counts carry the tag -- no counter, no wait);
-//   * the first wave that finds a batch complete and the previous batch's prefix published claims it
-//     (atomicOr SC_PUB | SC_CLAIM | inclusive id prefix), writes the batch's id_off entries, drains,
-//     and sets SC_OFS; an unpublished previous batch is published first, back to the nearest
-//     published one (a decoupled look-back that also serves batches whose strings no queue holds);
-//   * a queued string whose batch has SC_OFS is copied from the wave's own staging (its own stores:
-//     only the L1 could be stale, so the loads are sc1) to ids[id_off[s+1] - count ..].
-// Strings whose batch or an earlier one holds a string routed to a later pass (a.route_c), and strings
-// that do not fit the queue, stay for the finish pass (it copies every batch not fully copied here).
-// The id_off[s+1] of a string is the CSR offset (tokenizer_utils.py:76-79: ids concatenated per string).
+// agent-scope atomics and sc1 loads / stores only (MI355X: per-XCD L2s are not coherent; 8-byte
+// granules need no ordering and no release fence):
+//   * a finishing string adds count | 1 << BS_FIN_SHIFT to its batch's sum (a batch is complete when
+//     all its strings have added: its sum is then final) and stores its count TAGGED with the call's
+//     epoch, a.sc_epoch << 32 | count (the in-batch offsets read the counts, and the tag says the store
+//     has landed);
+//   * a batch's exclusive prefix is the nearest published inclusive prefix before it (up to 63 back)
+//     plus the sums of the complete batches in between, all read by ONE wave-wide load; the wave that
+//     finds it publishes every prefix on the way (the same value whoever stores it: plain sc1 stores, no
+//     claim, no chain of round trips from batch to batch);
+//   * a queued string's ids are read from the wave's own staging (its own stores: only the L1 could be
+//     stale, so the loads are sc1) and stored at ids[prefix + the counts of the batch's strings before it].
+// Strings of a batch holding a string routed to a later pass never complete it here (a.route_c drops
+// the queues' strings from there on), and strings that do not fit the queue, stay for the finish pass:
+// it writes every id_off entry and copies every batch the first pass did not copy whole.  The id_off[s+1]
+// of a string is the CSR offset (tokenizer_utils.py:76-79: ids concatenated per string).
 // (Cold code, kept out of line: inlined into the tokenize loop it cost 8 SGPR + 8 VGPR spills.)
 __device__ __forceinline__ unsigned long long sc_ld(const unsigned long long *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void sc_st(unsigned long long *p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ unsigned long long sc_readlane64(unsigned long long v, unsigned l) {
     return ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), l) << 32) |
            (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, l);
 }
-template <typename A>
-__device__ __forceinline__ unsigned sc_size(const A &a, unsigned b) {
-    const uint64_t rem = a.n_str - (uint64_t)b * FIN_BATCH;
+__device__ __forceinline__ unsigned sc_size(uint64_t n_str, uint64_t b) {
+    const uint64_t rem = n_str - b * FIN_BATCH;
     return rem < FIN_BATCH ? (unsigned)rem : FIN_BATCH;
 }
-// Publish batch b given E = the ids before it: claim it, write its id_off entries, set SC_OFS.  1: its
-// id_off entries are written (here or by another wave), 0: not yet (a string still runs, or another
-// wave writes them), -1: never in this pass.  *incl: the inclusive prefix when known (1, or 0 with PUB).
+// The ids before batch b (uniform), or ~0ull while b is incomplete or a batch between it and the nearest
+// published one (up to 63 back) is.  Lane l reads batch b - l's line; publishes what it computes.
 template <typename A>
-__device__ __forceinline__ int sc_publish_at(const A &a, unsigned b, unsigned long long E, unsigned lane,
-                                             unsigned long long &incl) {
+__device__ __forceinline__ unsigned long long sc_prefix(const A &a, unsigned b, unsigned lane) {
+    const int k = (int)b - (int)lane;
+    unsigned long long pv = SC_PUB, sv = 0;   // before batch 0: published, prefix 0
+    if (k >= 0) {
+        pv = sc_ld(a.inc + (size_t)k * BS_LINE);
+        sv = sc_ld(a.bsum + (size_t)k * BS_LINE);
+    }
+    const bool comp = k < 0 || (sv >> BS_FIN_SHIFT) == sc_size(a.n_str, (uint64_t)k);
+    const uint64_t cm = ballot(comp);
+    if (!(cm & 1ull)) return ~0ull;   // b itself is not complete
+    const unsigned long long x = comp ? (sv & BS_SUM_MASK) : 0ull;
+    uint64_t pm = ballot((pv & SC_PUB) != 0);
+    if (pm & 1ull) return (sc_readlane64(pv, 0) & SC_VAL_MASK) - sc_readlane64(x, 0);   // b is published
+    pm &= ~1ull;
+    if (!pm) return ~0ull;
+    const unsigned l0 = (unsigned)__builtin_ctzll(pm);
+    const uint64_t need = (1ull << l0) - 1ull;   // batches b - l0 + 1 .. b
+    if ((cm & need) != need) return ~0ull;
+    const unsigned long long xi = lane < l0 ? x : 0ull;
+    const unsigned long long sc = wave_incl_scan_add64(xi, lane);
+    const unsigned long long P0 = sc_readlane64(pv, l0) & SC_VAL_MASK, tot = sc_readlane64(sc, 63);
+    // batch b - lane's inclusive prefix: P0 + the sums of batches b - l0 + 1 .. b - lane
+    if (lane < l0) sc_st(a.inc + (size_t)k * BS_LINE, SC_PUB | (P0 + tot - sc + xi));
+    return P0 + tot - sc_readlane64(x, 0);
+}
+// The copy queue's n entries from qh: the head's batch prefix (*E), and the length of the run of entries
+// from the head in that batch (0: not ready yet; ~0u: drop the queue, a string before them went to a
+// later pass).
+__device__ __noinline__ unsigned sc_ready(ConstKernArgs *kp, unsigned bid, unsigned qh, unsigned n, unsigned lane,
+                                          unsigned long long *E) {
+    const auto &a = kp->ea;
+    unsigned s = 0;
+    if (lane < n) s = a.cq[(size_t)bid * CQ_CAP + ((qh + lane) % CQ_CAP)].x;
+    const unsigned bh = (unsigned)__builtin_amdgcn_readlane((int)s, 0) / FIN_BATCH;
+    if (const unsigned rc = uni(__hip_atomic_load(a.route_c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)); rc && bh >= ~rc) return ~0u;
+    const unsigned long long e = sc_prefix(a, bh, lane);
+    if (e == ~0ull) return 0;
+    *E = e;
+    const uint64_t run = ballot(lane < n && s / FIN_BATCH == bh);
+    return ~run ? (unsigned)__builtin_ctzll(~run) : 64u;
+}
+// Copy the queue's npop entries from qh (strings of one batch, whose first id is E): string s's cnt
+// staged ids (this wave's own stores, read sc1: only this CU's L1 could hold a stale line another wave
+// read) to ids[E + the counts of the batch's strings before s ..].  0: a count has not landed yet
+// (nothing copied).
+__device__ __noinline__ unsigned sc_copy_run(ConstKernArgs *kp, unsigned bid, unsigned qh, unsigned npop, unsigned lane,
+                                             bool w16, unsigned long long E) {
+    const auto &a = kp->ea;
+    uint4 e = make_uint4(0u, 0u, 0u, 0u);
+    if (lane < npop) e = a.cq[(size_t)bid * CQ_CAP + ((qh + lane) % CQ_CAP)];
+    const unsigned b = (unsigned)__builtin_amdgcn_readlane((int)e.x, 0) / FIN_BATCH;
     const uint64_t s0 = (uint64_t)b * FIN_BATCH;
-    const unsigned nsz = sc_size(a, b);
+    const unsigned nsz = sc_size(a.n_str, b);
     const unsigned long long tag = (unsigned long long)a.sc_epoch << 32;
     unsigned long long c[4], t = 0;
     bool missing = false;
@@ -841,83 +895,16 @@ __device__ __forceinline__ int sc_publish_at(const A &a, unsigned b, unsigned lo
         t += c[u];
     }
     if (ballot(missing)) return 0;
-    const unsigned long long scan = wave_incl_scan_add64(t, lane);
-    incl = E + sc_readlane64(scan, 63);
-    unsigned long long old = 0;
-    if (lane == 0) old = atomicOr(&a.inc[b], SC_PUB | SC_CLAIM | incl);
-    old = sc_readlane64(old, 0);
-    if (old & SC_CLAIM) return (old & SC_OFS) ? 1 : 0;   // another wave writes them
-    unsigned long long run = E + scan - t;   // string s0 + i ends at E + the counts of strings s0 .. s0 + i
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-        const unsigned i = 4u * lane + (unsigned)u;
-        run += c[u];
-        if (i < nsz)
-            __hip_atomic_store(reinterpret_cast<unsigned long long *>(a.id_off) + s0 + i + 1, run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the entries are out before SC_OFS says so
-    if (lane == 0) atomicOr(&a.inc[b], SC_OFS);
-    return 1;
-}
-// Batch b's id_off entries: publish b, and first the unpublished batches before it back to the nearest
-// published one (up to 64 back; else 0, retried later).
-template <typename A>
-__device__ __forceinline__ int sc_publish(const A &a, unsigned b, unsigned lane) {
-    if (const unsigned rc = uni(__hip_atomic_load(a.route_c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)); rc && b >= ~rc) return -1;
-    const unsigned long long v = uni64(sc_ld(&a.inc[b]));
-    if (v & SC_OFS) return 1;
-    if (v & SC_PUB) return 0;   // another wave is writing them
-    // the nearest published batch before b: lane l reads batch b-1-l (before batch 0: prefix 0)
-    const int k = (int)b - 1 - (int)lane;
-    const unsigned long long pv = k >= 0 ? sc_ld(&a.inc[k]) : SC_PUB;
-    const uint64_t pm = ballot((pv & SC_PUB) != 0);
-    if (!pm) return 0;
-    const unsigned l0 = (unsigned)__builtin_ctzll(pm);
-    unsigned long long E = sc_readlane64(pv, l0) & SC_VAL_MASK;
-    for (unsigned q = b - l0; q <= b; q++) {   // batches b - l0 .. b, in order
-        unsigned long long incl = 0;
-        const int r = sc_publish_at(a, q, E, lane, incl);
-        if (q == b) return r;
-        if (r == 0 && !(uni64(sc_ld(&a.inc[q])) & SC_PUB)) return 0;   // q is not complete yet
-        E = r ? incl : (uni64(sc_ld(&a.inc[q])) & SC_VAL_MASK);   // (claimed by another wave: its prefix)
-    }
-    return 0;
-}
-// The copy queue's n entries from qh: publish the head's batch if it can be, then the length of the run
-// of entries from the head whose batches have their id_off written (~0u: drop the queue, a string
-// before them went to a later pass).
-__device__ __noinline__ unsigned sc_ready(ConstKernArgs *kp, unsigned bid, unsigned qh, unsigned n, unsigned lane) {
-    const auto &a = kp->ea;
-    uint4 e = make_uint4(0u, 0u, 0u, 0u);
-    if (lane < n) e = a.cq[(size_t)bid * CQ_CAP + ((qh + lane) % CQ_CAP)];
-    const unsigned b = e.x / FIN_BATCH;
-    unsigned long long st = SC_OFS;
-    if (lane < n) st = sc_ld(&a.inc[b]);
-    uint64_t ready = ballot(lane < n && (st & SC_OFS) != 0);
-    if (!(ready & 1ull)) {
-        const unsigned bh = __builtin_amdgcn_readlane(b, 0);
-        const int r = sc_publish(a, bh, lane);
-        if (r < 0) return ~0u;
-        if (r > 0) ready |= ballot(lane < n && b == bh);
-    }
-    const unsigned npop = ~ready ? (unsigned)__builtin_ctzll(~ready) : 64u;   // the ready run from the head
-    return npop < n ? npop : n;
-}
-// Copy the queue's npop entries from qh: string s's cnt staged ids (this wave's own stores, read sc1: only
-// this CU's L1 could hold a stale line another wave read) to ids[id_off[s+1] - cnt ..].  Every string's
-// offset load is issued at once, and each string's staging loads before the previous string's stores.
-__device__ __noinline__ void sc_copy_run(ConstKernArgs *kp, unsigned bid, unsigned qh, unsigned npop, unsigned lane, bool w16) {
-    const auto &a = kp->ea;
-    uint4 e = make_uint4(0u, 0u, 0u, 0u);
-    unsigned long long o1 = 0;
-    if (lane < npop) {
-        e = a.cq[(size_t)bid * CQ_CAP + ((qh + lane) % CQ_CAP)];
-        o1 = sc_ld(reinterpret_cast<const unsigned long long *>(a.id_off) + e.x + 1);
-    }
+    const unsigned long long ex = wave_incl_scan_add64(t, lane) - t;   // ids of strings s0 .. s0 + 4 lane - 1
     for (unsigned q = 0; q < npop; q++) {
+        const unsigned i = (unsigned)__builtin_amdgcn_readlane((int)e.x, q) - (unsigned)s0;
         const unsigned cnt = __builtin_amdgcn_readlane(e.y, q);
         const uint64_t src = ((uint64_t)__builtin_amdgcn_readlane(e.w, q) << 32) | (unsigned)__builtin_amdgcn_readlane(e.z, q);
-        const uint64_t o0 = sc_readlane64(o1, q) - cnt;
+        const unsigned L = i >> 2, u = i & 3u;
+        uint64_t o0 = E + sc_readlane64(ex, L);
+        if (u > 0) o0 += sc_readlane64(c[0], L);
+        if (u > 1) o0 += sc_readlane64(c[1], L);
+        if (u > 2) o0 += sc_readlane64(c[2], L);
         const uint8_t *sb = w16 ? reinterpret_cast<const uint8_t *>(a.staging16 + src) : reinterpret_cast<const uint8_t *>(a.staging + src);
         const unsigned al = (unsigned)((uintptr_t)sb & 3u);   // (a dword-aligned resource base)
         const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)(sb - al), (short)0, (int)(al + cnt * (w16 ? 2u : 4u)), 0x00020000);
@@ -925,20 +912,21 @@ __device__ __noinline__ void sc_copy_run(ConstKernArgs *kp, unsigned bid, unsign
         for (unsigned k0 = 0; k0 < cnt; k0 += 256u) {
             int32_t v[4];
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const unsigned k = k0 + 64u * (unsigned)u + lane;
+            for (int u2 = 0; u2 < 4; u2++) {
+                const unsigned k = k0 + 64u * (unsigned)u2 + lane;
                 // aux 16: sc1 (past cnt the range check reads 0)
-                v[u] = w16 ? (int32_t)(int16_t)__builtin_amdgcn_raw_buffer_load_b16(r, al + 2u * k, 0, 16)
-                           : (int32_t)__builtin_amdgcn_raw_buffer_load_b32(r, al + 4u * k, 0, 16);
+                v[u2] = w16 ? (int32_t)(int16_t)__builtin_amdgcn_raw_buffer_load_b16(r, al + 2u * k, 0, 16)
+                            : (int32_t)__builtin_amdgcn_raw_buffer_load_b32(r, al + 4u * k, 0, 16);
             }
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const unsigned k = k0 + 64u * (unsigned)u + lane;
-                if (k < cnt) dst[k] = v[u];
+            for (int u2 = 0; u2 < 4; u2++) {
+                const unsigned k = k0 + 64u * (unsigned)u2 + lane;
+                if (k < cnt) dst[k] = v[u2];
             }
         }
     }
-    if (lane < npop) atomicAdd(&a.copied[e.x / FIN_BATCH], 1u);
+    if (lane == 0) atomicAdd(a.copied + (size_t)b * (2 * BS_LINE), npop);
+    return npop;
 }
 
 // SW: staged id width 0 = by a.staging16, 1 = int16, 2 = int32; RAW: DPT_MODE_RAW as a compile-time
@@ -1079,7 +1067,8 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
         const unsigned n = (qt - qh) & 0xFFu;
         if (!n) return 0;
         if (!draining && n < SC_MIN_QUEUE) return 0;   // (a step costs round trips: every few rounds)
-        const unsigned npop = sc_ready(kp, bid, qh, n, lane);
+        unsigned long long E = 0;
+        unsigned npop = sc_ready(kp, bid, qh, n, lane, &E);
         if (npop == ~0u) {   // a string before them went to a later pass: the finish pass copies the queue's strings
             if (lane == 0) SSr(0).qh = (uint8_t)qt;
             return 0;
@@ -1091,7 +1080,7 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                 n_pend = 0;
             }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's staging stores are out
-        sc_copy_run(kp, bid, qh, npop, lane, SW == 1 || (SW == 0 && a.staging16 != nullptr));
+        npop = sc_copy_run(kp, bid, qh, npop, lane, SW == 1 || (SW == 0 && a.staging16 != nullptr), uni64(E));
         if (lane == 0) SSr(0).qh = (uint8_t)(qh + npop);
         return npop;
     };
@@ -1127,7 +1116,7 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                         const unsigned k = (unsigned)__builtin_popcount(rem & ((1u << lane) - 1u));
                         if (k < got) {
                             const uint64_t idx = nb + k;
-                            const uint64_t s = BIG ? (uint64_t)a.work_list[idx] : part_string(npart, cp, (unsigned)idx);
+                                                        const uint64_t s = BIG ? (uint64_t)a.work_list[idx] : part_string(npart, cp, (unsigned)idx);
                             const uint64_t o0 = a.str_off[s], o1 = a.str_off[s + 1];
                             SlotState &S = SSr(lane);
                             S.s = (uint32_t)s; S.sb = o0 - base_off; S.slen = (uint32_t)(o1 - o0); S.pos = 0; S.active = 1;
@@ -1189,7 +1178,8 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                             atomicMax(a.route_c, ~b);
                         } else {
                             st_agent(reinterpret_cast<unsigned long long *>(a.counts) + s, (unsigned long long)a.sc_epoch << 32);
-                            atomicAdd(&a.copied[b], 1u);   // nothing to copy
+                            atomicAdd(a.bsum + (size_t)b * BS_LINE, 1ull << BS_FIN_SHIFT);   // finished here
+                            atomicAdd(a.copied + (size_t)b * (2 * BS_LINE), 1u);           // nothing to copy
                         }
                     } else {
                         a.counts[s] = 0;
@@ -2618,12 +2608,13 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                     a.status[s] = (int32_t)S.status;
                     if (a.capped) a.capped[s] = S.status == 3 ? -1 : (int32_t)S.capsum;
                     S.active = 0;
-                    if (a.bsum && cnt) atomicAdd(&a.bsum[s / FIN_BATCH], (unsigned long long)cnt);
-                    if (!BIG && SC_ON && a.inc) {
-                        // the count tagged with the call's epoch: the batch is complete when all its
-                        // counts carry the tag (sc_publish_at)
+                    // (self-copy: every string finished here counts, sc_prefix)
+                    const bool sc = !BIG && SC_ON && a.inc;
+                    if (a.bsum && (cnt || sc)) atomicAdd(a.bsum + (s / FIN_BATCH) * BS_LINE, cnt | (sc ? 1ull << BS_FIN_SHIFT : 0ull));
+                    if (sc) {
+                        // the count tagged with the call's epoch: the tag says it has landed (sc_copy_run)
                         st_agent(reinterpret_cast<unsigned long long *>(a.counts) + s, ((unsigned long long)a.sc_epoch << 32) | cnt);
-                        if (!cnt) atomicAdd(&a.copied[s / FIN_BATCH], 1u);   // nothing to copy
+                        if (!cnt) atomicAdd(a.copied + (s / FIN_BATCH) * (2 * BS_LINE), 1u);   // nothing to copy
                         fq = cnt != 0;
                         fq_s = (unsigned)s;
                         fq_n = (unsigned)cnt;
@@ -2635,6 +2626,7 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
             }
         }
         wave_sync();
+        STAMP(4);
         if (!BIG && SC_ON && a.inc) {
             // queue the strings that finished with ids (the rest of a full queue stays for the finish pass),
             // then one step of the queue
@@ -2652,7 +2644,7 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
             (void)sc_step(false);
             wave_sync();
         }
-        STAMP(4);
+        STAMP(8);
     }
     if constexpr (G == 16 && !BIG)
         if (n_pend) {
@@ -2672,6 +2664,7 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
             __builtin_amdgcn_s_sleep(8);
         }
     }
+    STAMP(9);
     STAMP_FLUSH;
 #undef a
 #undef tv
@@ -2740,7 +2733,7 @@ __device__ __forceinline__ void reset_counters(uint32_t *ctr, uint64_t *snap = n
 
 // Batch prefixes: the tokenize passes add every string's count to its FIN_BATCH-string batch's sum
 // as the string finishes (one no-return atomic per string, dpt_kernels.hip / dpt_long.hip); this ONE
-// block turns bsum[0..nb) into exclusive prefixes bpre[0..nb) (thread i over a contiguous chunk:
+// block turns the batch sums (one per BS_LINE) into exclusive prefixes bpre[0..nb) (thread i over a contiguous chunk:
 // chunk sums, one block scan, the chunk again), zeroes bsum for the next call and resets the counter
 // block -- every tokenize pass has finished when it runs.  It replaces round 2's decoupled look-back
 // inside a persistent finish kernel, which chained the batches: a finish block could not start its
@@ -2758,13 +2751,13 @@ __global__ void __launch_bounds__(SCAN_THREADS) batch_scan_kernel(uint64_t n_str
     const uint64_t per = (nb + SCAN_THREADS - 1) / SCAN_THREADS;
     const uint64_t c0 = (uint64_t)tid * per < nb ? (uint64_t)tid * per : nb, c1 = c0 + per < nb ? c0 + per : nb;
     uint64_t sum = 0;
-    for (uint64_t k = c0; k < c1; k++) sum += bsum[k] & BS_SUM_MASK;
+    for (uint64_t k = c0; k < c1; k++) sum += bsum[k * BS_LINE] & BS_SUM_MASK;
     uint64_t total;
     uint64_t run = block_incl_scan_add64<SCAN_THREADS>(sum, s_w, &total) - sum;
     for (uint64_t k = c0; k < c1; k++) {
-        const uint64_t b = bsum[k] & BS_SUM_MASK;
+        const uint64_t b = bsum[k * BS_LINE] & BS_SUM_MASK;
         bpre[k] = run;
-        bsum[k] = 0;
+        bsum[k * BS_LINE] = 0;
         run += b;
     }
     if (tid == 0) reset_counters(ctr, ctr_snap);
@@ -2781,15 +2774,15 @@ struct FinishArgs {
     unsigned slices;                  // blocks per batch
     unsigned long long *bsum;         // one-batch calls (no scan kernel): zeroed here ...
     uint32_t *ctr;                    // ... and the counter block reset here (null when the scan kernel ran)
-    const unsigned long long *fold;   // fin_fold calls: the batch sums, summed here per block (else null) ...
-    unsigned long long *fold_zero;    // ... while the other array is zeroed for the next call
-    uint64_t fold_n;                  // (its entries)
+    const unsigned long long *fold;   // fin_fold calls: the batch sums (BS_LINE apart), summed here per block (else null) ...
+    unsigned long long *fold_zero;    // ... while the other parity's batch lines are zeroed for the next call
+    uint64_t fold_n;                  // (its batches)
     unsigned long long *hist;         // nullable: the token-count histogram (dpt_ctx_set_histogram) ...
     int hist_store;                   // ... stored, not added (DPT_HIST_OVERWRITE in a one-batch call) ...
     const int32_t *status;            // ... with the statuses it counts
     uint32_t n_bins;
-    unsigned long long *inc;          // self-copy calls (finish_kernel<ST, true>): per batch SC_* flags + prefix
-    const uint32_t *copied;           // ... and the strings the first pass copied into place
+    unsigned long long *inc;          // self-copy calls (finish_kernel<ST, true>): per batch SC_PUB + prefix (BS_LINE apart)
+    const uint32_t *copied;           // ... and the strings the first pass copied into place (2 BS_LINE apart)
     uint64_t *ctr_snap;               // nullable: the counter block's first 64 bytes before the reset (reset_counters)
 };
 
@@ -2800,9 +2793,9 @@ struct FinishArgs {
 // per thread.  At 1M strings a batch is one block (3 907 blocks); small calls split each batch's copy
 // so the grid still has ~FIN_TARGET_BLOCKS blocks (a block's copy is a chain of dependent load rounds:
 // 125k strings were 489 blocks of 7 rounds each).
-// SC (self-copy calls): batches the first pass fully copied (SC_OFS and every string copied) only count
-// their histogram; the others take their first id from a look-back -- the nearest published prefix back
-// plus the final batch sums after it -- publish their own, and are copied here as usual.
+// SC (self-copy calls): every batch takes its first id from a look-back -- the nearest prefix the first
+// pass or another block published, plus the final batch sums after it -- publishes its own and writes
+// its id_off entries; the ids of batches the first pass did not copy whole are copied here as usual.
 template <typename ST, bool SC = false>
 __global__ void __launch_bounds__(FIN_THREADS) finish_kernel(FinishArgs f) {
     __shared__ uint64_t s_rel[FIN_BATCH + 1];   // ids of the batch's strings before string k, + the batch total
@@ -2824,24 +2817,23 @@ __global__ void __launch_bounds__(FIN_THREADS) finish_kernel(FinishArgs f) {
     bool done = false;   // SC: the first pass copied the whole batch
     if constexpr (SC) {
         for (uint64_t k = (uint64_t)blockIdx.x * FIN_THREADS + tid; k < f.fold_n; k += (uint64_t)gridDim.x * FIN_THREADS)
-            f.fold_zero[k] = 0;   // the other parity's arrays, for the next call
-        const unsigned long long iv = __hip_atomic_load(&f.inc[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (unsigned w = 0; w <= BS_COPIED; w++) f.fold_zero[k * BS_LINE + w] = 0;   // the other parity's lines, for the next call
         const uint64_t nsz = f.n_str - s0 < FIN_BATCH ? f.n_str - s0 : FIN_BATCH;
-        done = (iv & SC_OFS) && f.copied[t] == nsz;
-        if (!done) {
+        done = f.copied[t * (2 * BS_LINE)] == nsz;
+        {
             // look-back: the ids before batch t = the nearest published inclusive prefix + the sums after it
             uint64_t acc = 0;
             for (uint64_t top = t;;) {
                 const int64_t k = (int64_t)top - 1 - (int64_t)tid;
                 unsigned long long pv = SC_PUB;   // k < 0: before the first batch, prefix 0
-                if (k >= 0) pv = __hip_atomic_load(&f.inc[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (k >= 0) pv = __hip_atomic_load(&f.inc[k * BS_LINE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (tid == 0) s_pub = FIN_THREADS;
                 __syncthreads();
                 if (pv & SC_PUB) atomicMin(&s_pub, tid);
                 __syncthreads();
                 const unsigned l0 = s_pub;
                 uint64_t part = 0, sum = 0;
-                if (tid < l0 && k >= 0) part = f.fold[k] & BS_SUM_MASK;
+                if (tid < l0 && k >= 0) part = f.fold[k * BS_LINE] & BS_SUM_MASK;
                 (void)block_incl_scan_add64<FIN_THREADS>(part, s_w, &sum);
                 acc += sum;
                 if (l0 < FIN_THREADS) {
@@ -2856,10 +2848,10 @@ __global__ void __launch_bounds__(FIN_THREADS) finish_kernel(FinishArgs f) {
         }
     } else if (f.fold) {   // the batch's first id: the sums of the batches before it (t <= FIN_FOLD_MAX)
         uint64_t ps = 0;
-        for (uint64_t k = tid; k < t; k += FIN_THREADS) ps += f.fold[k] & BS_SUM_MASK;
+        for (uint64_t k = tid; k < t; k += FIN_THREADS) ps += f.fold[k * BS_LINE] & BS_SUM_MASK;
         (void)block_incl_scan_add64<FIN_THREADS>(ps, s_w, &o0);
         for (uint64_t k = (uint64_t)blockIdx.x * FIN_THREADS + tid; k < f.fold_n; k += (uint64_t)gridDim.x * FIN_THREADS)
-            f.fold_zero[k] = 0;
+            for (unsigned w = 0; w <= BS_COPIED; w++) f.fold_zero[k * BS_LINE + w] = 0;   // (a self-copy call's too)
     } else if (!f.bsum) {
         o0 = f.bpre[t];
     }
@@ -2899,14 +2891,8 @@ __global__ void __launch_bounds__(FIN_THREADS) finish_kernel(FinishArgs f) {
             else if (lh[b]) atomicAdd(&f.hist[b], lh[b]);
         }
     }
-    if (SC && done) {   // the first pass wrote the batch's offsets and ids
-        if (t == 0 && tid == 0 && sl == 0) {
-            f.id_off[0] = 0;
-            reset_counters(f.ctr, f.ctr_snap);
-        }
-        return;
-    }
-    if (SC && sl == 0 && tid == 0) atomicOr(&f.inc[t], SC_PUB | (o0 + total));   // for the later batches' look-backs
+    if (SC && sl == 0 && tid == 0)   // for the later batches' look-backs (the first pass may have stored the same)
+        __hip_atomic_store(&f.inc[t * BS_LINE], SC_PUB | (o0 + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (sl == 0) {
         if (has) f.id_off[s0 + tid + 1] = o0 + incl;
         if (t == 0 && tid == 0) {
@@ -2916,6 +2902,7 @@ __global__ void __launch_bounds__(FIN_THREADS) finish_kernel(FinishArgs f) {
             if (f.ctr) reset_counters(f.ctr, f.ctr_snap);
         }
     }
+    if (SC && done) return;   // the first pass copied the batch's ids
     const uint64_t k_beg = total * sl / f.slices, k_end = total * (sl + 1) / f.slices;
     constexpr unsigned U = FIN_U;
     // the string of this thread's first id: the last string whose start is <= it (binary search;
@@ -3292,13 +3279,14 @@ hipError_t kernel_init() {
 }
 
 int small_window_bytes() { return SMALL_CH; }
+bool self_copy_built() { return SC_ON; }
 int big_window_bytes() { return BIG_CH; }
 
 #ifdef DPT_STAMPS
 extern "C" int dpt_debug_stamps(unsigned long long *out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 10) != hipSuccess) return -1;
     if (reset) {
-        unsigned long long z[8] = {0};
+        unsigned long long z[10] = {0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z)) != hipSuccess) return -1;
     }
     return 0;

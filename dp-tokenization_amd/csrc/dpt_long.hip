@@ -547,7 +547,7 @@ __device__ __forceinline__ void long_body(const Args &a) {
         if (lane == 0) {
             a.status[s] = (int32_t)status;
             a.counts[s] = (status == 0 && !len_only) ? (uint64_t)total : 0ull;
-            if (a.bsum && status == 0 && !len_only && total) atomicAdd(&a.bsum[s / FIN_BATCH], (unsigned long long)total);
+            if (a.bsum && status == 0 && !len_only && total) atomicAdd(&a.bsum[(s / FIN_BATCH) * BS_LINE], (unsigned long long)total);
             if (a.capped) a.capped[s] = status == 3 ? -1 : (int32_t)capsum;
         }
         phase_sync();

@@ -115,11 +115,14 @@ int dpt_ctx_workspace_bytes(const dpt_ctx *c, uint64_t *device_path, uint64_t *h
 int dpt_ctx_long_need(dpt_ctx *c, uint64_t *need, uint64_t *cap);
 /* ABI 3.  After the ctx's last dpt_encode / dpt_encode_host has completed (synchronise its stream
  * first): the strings whose ids the first tokenize pass copied into the CSR arrays itself (*copied,
- * strings without ids included; the finish pass copies the others), the 256-string batches whose
- * offsets it wrote (*batches_ofs) and the call's batches (*n_batches).  All 0 when the call did not
- * self-copy (fewer than 8 batches, dpt_encode_padded / dpt_dp_host*, or DPT_SELF_COPY=0 in the
- * environment -- an A/B switch read per call). */
-int dpt_ctx_copy_stats(dpt_ctx *c, uint64_t *copied, uint64_t *batches_ofs, uint64_t *n_batches);
+ * strings without ids included; the finish pass copies the others), the 256-string batches it
+ * copied whole (*batches_whole) and the call's batches (*n_batches).  All 0 when the call did not
+ * self-copy: it is opt-in (DPT_SELF_COPY=1 in the environment, read per call) in a library built with
+ * it (dpt_self_copy_available), and never for calls of fewer than 8 batches, dpt_encode_padded or
+ * dpt_dp_host*.  Measured slower than the finish pass's copy: an experiment, off by default. */
+int dpt_ctx_copy_stats(dpt_ctx *c, uint64_t *copied, uint64_t *batches_whole, uint64_t *n_batches);
+/* 1 when the library was built with the first pass's self-copy (csrc/Makefile `sc`), else 0. */
+int dpt_self_copy_available(void);
 
 /*
  * Tokenize n_str strings, CSR-packed: string s is text[str_off[s]-str_off[0] .. str_off[s+1]-str_off[0]),
