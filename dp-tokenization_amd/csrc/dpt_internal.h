@@ -43,6 +43,9 @@ struct EncodeLaunch {
     uint32_t sc_epoch;           // self-copy: the call's tag for its counts (never 0)
     uint64_t *ctr_snap;          // nullable (host path): the counter block's first 64 bytes, copied here by its reset
     bool no_fallback;            // the host checked that no string needs the 2048-byte or unbounded pass: skip them
+    bool solo;                   // one-string host-path call without fallbacks, histogram, edges or profiling: the first
+                                 //   pass writes the CSR arrays itself (ids at 0.., id_off = {0, count}) and resets
+                                 //   the counter block (its snapshot to ctr_snap); nothing else is launched
     unsigned max_blocks;
     int variant;             // KERNEL_* below
     bool padded;             // dpt_encode_padded: staging = the caller's ids, counts = the caller's; no finish pass

@@ -364,6 +364,11 @@ struct EncodeArgs {
     uint32_t *route_c;          // ~(first batch holding a string routed to a later pass), 0: none (atomicMax)
     uint64_t *id_off;
     int32_t *ids;
+    // one-string host-path calls (EncodeLaunch::solo): the string's ids go straight to ids (staging =
+    // ids, counts = id_off + 1) and the lone wave writes id_off[0] and resets the counter block (its
+    // first 64 bytes to ctr_snap) -- no fallback, scan or finish launch follows
+    int solo;
+    uint64_t *ctr_snap;
 };
 
 #ifdef DPT_STAMPS
@@ -789,6 +794,34 @@ __device__ __forceinline__ TrieView tv_of(ConstKernArgs *kp) {
 }
 // (the 16-lane instantiations: the 64-lane ones do not spill, and measured 1.7 % slower with it)
 #define KREFRESH() do { if constexpr (G == 16) asm volatile("" : "+s"(kp)); } while (0)
+
+// Counter block (EncodeLaunch::retry_count, CTR_ALLOC_BYTES; zeroed once at allocation, then reset for
+// the next call by the batch scan or the finish pass -- or, in a one-string host-path call, by the lone
+// wave of the first pass): uint32 [0] retry count, [1] 2048-byte blocks done (fallback_kernel), [2]
+// 2048-byte pass work, [3] long count, [4] long work, [5] self-copy route mark, [6] fallback_kernel's
+// block ticket; uint64 [4] (byte
+// 32) the unbounded pass's claimed bytes, [5] (byte 40) the last call's claimed bytes
+// (dpt_ctx_long_need), [6] (byte 48) far edge pairs found, [7] (byte 56) the last call's far edge pairs
+// (dpt_dp_host_far); from byte PART_CTR_OFFSET the first pass's partition counters and their used-up
+// mask (dpt_internal.h).
+constexpr unsigned CTR_ARENA64 = 4, CTR_LASTNEED64 = 5, CTR_FAR64 = 6, CTR_LASTFAR64 = 7;
+
+// Reset the counter block for the next call (the claimed arena bytes and far pairs stay readable as
+// the call's "last need" / "last far").
+// snap (nullable): the block's first 64 bytes as the host reads them after the call (the host path's
+// one device-to-host copy carries them, instead of a copy of the counter block of its own)
+__device__ __forceinline__ void reset_counters(uint32_t *ctr, uint64_t *snap = nullptr) {
+    uint64_t *c64 = reinterpret_cast<uint64_t *>(ctr);
+    c64[CTR_LASTNEED64] = c64[CTR_ARENA64];
+    c64[CTR_ARENA64] = 0;
+    c64[CTR_LASTFAR64] = c64[CTR_FAR64];
+    c64[CTR_FAR64] = 0;
+    if (snap)
+        for (unsigned q = 0; q < 8; q++) snap[q] = c64[q];
+    ctr[0] = 0; ctr[1] = 0; ctr[2] = 0; ctr[3] = 0; ctr[4] = 0; ctr[5] = 0; ctr[6] = 0;
+    uint32_t *pc = ctr + PART_CTR_OFFSET / 4;
+    for (unsigned q = 0; q <= NPART; q++) pc[q * PART_STRIDE] = 0;   // the partition counters and the mask
+}
 
 // ---- self-copy (first pass of CSR calls, a.inc != nullptr).  The finish pass used to copy every
 // staged id into the CSR arrays after this kernel (0.33 ms, 13 % of a cfg2 step, half its HBM
@@ -2664,6 +2697,10 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
             __builtin_amdgcn_s_sleep(8);
         }
     }
+    if (!BIG && a.solo && lane == 0) {   // the call's only string, the grid's only wave
+        a.id_off[0] = 0;
+        reset_counters(a.retry_count, a.ctr_snap);
+    }
     STAMP(9);
     STAMP_FLUSH;
 #undef a
@@ -2680,14 +2717,6 @@ tokenize_kernel(KernArgs ka) {
 
 // ------------------------------------------------------------------ finish: offsets + CSR ids in one pass
 
-// Counter block (EncodeLaunch::retry_count, CTR_ALLOC_BYTES; zeroed once at allocation, then reset for
-// the next call by batch_scan_kernel, which runs after every tokenize pass): uint32 [0] retry count,
-// [1] unused, [2] 2048-byte pass work, [3] long count, [4] long work, [5], [6] unused; uint64 [4] (byte
-// 32) the unbounded pass's claimed bytes, [5] (byte 40) the last call's claimed bytes
-// (dpt_ctx_long_need), [6] (byte 48) far edge pairs found, [7] (byte 56) the last call's far edge pairs
-// (dpt_dp_host_far); from byte PART_CTR_OFFSET the first pass's partition counters and their used-up
-// mask (dpt_internal.h).
-constexpr unsigned CTR_ARENA64 = 4, CTR_LASTNEED64 = 5, CTR_FAR64 = 6, CTR_LASTFAR64 = 7;
 constexpr unsigned FIN_U = 16;                // loads in flight per thread of the copy
 constexpr unsigned FIN_THREADS = 512;         // threads per finish block (>= FIN_BATCH): all of them copy
 constexpr unsigned SCAN_THREADS = 1024;       // threads of the batch-scan block
@@ -2714,22 +2743,6 @@ __device__ __forceinline__ uint64_t block_incl_scan_add64(uint64_t v, uint64_t *
     return incl;
 }
 
-// Reset the counter block for the next call (the claimed arena bytes and far pairs stay readable as
-// the call's "last need" / "last far").
-// snap (nullable): the block's first 64 bytes as the host reads them after the call (the host path's
-// one device-to-host copy carries them, instead of a copy of the counter block of its own)
-__device__ __forceinline__ void reset_counters(uint32_t *ctr, uint64_t *snap = nullptr) {
-    uint64_t *c64 = reinterpret_cast<uint64_t *>(ctr);
-    c64[CTR_LASTNEED64] = c64[CTR_ARENA64];
-    c64[CTR_ARENA64] = 0;
-    c64[CTR_LASTFAR64] = c64[CTR_FAR64];
-    c64[CTR_FAR64] = 0;
-    if (snap)
-        for (unsigned q = 0; q < 8; q++) snap[q] = c64[q];
-    ctr[0] = 0; ctr[1] = 0; ctr[2] = 0; ctr[3] = 0; ctr[4] = 0; ctr[5] = 0; ctr[6] = 0;
-    uint32_t *pc = ctr + PART_CTR_OFFSET / 4;
-    for (unsigned q = 0; q <= NPART; q++) pc[q * PART_STRIDE] = 0;   // the partition counters and the mask
-}
 
 // Batch prefixes: the tokenize passes add every string's count to its FIN_BATCH-string batch's sum
 // as the string finishes (one no-return atomic per string, dpt_kernels.hip / dpt_long.hip); this ONE
@@ -3101,6 +3114,14 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     a.inc = p.self_copy ? p.inc : nullptr; a.copied = p.copied; a.cq = p.cq; a.sc_epoch = p.sc_epoch;
     a.route_c = p.retry_count + 5;   // (counter block uint32 [5]: reset_counters zeroes it)
     a.id_off = p.id_off; a.ids = p.ids;
+    a.solo = p.solo ? 1 : 0; a.ctr_snap = p.ctr_snap;
+    const bool solo = p.solo && p.n_str == 1 && !p.padded;
+    int16_t *const st16 = solo ? nullptr : p.staging16;   // (the 16-lane launch below picks the width by it)
+    if (solo) {
+        a.staging = p.ids; a.staging16 = nullptr; a.counts = p.id_off + 1; a.bsum = nullptr;
+    } else {
+        a.solo = 0;
+    }
     TrieView tv{p.slots, p.slot_ids, p.slots4, p.root_base, p.n_slots, p.pair16};
     const bool wide = (p.mode & DPT_MODE_MASK) == DPT_MODE_ATOMS;   // atoms of up to 8 bytes
     const bool raw = (p.mode & DPT_MODE_MASK) == DPT_MODE_RAW;
@@ -3127,21 +3148,26 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
                 // the hot kernel gets the staged id width as a template constant
                 const uint64_t nu = (p.n_str + 3) / 4;
                 if (wide) {
-                    if (p.staging16) launch_tok<SMALL_CH, 16, false, true, 1>(a, tv, nu, n_cu, stream, e0);
+                    if (st16) launch_tok<SMALL_CH, 16, false, true, 1>(a, tv, nu, n_cu, stream, e0);
                     else launch_tok<SMALL_CH, 16, false, true, 2>(a, tv, nu, n_cu, stream, e0);
                 } else if (raw) {
-                    if (p.staging16) launch_tok<SMALL_CH, 16, false, false, 1, true>(a, tv, nu, n_cu, stream, e0);
+                    if (st16) launch_tok<SMALL_CH, 16, false, false, 1, true>(a, tv, nu, n_cu, stream, e0);
                     else launch_tok<SMALL_CH, 16, false, false, 2, true>(a, tv, nu, n_cu, stream, e0);
                 } else {
-                    if (p.staging16) launch_tok<SMALL_CH, 16, false, false, 1>(a, tv, nu, n_cu, stream, e0);
+                    if (st16) launch_tok<SMALL_CH, 16, false, false, 1>(a, tv, nu, n_cu, stream, e0);
                     else launch_tok<SMALL_CH, 16, false, false, 2>(a, tv, nu, n_cu, stream, e0);
                 }
             } else {
+#if DPT_STOP == 3   // (this diagnostic build crashes ROCm 7.2's register allocator on the 64-lane first pass)
+                return hipErrorNotSupported;
+#else
                 if (wide) launch_tok<SMALL_CH, 64, false, true>(a, tv, p.n_str, n_cu, stream, e0);
                 else if (raw) launch_tok<SMALL_CH, 64, false, false, 0, true>(a, tv, p.n_str, n_cu, stream, e0);
                 else launch_tok<SMALL_CH, 64, false, false>(a, tv, p.n_str, n_cu, stream, e0);
+#endif
             }
         }
+        if (solo) return hipGetLastError();   // the lone wave did the rest
         // second pass over the strings whose single word (or expansion) did not fit the small window
         EncodeArgs b = a;
         b.work_list = p.retry_list; b.work_count = p.retry_count;

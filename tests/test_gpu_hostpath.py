@@ -69,3 +69,34 @@ def test_presplit_small_calls(vocabs):
         ref = orc.encode_csr(text, offs, mode=oracle.PRESPLIT, cut_mask=cut)
         for g, r, what in zip(got, ref, ("ids", "offsets", "status", "capped")):
             assert np.array_equal(g, r), (what, L)
+
+
+def test_one_string_calls(vocabs):
+    """One-string host-path calls run the first pass alone (EncodeLaunch::solo: ids straight into the
+    output, id_off and the counter reset by the lone wave): every mode, empty and untokenizable
+    strings, the 64-lane kernel's vocabulary, interleaved with multi-string calls on the same context
+    (a counter the lone wave failed to reset would show in the next call)."""
+    from dptok import Encoder, Vocab, pack_strings
+    from oracle import oracle
+    rng = np.random.default_rng(8)
+    t2i_long = dict(vocabs["llama32k"])
+    for L in (17, 24, 40):
+        for _ in range(10):
+            tok = "".join(chr(c) for c in rng.integers(0x61, 0x65, size=L))
+            t2i_long.setdefault(tok, len(t2i_long))
+    pool = [chr(c) for c in range(0x21, 0x7F)] + ["é", "中", "😀", "\n", " ", "  "]
+    texts = ["", " ", "a", "\n", "中文 😀", "abcd" * 40] + \
+            ["".join(rng.choice(pool, size=int(rng.integers(1, 250)))) for _ in range(40)] + \
+            ["".join(chr(c) for c in rng.integers(0x61, 0x65, size=200))]
+    for name, t2i in (("llama32k", vocabs["llama32k"]), ("toy1k", vocabs["toy1k"]), ("long", t2i_long)):
+        enc, orc = Encoder(Vocab(t2i, 0)), oracle.OracleVocab(t2i)
+        for k, s in enumerate(texts):
+            text, offs = pack_strings([s])
+            got, ref = enc.encode_csr(text, offs), orc.encode_csr(text, offs)
+            for g, r, what in zip(got, ref, ("ids", "offsets", "status", "capped")):
+                assert np.array_equal(g, r), (name, k, what, s[:30])
+            if k % 7 == 3:   # a multi-string call between one-string calls
+                text, offs = pack_strings(texts[:k + 2])
+                got, ref = enc.encode_csr(text, offs), orc.encode_csr(text, offs)
+                for g, r in zip(got, ref):
+                    assert np.array_equal(g, r), (name, k, "batch")

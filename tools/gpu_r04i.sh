@@ -9,3 +9,5 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout
 tail -3 $out/pytest_gpu.txt
 timeout -k 10 300 python bench.py > $out/bench.json 2> $out/bench.err || { tail -5 $out/bench.err; exit 1; }
 cut -c1-400 $out/bench.json
+timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d $out/pc -o pc --output-format csv -- python3 tools/percall_trace.py 300 > $out/pc.log 2>&1 || { tail -5 $out/pc.log; exit 1; }
+timeout -k 10 300 python tools/percall.py 2000 > $out/percall.json 2>&1 && cat $out/percall.json

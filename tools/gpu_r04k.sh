@@ -1,0 +1,15 @@
+#!/bin/bash
+# round 4: per-call A/B on one box (DPT_NO_SOLO: the finish kernel back), twice, and per-phase stamps of
+# a one-string call
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+out=gpurun_out/r04k; mkdir -p $out
+for r in 1 2; do
+  for v in solo nosolo; do
+    e=""; [ $v = nosolo ] && e="DPT_NO_SOLO=1"
+    env $e timeout -k 10 300 python tools/percall.py 3000 > $out/percall_${v}_$r.json 2>/dev/null || { echo fail; exit 1; }
+    echo $v $r; cat $out/percall_${v}_$r.json
+  done
+done
+STAMP_REPS=500 timeout -k 10 120 python3 tools/stamps.py 1 > $out/stamps_1.txt 2>&1 && cat $out/stamps_1.txt
