@@ -63,6 +63,7 @@ struct dpt_ctx {
     // host path: one device buffer in (text | offsets | cut) and one out (id_off | status | capped |
     // counters | ids | edges), each mirrored by a pinned host buffer so every copy is one async DMA
     uint8_t *d_in = nullptr, *p_in = nullptr, *d_out = nullptr, *p_out = nullptr;
+    uint8_t *pd_in = nullptr, *pd_out = nullptr;   // p_in / p_out as the device addresses them (zero-copy calls)
     uint64_t cap_in = 0, cap_pin_in = 0, cap_out = 0, cap_pin_out = 0;
     // dpt_ctx_set_histogram: folded into the next encode's finish pass
     int64_t *hist = nullptr;
@@ -750,14 +751,22 @@ static int encode_host_impl(dpt_ctx *c, const dpt_vocab *v, int mode, const uint
     const uint64_t out_bytes = o_far + (want_far ? 16 * far_cap : 0);
     if ((e = grow(&c->d_in, &c->cap_in, in_bytes)) != hipSuccess) return hip_fail(e, "hipMalloc(host-path in)");
     if ((e = grow(&c->d_out, &c->cap_out, out_bytes)) != hipSuccess) return hip_fail(e, "hipMalloc(host-path out)");
-    if ((e = grow_pinned(&c->p_in, &c->cap_pin_in, in_bytes)) != hipSuccess) return hip_fail(e, "hipHostMalloc(in)");
-    if ((e = grow_pinned(&c->p_out, &c->cap_pin_out, out_bytes)) != hipSuccess) return hip_fail(e, "hipHostMalloc(out)");
+    {
+        uint8_t *pi = c->p_in, *po = c->p_out;
+        if ((e = grow_pinned(&c->p_in, &c->cap_pin_in, in_bytes)) != hipSuccess) return hip_fail(e, "hipHostMalloc(in)");
+        if ((e = grow_pinned(&c->p_out, &c->cap_pin_out, out_bytes)) != hipSuccess) return hip_fail(e, "hipHostMalloc(out)");
+        if (pi != c->p_in || !c->pd_in) {
+            if ((e = hipHostGetDevicePointer((void **)&c->pd_in, c->p_in, 0)) != hipSuccess) return hip_fail(e, "hipHostGetDevicePointer");
+        }
+        if (po != c->p_out || !c->pd_out) {
+            if ((e = hipHostGetDevicePointer((void **)&c->pd_out, c->p_out, 0)) != hipSuccess) return hip_fail(e, "hipHostGetDevicePointer");
+        }
+    }
     if (n_bytes) memcpy(c->p_in, text, n_bytes);
     uint64_t *off = reinterpret_cast<uint64_t *>(c->p_in + o_off);
     for (uint64_t i = 0; i <= n_str; i++) off[i] = str_off[i] - str_off[0];
     if (cut) memcpy(c->p_in + o_cut, cut_mask, n_bytes);
     hipStream_t st = 0;
-    if ((e = hipMemcpyAsync(c->d_in, c->p_in, in_bytes, hipMemcpyHostToDevice, st)) != hipSuccess) return hip_fail(e, "H2D");
     uint64_t *d_idoff = reinterpret_cast<uint64_t *>(c->d_out);
     int32_t *d_status = reinterpret_cast<int32_t *>(c->d_out + o_st);
     int32_t *d_capped = reinterpret_cast<int32_t *>(c->d_out + o_cap);
@@ -774,6 +783,27 @@ static int encode_host_impl(dpt_ctx *c, const dpt_vocab *v, int mode, const uint
     const bool no_fb = n_bytes <= NO_FALLBACK_CHECK_BYTES && !edges && v->stats.max_cp <= 64 &&
                        no_fallback_needed(mode & DPT_MODE_MASK, text, str_off, cut ? cut_mask : nullptr, n_str);
     bool overflow = false;   // some strings got status 3 (arena full): they alone run again below
+    // One string with no fallback pass (a per-string dp_tokenize call): zero-copy -- its lone wave
+    // (EncodeLaunch::solo) reads the text from and writes the outputs to the pinned host buffers, so the
+    // call is one launch and a sync (two copies and their gaps less)
+    if (no_fb && n_str == 1 && !edges && !c->profile && !getenv("DPT_NO_SOLO")) {
+        int rc = encode_impl(c, v, mode, c->pd_in, n_bytes, reinterpret_cast<const uint64_t *>(c->pd_in + o_off),
+                             cut ? c->pd_in + o_cut : nullptr, n_str, reinterpret_cast<int32_t *>(c->pd_out + o_ids),
+                             n_bytes ? n_bytes : 1, reinterpret_cast<uint64_t *>(c->pd_out),
+                             reinterpret_cast<int32_t *>(c->pd_out + o_st), reinterpret_cast<int32_t *>(c->pd_out + o_cap),
+                             nullptr, st, nullptr, 0, nullptr, false, reinterpret_cast<uint64_t *>(c->pd_out + o_ctr), true);
+        if (rc) return rc;
+        if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(e, "sync");
+        const uint64_t total = p_idoff[1];
+        if (total > ids_cap || total > n_bytes) return fail(DPT_E_CAP, "ids overflow");
+        id_off[0] = 0;
+        id_off[1] = total;
+        status[0] = *reinterpret_cast<const int32_t *>(c->p_out + o_st);
+        if (capped_len) capped_len[0] = *reinterpret_cast<const int32_t *>(c->p_out + o_cap);
+        if (total) memcpy(ids, c->p_out + o_ids, 4 * total);
+        return DPT_OK;
+    }
+    if ((e = hipMemcpyAsync(c->d_in, c->p_in, in_bytes, hipMemcpyHostToDevice, st)) != hipSuccess) return hip_fail(e, "H2D");
     for (int attempt = 0;; attempt++) {
         int rc = encode_impl(c, v, mode, c->d_in, n_bytes, reinterpret_cast<const uint64_t *>(c->d_in + o_off),
                              cut ? c->d_in + o_cut : nullptr, n_str, d_ids, n_bytes ? n_bytes : 1, d_idoff, d_status,

@@ -204,7 +204,6 @@ struct LongLaunch {
     int long_span;
     unsigned blocks;
 };
-void launch_long(const LongLaunch &p, hipStream_t stream, hipEvent_t ev_stop = nullptr);
 
 hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t ev[2]);
 size_t wsl_scratch_bytes(unsigned max_blocks);

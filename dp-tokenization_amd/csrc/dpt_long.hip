@@ -196,7 +196,7 @@ __device__ bool span_is_token(const Args &a, const Str &S, unsigned j, unsigned 
     return false;
 }
 
-// (the body of long_kernel and of dpt_kernels.hip fallback_kernel's unbounded-pass blocks)
+// (the body of dpt_kernels.hip fallback_kernel's unbounded-pass blocks)
 __device__ __forceinline__ void long_body(const Args &a) {
     const unsigned lane = lane_id();
     const int mode = a.mode & DPT_MODE_MASK;
@@ -554,9 +554,7 @@ __device__ __forceinline__ void long_body(const Args &a) {
     }
 }
 
-__global__ void __launch_bounds__(64) long_kernel(Args a) { long_body(a); }
-
-// launch_long's arguments from a LongLaunch
+// the unbounded pass's arguments from a LongLaunch (fallback_kernel's unbounded-pass blocks)
 inline Args long_args(const LongLaunch &p) {
     Args a;
     a.text = p.text; a.str_off = p.str_off; a.cut_mask = p.cut_mask;
@@ -572,13 +570,5 @@ inline Args long_args(const LongLaunch &p) {
 }
 
 }  // namespace lng
-
-void launch_long(const LongLaunch &p, hipStream_t stream, hipEvent_t ev_stop) {
-    const lng::Args a = lng::long_args(p);
-    if (ev_stop)   // the end timestamp of the tokenize passes rides on this dispatch (dpt_ctx_profile)
-        hipExtLaunchKernelGGL(lng::long_kernel, dim3(p.blocks), dim3(64), 0, stream, nullptr, ev_stop, 0, a);
-    else
-        hipLaunchKernelGGL(lng::long_kernel, dim3(p.blocks), dim3(64), 0, stream, a);
-}
 
 }  // namespace dpt

@@ -13,3 +13,4 @@ for r in 1 2; do
   done
 done
 STAMP_REPS=500 timeout -k 10 120 python3 tools/stamps.py 1 > $out/stamps_1.txt 2>&1 && cat $out/stamps_1.txt
+timeout -k 10 300 python tools/overlap_probe.py 10 > $out/overlap.json 2>&1; tail -2 $out/overlap.json
