@@ -63,6 +63,9 @@ def parse():
                          "that follows forks)")
     ap.add_argument("--cpu-budget", type=float, default=25.0, help="seconds of CPU-baseline wall time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="ordinary calls: each step's CSR pass on the step's stream, after its tokenize passes "
+                         "(default: pipelined, dpt_ctx_pipeline -- the CSR pass runs beside the next step's tokenize)")
     ap.add_argument("--host-path", action="store_true",
                     help="instead of the headline line: the drop-in surface the reference's callers use "
                          "(dp_tokenize(str) per call and dp_tokenize.batch, raw and llama mode, cfg2 and cfg4)")
@@ -369,6 +372,12 @@ def main():
     d_hists = [torch.zeros(N_BINS + 8, dtype=torch.int64, device=dev) for _ in range(2)]
     pending = [None, None]
     n_step = [0]
+    # pipelined calls (dpt_ctx_pipeline): step k's CSR pass (ids, offsets, histogram) runs on csr_stream
+    # beside step k+1's tokenize passes; its histogram's all-reduce is issued on that stream too
+    pipelined = not args.no_pipeline
+    csr_stream = torch.cuda.Stream(dev) if pipelined else None
+    if pipelined:
+        enc.pipeline(csr_stream.cuda_stream)
     enc.reserve(n_bytes, M)
     stream = torch.cuda.current_stream(dev).cuda_stream
 
@@ -387,13 +396,20 @@ def main():
                           cut_ptr=d_cut.data_ptr() if bloom else 0, mode="atoms" if bloom else "raw")
         if coll:   # the single collective: RCCL over xGMI with nccl, gloo in rehearsals
             if red_dev.type == "cpu":
+                if pipelined:
+                    enc.join(stream)   # (the histogram is complete once the CSR pass is)
                 hc = h.cpu()
                 ddist.allreduce_histogram(hc)
                 h.copy_(hc)
+            elif pipelined:
+                with torch.cuda.stream(csr_stream):   # ordered after this step's CSR pass
+                    pending[b] = ddist.allreduce_histogram(h, async_op=True)
             else:
                 pending[b] = ddist.allreduce_histogram(h, async_op=True)
 
-    def drain():   # every outstanding all-reduce is ordered before what the stream does next
+    def drain():   # every outstanding CSR pass and all-reduce is ordered before what the stream does next
+        if pipelined:
+            enc.join(stream)
         for b in range(2):
             if pending[b] is not None:
                 pending[b].wait()
@@ -431,6 +447,31 @@ def main():
         dt = float(t.item())
     ms_stage, launches = enc.profile_read()
     enc.profile(False)
+    # the same steps as ordinary calls (each CSR pass after its own tokenize passes), for the record
+    ms_off = None
+    if pipelined:
+        enc.pipeline(0)
+        pipelined = False
+        for _ in range(2):
+            step()
+        drain()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0o = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        drain()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dto = time.perf_counter() - t0o
+        if world > 1:
+            t = torch.tensor([dto], dtype=torch.float64, device=red_dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dto = float(t.item())
+        ms_off = dto / args.steps * 1e3
+        pipelined = True
     # the last timed call's self-copy (dpt_ctx_copy_stats): strings its first pass copied into the CSR
     # arrays itself, batches whose offsets it wrote (the finish pass copied the rest)
     sc_copied, sc_batches, sc_nb = enc.copy_stats()
@@ -545,8 +586,12 @@ def main():
                          "alg_bytes_staged_width": alg_staged, "staged_id_bytes": id_bytes,
                          "frac_staged_width": alg_staged / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
             "cpu_baseline": cpu,
+            "csr_pipeline": {"on": ms_off is not None, "api": "dpt_ctx_pipeline / dpt_ctx_join",
+                             "what": "each step's CSR pass (LDS-free finish_lite_kernel) on a second stream, beside the "
+                                     "next step's tokenize passes; every step's outputs complete inside the timed region",
+                             "ms_per_step_ordinary_calls": ms_off},
             "self_copy": {"strings_copied_by_first_pass": sc_copied, "strings": M, "batches_copied_whole": sc_batches,
-                          "batches": sc_nb, "enabled": os.environ.get("DPT_SELF_COPY", "1") != "0"},
+                          "batches": sc_nb, "enabled": os.environ.get("DPT_SELF_COPY") == "1"},
             "padded_layout": {"api": "dpt_encode_padded (ids at each string's byte offset + per-string counts, no CSR pass); encode only, no histogram",
                               "ms_per_step": dtp / args.steps * 1e3, "bytes_per_s": bytes_all * args.steps / dtp,
                               "counts_and_status_equal_csr": padded_same},

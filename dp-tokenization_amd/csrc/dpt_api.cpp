@@ -10,6 +10,7 @@
 
 #include <atomic>
 #include <string>
+#include <utility>
 #include <unordered_map>
 #include <vector>
 
@@ -30,6 +31,23 @@ struct dpt_vocab {
 };
 
 static uint64_t flag_words(uint64_t cap_batches) { return cap_batches * (2 * dpt::BS_LINE + 1); }
+
+// What a call's CSR pass reads or resets -- staged ids, counts, batch lines, the counter block (and the
+// retry lists with them): pipelined calls (dpt_ctx_pipeline) alternate between the ctx's own set and
+// a second one, so call k+1's first pass never writes what call k's CSR pass is still reading.
+struct WsSet {
+    int32_t *staging32 = nullptr;
+    uint64_t cap32 = 0;
+    int16_t *staging16 = nullptr;
+    uint64_t cap16 = 0;
+    uint64_t *counts = nullptr;
+    uint32_t *retry_list = nullptr;
+    uint64_t cap_str = 0;
+    unsigned long long *flags = nullptr;
+    uint64_t cap_batches = 0;
+    int flag_parity = 0;
+    uint32_t *retry_count = nullptr;
+};
 
 struct dpt_ctx {
     int device = 0;
@@ -69,6 +87,12 @@ struct dpt_ctx {
     int64_t *hist = nullptr;
     uint32_t hist_bins = 0;
     bool hist_overwrite = false;
+    // pipelined calls (dpt_ctx_pipeline): the CSR pass on `pipe`; the other workspace set; ev_fin[k]:
+    // recorded after the last CSR pass that read set k (cur: the set in the fields above)
+    hipStream_t pipe = nullptr;
+    WsSet other;
+    hipEvent_t ev_tok = nullptr, ev_fin[2] = {nullptr, nullptr};
+    int cur = 0;
     // profiling
     bool profile = false;
     std::vector<hipEvent_t> events;   // groups of 4 per call
@@ -137,6 +161,17 @@ uint64_t default_long_bytes(uint64_t n_bytes) {
 
 constexpr uint64_t ARENA_PER_BYTE = 20;   // uint4 rec + int32 stg (dpt_long.hip)
 constexpr size_t COUNTER_BYTES = 64;
+
+// Exchange the ctx's workspace set with the other one (pipelined calls)
+void swap_set(dpt_ctx *c) {
+    WsSet &o = c->other;
+    std::swap(c->staging32, o.staging32); std::swap(c->cap32, o.cap32);
+    std::swap(c->staging16, o.staging16); std::swap(c->cap16, o.cap16);
+    std::swap(c->counts, o.counts); std::swap(c->retry_list, o.retry_list); std::swap(c->cap_str, o.cap_str);
+    std::swap(c->flags, o.flags); std::swap(c->cap_batches, o.cap_batches); std::swap(c->flag_parity, o.flag_parity);
+    std::swap(c->retry_count, o.retry_count);
+    c->cur ^= 1;
+}
 
 // v == nullptr: both staging widths (the vocabulary is not known yet); staging = false: no staging
 // (dpt_encode_padded writes the ids into the caller's buffer)
@@ -473,13 +508,18 @@ int dpt_ctx_create(int device, dpt_ctx **out) {
 int dpt_ctx_destroy(dpt_ctx *c) {
     if (!c) return DPT_OK;
     DeviceGuard g(c->device);
+    if (c->pipe) (void)hipDeviceSynchronize();   // (a CSR pass may still read the sets)
+    const WsSet &o = c->other;
     void *ps[] = {c->staging32, c->staging16, c->arena, c->counts, c->retry_list, c->retry_count, c->wsl_scratch,
-                  c->pend, c->cq, c->flags, c->d_in, c->d_out};
+                  c->pend, c->cq, c->flags, c->d_in, c->d_out, o.staging32, o.staging16, o.counts, o.retry_list,
+                  o.flags, o.retry_count};
     for (void *p : ps)
         if (p) (void)hipFree(p);
     if (c->p_in) (void)hipHostFree(c->p_in);
     if (c->p_out) (void)hipHostFree(c->p_out);
     for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
+    for (hipEvent_t e : {c->ev_tok, c->ev_fin[0], c->ev_fin[1]})
+        if (e) (void)hipEventDestroy(e);
     delete c;
     return DPT_OK;
 }
@@ -492,9 +532,39 @@ int dpt_ctx_reserve_vocab(dpt_ctx *c, const dpt_vocab *v, uint64_t n_bytes, uint
     if (!c) return fail(DPT_E_ARG, "null ctx");
     if (v && v->device != c->device) return fail(DPT_E_ARG, "ctx and vocab on different devices");
     DeviceGuard g(c->device);
-    const int rc = ensure_workspace(c, v, n_bytes, n_str, long_bytes);
+    int rc = ensure_workspace(c, v, n_bytes, n_str, long_bytes);
+    if (rc == DPT_OK && c->pipe) {   // both sets (the other one's last CSR pass has finished first)
+        if (c->ev_fin[c->cur ^ 1]) (void)hipEventSynchronize(c->ev_fin[c->cur ^ 1]);
+        swap_set(c);
+        rc = ensure_workspace(c, v, n_bytes, n_str, long_bytes);
+        swap_set(c);
+    }
     if (rc == DPT_OK && long_bytes) c->arena_reserved = true;
     return rc;
+}
+
+int dpt_ctx_pipeline(dpt_ctx *c, void *csr_stream) {
+    if (!c) return fail(DPT_E_ARG, "null ctx");
+    DeviceGuard g(c->device);
+    hipError_t e;
+    if (c->pipe && (e = hipDeviceSynchronize()) != hipSuccess) return hip_fail(e, "sync (pipeline change)");
+    c->pipe = (hipStream_t)csr_stream;
+    if (c->pipe && !c->ev_tok) {
+        for (hipEvent_t *ev : {&c->ev_tok, &c->ev_fin[0], &c->ev_fin[1]})
+            if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) return hip_fail(e, "hipEventCreate");
+    }
+    return DPT_OK;
+}
+
+int dpt_ctx_join(dpt_ctx *c, void *stream) {
+    if (!c) return fail(DPT_E_ARG, "null ctx");
+    if (!c->pipe) return DPT_OK;
+    DeviceGuard g(c->device);
+    for (int k = 0; k < 2; k++) {   // (an event never recorded is complete)
+        const hipError_t e = hipStreamWaitEvent((hipStream_t)stream, c->ev_fin[k], 0);
+        if (e != hipSuccess) return hip_fail(e, "hipStreamWaitEvent");
+    }
+    return DPT_OK;
 }
 
 int dpt_ctx_workspace_bytes(const dpt_ctx *c, uint64_t *device_path, uint64_t *host_path) {
@@ -568,8 +638,25 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
     if (n_str > 0x7FFFFFFFull) return fail(DPT_E_ARG, "too many strings for one call (max 2^31-1)");
     if (c->device != v->device) return fail(DPT_E_ARG, "ctx and vocab on different devices");
     DeviceGuard g(c->device);
+    // pipelined calls (dpt_ctx_pipeline, device path): the other workspace set, free once its last CSR
+    // pass has finished -- a wait on the call's stream, or on the host when the set must grow first
+    const bool piped = c->pipe && !padded && !edges && !ctr_snap;
+    if (piped) {
+        swap_set(c);
+        const uint64_t nbat = (n_str + dpt::FIN_BATCH - 1) / dpt::FIN_BATCH;
+        const bool grows = !c->counts || !c->flags || !c->retry_count || n_str > c->cap_str || nbat > c->cap_batches ||
+                           n_bytes + 8 > (v->ids16 ? c->cap16 : c->cap32);
+        if (grows) {
+            const hipError_t e = hipEventSynchronize(c->ev_fin[c->cur]);
+            if (e != hipSuccess) return hip_fail(e, "hipEventSynchronize (pipelined set)");
+        }
+    }
     int rc = ensure_workspace(c, v, n_bytes, n_str, 0, !padded);
     if (rc) return rc;
+    if (piped) {
+        const hipError_t e = hipStreamWaitEvent((hipStream_t)hip_stream, c->ev_fin[c->cur], 0);
+        if (e != hipSuccess) return hip_fail(e, "hipStreamWaitEvent (pipelined set)");
+    }
     hipStream_t st = (hipStream_t)hip_stream;
     dpt::EncodeLaunch p;
     p.mode = mode_flags;
@@ -611,7 +698,7 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
         uint32_t ep = ++epoch;
         if (ep == 0) ep = ++epoch;
         p.sc_epoch = ep;
-        p.self_copy = dpt::self_copy_built() && sce && !strcmp(sce, "1") && !padded && !edges && !(mode_flags & (DPT_FLAG_UNCAPPED | DPT_FLAG_LEN_ONLY)) &&
+        p.self_copy = !piped && dpt::self_copy_built() && sce && !strcmp(sce, "1") && !padded && !edges && !(mode_flags & (DPT_FLAG_UNCAPPED | DPT_FLAG_LEN_ONLY)) &&
                       (n_str + dpt::FIN_BATCH - 1) / dpt::FIN_BATCH >= dpt::SC_MIN_BATCHES;
     }
     p.max_blocks = c->max_blocks;
@@ -627,6 +714,13 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
     p.hist_overwrite = hist_overwrite;
     p.ctr_snap = ctr_snap;
     p.no_fallback = no_fallback;
+    if (piped) {
+        p.csr_stream = c->pipe;
+        p.ev_tok = c->ev_tok;
+        p.ev_fin = c->ev_fin[c->cur];
+    }
+    p.n_bytes = n_bytes;
+    p.lite = piped || getenv("DPT_LITE");   // (DPT_LITE: the LDS-free CSR pass without the pipeline, for A/Bs)
     // (a per-string dp_tokenize call: one launch instead of two -- the finish kernel was 5 us of its 43)
     p.solo = !getenv("DPT_NO_SOLO") && no_fallback && n_str == 1 && !padded && !edges && !hist && !c->profile && !p.self_copy && ctr_snap;
     if (padded) {   // the ids go straight to their final place (int32), the counts to the caller's array

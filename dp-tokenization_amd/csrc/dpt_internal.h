@@ -43,6 +43,11 @@ struct EncodeLaunch {
     uint32_t sc_epoch;           // self-copy: the call's tag for its counts (never 0)
     uint64_t *ctr_snap;          // nullable (host path): the counter block's first 64 bytes, copied here by its reset
     bool no_fallback;            // the host checked that no string needs the 2048-byte or unbounded pass: skip them
+    uint64_t n_bytes = 0;        // the call's input bytes
+    bool lite = false;           // the CSR pass without LDS (finish_lite_kernel): it can run beside a first pass
+    hipStream_t csr_stream = nullptr;   // non-null (pipelined calls, dpt_ctx_pipeline): the CSR pass goes on this stream,
+    hipEvent_t ev_tok = nullptr, ev_fin = nullptr;   // after ev_tok (recorded on the call's stream after the other passes); ev_fin is
+                                 //   recorded after it (the workspace set it read is free again)
     bool solo;                   // one-string host-path call without fallbacks, histogram, edges or profiling: the first
                                  //   pass writes the CSR arrays itself (ids at 0.., id_off = {0, count}) and resets
                                  //   the counter block (its snapshot to ctr_snap); nothing else is launched

@@ -2950,6 +2950,164 @@ __global__ void __launch_bounds__(FIN_THREADS) finish_kernel(FinishArgs f) {
     }
 }
 
+// The CSR pass without LDS (pipelined calls, dpt_ctx_pipeline): ONE wave per batch, at most 64 VGPRs,
+// so it fits beside a running first pass -- whose waves hold every CU's LDS and 80 VGPRs x 5.5 waves
+// per SIMD -- and runs under the next call's first pass instead of after it.  The wave holds strings
+// lane + 64 u (u < 4): counts, staging offsets, exclusive prefixes by four wave scans; the copy goes
+// in rounds of up to 16 chunks of <= 64 ids (chunk u's source, destination and length parked in lane
+// u), the next round's loads issued before the current round's stores (a load waits for every older
+// store of the wave: one round trip per round, not two).  The histogram: one atomic per distinct count
+// value of the batch (peeled by ballots) and per status value.  Batch prefixes as in finish_kernel:
+// bpre (the scan kernel) or the fold sums; one-batch calls and DPT_HIST_OVERWRITE one-batch stores
+// take finish_kernel.
+template <typename ST>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) finish_lite_kernel(FinishArgs f) {
+    const unsigned lane = threadIdx.x;
+    const uint64_t t = blockIdx.x, s0 = t * FIN_BATCH;
+    const unsigned nsz = (unsigned)(f.n_str - s0 < FIN_BATCH ? f.n_str - s0 : FIN_BATCH);
+    // (32-bit per-string values relative to the batch: the host sends batches of 4 GiB of text or more
+    // to finish_kernel)
+    const uint64_t sbase = f.str_off[s0] - f.str_off[0];   // the batch's first staged id
+    const ST *__restrict__ staging = reinterpret_cast<const ST *>(f.staging) + sbase;
+    uint32_t c[4], src[4], ex[4];
+    uint64_t carry = 0;
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const unsigned i = lane + 64u * (unsigned)u;
+        const bool has = i < nsz;
+        c[u] = has ? (uint32_t)f.counts[s0 + i] : 0u;
+        src[u] = has ? (uint32_t)(f.str_off[s0 + i] - f.str_off[s0]) : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const uint64_t incl = wave_incl_scan_add64(c[u], lane);
+        ex[u] = (uint32_t)(carry + incl - c[u]);
+        carry += sc_readlane64(incl, 63);
+    }
+    const uint64_t total = carry;
+    uint64_t o0 = 0;
+    if (f.fold) {   // the sums of the batches before this one; the other parity's lines zeroed
+        uint64_t ps = 0;
+        for (uint64_t k = lane; k < t; k += 64u) ps += f.fold[k * BS_LINE] & BS_SUM_MASK;
+        o0 = sc_readlane64(wave_incl_scan_add64(ps, lane), 63);
+        for (uint64_t k = t * 64u + lane; k < f.fold_n; k += (uint64_t)gridDim.x * 64u)
+            for (unsigned w = 0; w <= BS_COPIED; w++) f.fold_zero[k * BS_LINE + w] = 0;
+    } else {
+        o0 = f.bpre[t];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const unsigned i = lane + 64u * (unsigned)u;
+        if (i < nsz) f.id_off[s0 + i + 1] = o0 + ex[u] + c[u];
+    }
+    if (t == 0 && lane == 0) {
+        f.id_off[0] = 0;
+        if (f.ctr) reset_counters(f.ctr, f.ctr_snap);
+    }
+    if (f.hist) {
+        const uint32_t top = f.n_bins - 1;
+        uint32_t pend = 0;   // bit u: string lane + 64 u still to count
+#pragma unroll
+        for (int u = 0; u < 4; u++) pend |= (lane + 64u * (unsigned)u < nsz ? 1u : 0u) << u;
+        const uint32_t live = pend;
+        for (;;) {   // one atomic per distinct bin of the batch
+            uint32_t cand = 0xFFFFFFFFu;
+#pragma unroll
+            for (int u = 3; u >= 0; u--) cand = ((pend >> u) & 1u) ? min(c[u], top) : cand;
+            const uint64_t any = ballot(cand != 0xFFFFFFFFu);
+            if (!any) break;
+            const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)cand, (int)__builtin_ctzll(any));
+            unsigned n = 0;
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const bool hit = ((pend >> u) & 1u) && min(c[u], top) == v;
+                n += (unsigned)__builtin_popcountll(ballot(hit));
+                pend &= ~((hit ? 1u : 0u) << u);
+            }
+            if (lane == 0) atomicAdd(&f.hist[v], (unsigned long long)n);
+        }
+        int32_t st[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            st[u] = -1;
+            if ((live >> u) & 1u) {
+                st[u] = f.status[s0 + lane + 64u * (unsigned)u];
+                st[u] = st[u] >= 0 && st[u] <= 4 ? st[u] : 4;
+            }
+        }
+#pragma unroll
+        for (int v = 0; v < 5; v++) {
+            unsigned n = 0;
+#pragma unroll
+            for (int u = 0; u < 4; u++) n += (unsigned)__builtin_popcountll(ballot(st[u] == v));
+            if (lane == 0 && n) atomicAdd(&f.hist[f.n_bins + 2 + v], (unsigned long long)n);
+        }
+        if (lane == 0) {
+            atomicAdd(&f.hist[f.n_bins], (unsigned long long)total);
+            atomicAdd(&f.hist[f.n_bins + 1], (unsigned long long)nsz);
+        }
+    }
+    // ---- the copy: chunks of the batch's strings in order (string j, ids 64 m .. 64 m + 63)
+#define LITE_PICK(r, jj) ((uint32_t)__builtin_amdgcn_readlane((int)(((jj) >> 6) == 0 ? r[0] : (((jj) >> 6) == 1 ? r[1] : (((jj) >> 6) == 2 ? r[2] : r[3]))), (int)((jj) & 63u)))
+    unsigned j = 0, m = 0;
+    uint32_t cj = 0, sj = 0, dj = 0;   // the current string's count, staged and output offsets (batch-relative)
+    auto seek = [&]() __attribute__((always_inline)) {   // from j on: the first string with ids
+        for (; j < nsz; j++) {
+            cj = LITE_PICK(c, j);
+            if (cj) break;
+        }
+        if (j < nsz) {
+            sj = LITE_PICK(src, j);
+            dj = LITE_PICK(ex, j);
+        }
+    };
+    seek();
+    // rounds of up to RC chunks: lane u < n parks chunk u's source, destination and length; all the
+    // round's loads, then its stores (the next round's loads wait for those stores: two round trips
+    // per round of up to RC x 64 ids)
+    constexpr unsigned RC = 32;
+    int32_t *const out = f.ids + o0;
+    for (;;) {
+        unsigned n = 0;
+        uint32_t csrc = 0, cdst = 0, clim = 0;
+        while (n < RC && j < nsz) {
+            const uint32_t k = 64u * m;
+            if (lane == n) {
+                csrc = sj + k;
+                cdst = dj + k;
+                clim = cj - k < 64u ? cj - k : 64u;
+            }
+            n++;
+            m++;
+            if (64u * m >= cj) {
+                j++;
+                m = 0;
+                seek();
+            }
+        }
+        if (!n) break;
+        int32_t v[RC];
+#pragma unroll
+        for (unsigned u = 0; u < RC; u++) {
+            v[u] = 0;
+            if (u < n) {
+                const uint32_t sa = (uint32_t)__builtin_amdgcn_readlane((int)csrc, u);
+                const uint32_t lim = (uint32_t)__builtin_amdgcn_readlane((int)clim, u);
+                if (lane < lim) v[u] = (int32_t)staging[(uint64_t)sa + lane];
+            }
+        }
+#pragma unroll
+        for (unsigned u = 0; u < RC; u++) {
+            if (u < n) {
+                const uint32_t da = (uint32_t)__builtin_amdgcn_readlane((int)cdst, u);
+                const uint32_t lim = (uint32_t)__builtin_amdgcn_readlane((int)clim, u);
+                if (lane < lim) out[(uint64_t)da + lane] = v[u];
+            }
+        }
+    }
+#undef LITE_PICK
+}
+
 // dpt_encode_padded runs no finish pass: one lane resets the counter block after the tokenize passes
 __global__ void __launch_bounds__(64) reset_kernel(uint32_t *ctr) {
     if (threadIdx.x == 0) reset_counters(ctr);
@@ -3224,7 +3382,15 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
         return hipGetLastError();
     }
     // batch prefixes (and the counter block's reset), then the CSR pass; a one-batch call (<= 256
-    // strings: the drop-in's per-string calls) needs no prefix, and its finish block does the rest
+    // strings: the drop-in's per-string calls) needs no prefix, and its finish block does the rest.
+    // Pipelined calls (dpt_ctx_pipeline): on the ctx's CSR stream, after the passes above
+    hipStream_t fs = stream;
+    if (p.csr_stream) {
+        hipError_t e = hipEventRecord(p.ev_tok, stream);
+        if (e == hipSuccess) e = hipStreamWaitEvent(p.csr_stream, p.ev_tok, 0);
+        if (e != hipSuccess) return e;
+        fs = p.csr_stream;
+    }
     const uint64_t nb = (p.n_str + FIN_BATCH - 1) / FIN_BATCH;
     FinishArgs f;
     f.bsum = nullptr; f.ctr = nullptr; f.fold = nullptr; f.fold_zero = nullptr; f.fold_n = 0;
@@ -3238,7 +3404,7 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     f.hist_store = (fold_hist && p.hist_overwrite && nb <= 1) ? 1 : 0;
     unsigned long long *hz = (fold_hist && p.hist_overwrite && nb > 1 && !fold && !sc) ? f.hist : nullptr;
     if (fold || sc) { f.fold = p.flags; f.fold_zero = p.zero_other; f.fold_n = p.zero_n; f.ctr = p.retry_count; }
-    else if (nb > 1) hipLaunchKernelGGL(batch_scan_kernel, dim3(1), dim3(SCAN_THREADS), 0, stream, p.n_str, p.flags, p.bpre, p.retry_count,
+    else if (nb > 1) hipLaunchKernelGGL(batch_scan_kernel, dim3(1), dim3(SCAN_THREADS), 0, fs, p.n_str, p.flags, p.bpre, p.retry_count,
                                         hz, p.hist_bins + 8u, p.ctr_snap);
     else { f.bsum = p.flags; f.ctr = p.retry_count; }
     f.staging = p.staging16 ? (const void *)p.staging16 : (const void *)p.staging;
@@ -3248,21 +3414,24 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     f.slices = (unsigned)(sls < 1 ? 1 : (sls > FIN_MAX_SLICES ? FIN_MAX_SLICES : sls));
     const uint64_t fb = nb * f.slices;
     if (sc) {
-        if (p.staging16) hipLaunchKernelGGL((finish_kernel<int16_t, true>), dim3((unsigned)fb), dim3(FIN_THREADS), 0, stream, f);
-        else hipLaunchKernelGGL((finish_kernel<int32_t, true>), dim3((unsigned)fb), dim3(FIN_THREADS), 0, stream, f);
+        if (p.staging16) hipLaunchKernelGGL((finish_kernel<int16_t, true>), dim3((unsigned)fb), dim3(FIN_THREADS), 0, fs, f);
+        else hipLaunchKernelGGL((finish_kernel<int32_t, true>), dim3((unsigned)fb), dim3(FIN_THREADS), 0, fs, f);
+    } else if (p.lite && nb > 1 && !f.hist_store && p.n_bytes < (1ull << 32)) {   // the LDS-free CSR pass (one wave per batch)
+        if (p.staging16) hipLaunchKernelGGL(finish_lite_kernel<int16_t>, dim3((unsigned)nb), dim3(64), 0, fs, f);
+        else hipLaunchKernelGGL(finish_lite_kernel<int32_t>, dim3((unsigned)nb), dim3(64), 0, fs, f);
     } else if (p.staging16) {
-        hipLaunchKernelGGL(finish_kernel<int16_t>, dim3((unsigned)fb), dim3(FIN_THREADS), 0, stream, f);
+        hipLaunchKernelGGL(finish_kernel<int16_t>, dim3((unsigned)fb), dim3(FIN_THREADS), 0, fs, f);
     } else {
-        hipLaunchKernelGGL(finish_kernel<int32_t>, dim3((unsigned)fb), dim3(FIN_THREADS), 0, stream, f);
+        hipLaunchKernelGGL(finish_kernel<int32_t>, dim3((unsigned)fb), dim3(FIN_THREADS), 0, fs, f);
     }
-    if (p.hist && !fold_hist) {   // too many bins for the finish pass's LDS: the separate pass
-        hipError_t eh = hipGetLastError();
-        if (eh != hipSuccess) return eh;
-        if (p.hist_overwrite && (eh = hipMemsetAsync(p.hist, 0, ((size_t)p.hist_bins + 8u) * sizeof(int64_t), stream)) != hipSuccess)
+    hipError_t eh = hipGetLastError();
+    if (eh == hipSuccess && p.hist && !fold_hist) {   // too many bins for the finish pass's LDS: the separate pass
+        if (p.hist_overwrite && (eh = hipMemsetAsync(p.hist, 0, ((size_t)p.hist_bins + 8u) * sizeof(int64_t), fs)) != hipSuccess)
             return eh;
-        return launch_histogram(p.id_off, p.status, p.n_str, p.hist, p.hist_bins, stream);
+        eh = launch_histogram(p.id_off, p.status, p.n_str, p.hist, p.hist_bins, fs);
     }
-    return hipGetLastError();
+    if (eh == hipSuccess && p.csr_stream) eh = hipEventRecord(p.ev_fin, fs);   // the set is free again after it
+    return eh;
 }
 
 size_t pend_scratch_bytes(unsigned max_blocks) { return (size_t)max_blocks * 64 * sizeof(uint4); }

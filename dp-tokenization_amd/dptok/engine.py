@@ -430,6 +430,16 @@ class Encoder:
               "dpt_ctx_copy_stats")
         return a.value, b.value, c.value
 
+    def pipeline(self, csr_stream: int) -> None:
+        """Pipelined device calls (dpt_ctx_pipeline): each later encode_device puts its CSR pass on
+        ``csr_stream`` (a stream handle, e.g. ``torch.cuda.Stream().cuda_stream``; 0 turns it off), where
+        it runs beside the next call's tokenize passes.  Outputs are complete after ``join``."""
+        check(_lib.lib().dpt_ctx_pipeline(self.handle, ctypes.c_void_p(csr_stream or None)), "dpt_ctx_pipeline")
+
+    def join(self, stream: int = 0) -> None:
+        """``stream`` waits for every CSR pass issued so far (dpt_ctx_join)."""
+        check(_lib.lib().dpt_ctx_join(self.handle, ctypes.c_void_p(stream or None)), "dpt_ctx_join")
+
     def set_histogram(self, hist_ptr: int, n_bins: int, overwrite: bool = False) -> None:
         """Fold the token-count histogram into the next encode on this engine (dpt_ctx_set_histogram_ex:
         its finish pass adds to hist, device int64[n_bins + 8], or with ``overwrite`` replaces it -- the

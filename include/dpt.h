@@ -123,6 +123,17 @@ int dpt_ctx_long_need(dpt_ctx *c, uint64_t *need, uint64_t *cap);
 int dpt_ctx_copy_stats(dpt_ctx *c, uint64_t *copied, uint64_t *batches_whole, uint64_t *n_batches);
 /* 1 when the library was built with the first pass's self-copy (csrc/Makefile `sc`), else 0. */
 int dpt_self_copy_available(void);
+/* ABI 3.  Pipelined calls: with csr_stream non-null, every later dpt_encode of the ctx runs its tokenize
+ * passes on its own stream as usual but its CSR pass (batch prefixes, id_off, ids, the histogram) on
+ * csr_stream, after them -- without making the call's stream wait -- and with a CSR pass that needs no
+ * LDS, so it runs beside the NEXT call's tokenize passes instead of after them.  Two workspace sets
+ * alternate between calls (dpt_ctx_workspace_bytes counts both once used).  A call's outputs are
+ * complete once csr_stream has passed its CSR pass: dpt_ctx_join(ctx, s) makes stream s wait for every
+ * CSR pass issued so far (or synchronise csr_stream).  The ctx's calls must come from one host thread,
+ * in order.  csr_stream = NULL returns to ordinary calls (after a device synchronisation).  The host
+ * path and dpt_encode_padded are never pipelined. */
+int dpt_ctx_pipeline(dpt_ctx *c, void *csr_stream);
+int dpt_ctx_join(dpt_ctx *c, void *stream);
 
 /*
  * Tokenize n_str strings, CSR-packed: string s is text[str_off[s]-str_off[0] .. str_off[s+1]-str_off[0]),
