@@ -3330,7 +3330,7 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
         EncodeArgs b = a;
         b.work_list = p.retry_list; b.work_count = p.retry_count;
         b.work_next = p.retry_count + 2;
-        if (!p.padded && (fin_fold(p.n_str) || p.self_copy) && p.hist && p.hist_overwrite && p.hist_bins >= 2 &&
+        if (!p.padded && !p.csr_stream && (fin_fold(p.n_str) || p.self_copy) && p.hist && p.hist_overwrite && p.hist_bins >= 2 &&
             p.hist_bins <= FIN_MAX_BINS) {
             b.hist_zero = reinterpret_cast<unsigned long long *>(p.hist);   // (the finish pass adds to it)
             b.n_hist = p.hist_bins + 8u;
@@ -3402,7 +3402,13 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     f.status = p.status;
     f.n_bins = p.hist_bins;
     f.hist_store = (fold_hist && p.hist_overwrite && nb <= 1) ? 1 : 0;
-    unsigned long long *hz = (fold_hist && p.hist_overwrite && nb > 1 && !fold && !sc) ? f.hist : nullptr;
+    unsigned long long *hz = (fold_hist && p.hist_overwrite && nb > 1 && !fold && !sc && !p.csr_stream) ? f.hist : nullptr;
+    if (p.csr_stream && fold_hist && p.hist_overwrite && nb > 1) {
+        // pipelined: zeroed on the CSR stream, after the previous call's CSR pass (which may still be
+        // adding to the same buffer), not by this call's first passes on the other stream
+        const hipError_t e = hipMemsetAsync(f.hist, 0, ((size_t)p.hist_bins + 8u) * sizeof(unsigned long long), fs);
+        if (e != hipSuccess) return e;
+    }
     if (fold || sc) { f.fold = p.flags; f.fold_zero = p.zero_other; f.fold_n = p.zero_n; f.ctr = p.retry_count; }
     else if (nb > 1) hipLaunchKernelGGL(batch_scan_kernel, dim3(1), dim3(SCAN_THREADS), 0, fs, p.n_str, p.flags, p.bpre, p.retry_count,
                                         hz, p.hist_bins + 8u, p.ctr_snap);

@@ -36,14 +36,15 @@ def _inputs(n, seed, kind):
     return _pack(texts)
 
 
-def _device_call(torch, enc, text, offs, s, outs=None):
+def _device_call(torch, enc, text, offs, s, hist=None):
     n = len(offs) - 1
     dt = torch.from_numpy(np.ascontiguousarray(text)).cuda()
     do = torch.from_numpy(np.ascontiguousarray(offs).view(np.int64)).cuda()
     ids = torch.empty(max(len(text), 1), dtype=torch.int32, device="cuda")
     id_off = torch.empty(n + 1, dtype=torch.int64, device="cuda")
     st = torch.empty(max(n, 1), dtype=torch.int32, device="cuda")
-    hist = torch.full((N_BINS + 8,), -3, dtype=torch.int64, device="cuda")
+    if hist is None:
+        hist = torch.full((N_BINS + 8,), -3, dtype=torch.int64, device="cuda")
     enc.set_histogram(hist.data_ptr(), N_BINS, overwrite=True)
     enc.encode_device(dt.data_ptr(), len(text), do.data_ptr(), n, ids.data_ptr(), max(len(text), 1),
                       id_off.data_ptr(), st.data_ptr(), stream=s)
@@ -116,3 +117,36 @@ def test_pipelined_calls(vocabs):
     res = _device_call(torch, enc, text, offs, s)
     torch.cuda.synchronize()
     _check(orc, text, offs, res, "after")
+
+
+def test_pipelined_calls_one_histogram(vocabs):
+    """Every pipelined call arms the SAME histogram buffer (DPT_HIST_OVERWRITE): each call's zeroing is
+    ordered after the previous call's CSR pass, so after the join it holds the last call's counts."""
+    torch = pytest.importorskip("torch")
+    from dptok import Encoder, Vocab
+    from oracle import oracle
+    t2i = vocabs["llama32k"]
+    enc, orc = Encoder(Vocab(t2i, 0)), oracle.OracleVocab(t2i)
+    csr = torch.cuda.Stream()
+    enc.pipeline(csr.cuda_stream)
+    s = torch.cuda.current_stream().cuda_stream
+    hist = torch.full((N_BINS + 8,), -3, dtype=torch.int64, device="cuda")
+    keep = []
+    try:
+        for k, n in enumerate([30000, 3000, 30000, 600, 20000]):
+            text, offs = _inputs(n, 40 + k, "ascii")
+            keep.append((text, offs, _device_call(torch, enc, text, offs, s, hist=hist)))
+        enc.join(s)
+        torch.cuda.synchronize()
+    finally:
+        enc.pipeline(0)
+    for text, offs, res in keep:   # every call's CSR arrays
+        _, _, ids, id_off, st, _ = res
+        rids, roff, rst, _ = orc.encode_csr(text, offs)
+        assert np.array_equal(id_off.cpu().numpy().view(np.uint64), roff)
+        assert np.array_equal(ids[: int(roff[-1])].cpu().numpy(), rids)
+    text, offs, _ = keep[-1]
+    counts = np.diff(orc.encode_csr(text, offs)[1].astype(np.int64))
+    h = hist.cpu().numpy()
+    assert np.array_equal(h[:N_BINS], np.bincount(np.minimum(counts, N_BINS - 1), minlength=N_BINS))
+    assert h[N_BINS] == counts.sum() and h[N_BINS + 1] == len(counts)
