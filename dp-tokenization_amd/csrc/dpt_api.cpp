@@ -575,6 +575,11 @@ int dpt_ctx_workspace_bytes(const dpt_ctx *c, uint64_t *device_path, uint64_t *h
                        (c->pend ? dpt::pend_scratch_bytes(c->max_blocks) : 0) +
                        (c->cq ? dpt::cq_scratch_bytes(c->max_blocks) : 0) +
                        (c->retry_count ? dpt::CTR_ALLOC_BYTES : 0);
+    if (device_path) {   // the second workspace set of pipelined calls (dpt_ctx_pipeline), once allocated
+        const WsSet &o = c->other;
+        *device_path += o.cap16 * 2 + o.cap32 * 4 + o.cap_str * (8 + 2 * 4) + flag_words(o.cap_batches) * 8 +
+                        (o.retry_count ? dpt::CTR_ALLOC_BYTES : 0);
+    }
     if (host_path) *host_path = c->cap_in + c->cap_out;
     return DPT_OK;
 }
