@@ -63,9 +63,9 @@ def parse():
                          "that follows forks)")
     ap.add_argument("--cpu-budget", type=float, default=25.0, help="seconds of CPU-baseline wall time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-pipeline", action="store_true",
-                    help="ordinary calls: each step's CSR pass on the step's stream, after its tokenize passes "
-                         "(default: pipelined, dpt_ctx_pipeline -- the CSR pass runs beside the next step's tokenize)")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="pipelined calls (dpt_ctx_pipeline): each step's CSR pass on a second stream beside the next "
+                         "step's tokenize passes (measured slower than ordinary calls, DESIGN.md 9; default off)")
     ap.add_argument("--host-path", action="store_true",
                     help="instead of the headline line: the drop-in surface the reference's callers use "
                          "(dp_tokenize(str) per call and dp_tokenize.batch, raw and llama mode, cfg2 and cfg4)")
@@ -374,7 +374,7 @@ def main():
     n_step = [0]
     # pipelined calls (dpt_ctx_pipeline): step k's CSR pass (ids, offsets, histogram) runs on csr_stream
     # beside step k+1's tokenize passes; its histogram's all-reduce is issued on that stream too
-    pipelined = not args.no_pipeline
+    pipelined = args.pipeline
     csr_stream = torch.cuda.Stream(dev) if pipelined else None
     if pipelined:
         enc.pipeline(csr_stream.cuda_stream)

@@ -16,7 +16,7 @@ STAMP_REPS=500 timeout -k 10 120 python3 tools/stamps.py 1 > $out/stamps_1.txt 2
 timeout -k 10 300 python tools/overlap_probe.py 10 > $out/overlap.json 2>&1; tail -2 $out/overlap.json
 timeout -k 10 600 python -u -m pytest tests/test_gpu_pipeline.py -x -v --timeout 200 --timeout-method thread > $out/pytest_pipe.txt 2>&1 || { tail -40 $out/pytest_pipe.txt; exit 1; }
 tail -3 $out/pytest_pipe.txt
-for a in "" "--no-pipeline"; do
+for a in "--pipeline" ""; do
   for w in "--workload cfg2" "--workload cfg2 --strings 125000" "--workload cfg4"; do
     timeout -k 10 300 python bench.py $w $a --steps 10 --warmup 3 --no-cpu-baseline --exact-sample 65536 > $out/bench.log 2>&1 || { tail -5 $out/bench.log; exit 1; }
     tail -1 $out/bench.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$w $a', 'GB/s %.2f' % (d['value']/1e9), 'ms %.3f' % d['ms_per_step'], 'exact', d['exact_match']['rate'], 'pipe', d['csr_pipeline'])"
