@@ -2,11 +2,13 @@
 # Final evidence of a round (GPU box): GPU suite, smoke, HBM traffic (calibrated PMC passes -- BEFORE the
 # bench, so its line reports the traffic of the same source), the default bench line (CPU baseline
 # included), its rocprofv3 kernel trace + stats, the PMC summary; then the other workloads, the
-# strong-scaling points, the host path and the per-call floor.  Usage: bash tools/gpu_evidence.sh <tag>
+# strong-scaling points, the host path and the per-call floor.
+# Usage: bash tools/gpu_evidence.sh <tag> [1|2]   (part 1: up to the PMC summary; part 2: the rest)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-tag=$1; out=gpurun_out/round_$tag; mkdir -p $out
+tag=$1; part=${2:-all}; out=gpurun_out/round_$tag; mkdir -p $out
+if [ $part != 2 ]; then
 timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $out/pytest_gpu.log 2>&1 || { tail -40 $out/pytest_gpu.log; exit 1; }
 tail -1 $out/pytest_gpu.log
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 || { tail -20 $out/smoke.log; exit 1; }
@@ -17,6 +19,9 @@ timeout -k 10 400 python -u bench.py > $out/bench.log 2>&1 || { tail -20 $out/be
 tail -1 $out/bench.log > $out/bench.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 10 --warmup 3 > $out/trace.log 2>&1 || { tail -20 $out/trace.log; exit 1; }
 bash tools/pmc.sh $tag > $out/pmc.log 2>&1 || { tail -20 $out/pmc.log; exit 1; }
+cp gpurun_out/pmc_$tag/summary.txt $out/pmc_summary.txt 2>/dev/null
+fi
+[ $part = 1 ] && exit 0
 for wl in cfg1 cfg4 cfg5 bloom; do
   timeout -k 10 400 python -u bench.py --workload $wl --steps 10 --warmup 3 > $out/bench_$wl.log 2>&1 || { tail -20 $out/bench_$wl.log; exit 1; }
   tail -1 $out/bench_$wl.log > $out/bench_$wl.json
@@ -28,7 +33,7 @@ done
 timeout -k 10 400 python -u bench.py --host-path > $out/host.log 2>&1 || { tail -20 $out/host.log; exit 1; }
 tail -1 $out/host.log > $out/host_path.json
 timeout -k 10 300 python tools/percall.py 3000 > $out/percall.json 2>/dev/null || { echo percall failed; exit 1; }
-for f in $out/bench.json $out/bench_*.json $out/strong_*.json; do
+for f in $(ls $out/bench.json $out/bench_*.json $out/strong_*.json 2>/dev/null); do
   python3 -c "import json; d=json.loads(open('$f').read()); print('$f', '%.2f GB/s' % (d['value']/1e9), 'ms/step %.4f' % d['ms_per_step'], 'exact', d['exact_match']['rate'], d['exact_match']['sample'], 'tok ms %.4f' % d['stage_ms_per_step']['tokenize'], 'frac %.4f' % d['roofline']['frac'], 'traffic', d['roofline'].get('traffic'))"
 done
 cat $out/percall.json
