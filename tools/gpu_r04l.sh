@@ -9,6 +9,8 @@ B=dp-tokenization_amd/csrc/build
 H=dp-tokenization_amd/dptok/libdpt.so   # the product build
 out=gpurun_out/r04l; mkdir -p $out/phase
 CTRS="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_INSTS_VALU"
+part=${1:-all}
+if [ $part != 2 ]; then
 timeout -k 10 300 python3 tools/prof_driver.py 200000 1 s2orc gen-only || exit 1
 for wl in "ascii 1000000" "s2orc 200000"; do
   set -- $wl
@@ -21,6 +23,8 @@ for wl in "ascii 1000000" "s2orc 200000"; do
     echo "== $tag"; python3 tools/pmc_summary.py $d | grep -A9 "256, 16" | head -10
   done
 done
+fi
+[ $part = 1 ] && exit 0
 # BLOOM scale: corpus, kernel trace + PMC passes (tools/pmc.sh)
 timeout -k 10 600 python3 tools/prof_driver.py 500000 1 bloom gen-only || exit 1
 timeout -k 10 900 bash tools/pmc.sh r04l_bloom 500000 bloom > $out/bloom_pmc.log 2>&1 || { tail -20 $out/bloom_pmc.log; exit 1; }
