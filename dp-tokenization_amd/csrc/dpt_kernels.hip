@@ -52,8 +52,9 @@
 namespace dpt {
 
 // Compile-time options are diagnostics only (DPT_STOP, DPT_C2STOP, DPT_STAMPS: wrong results or extra
-// counters by design, never in the product build) plus PUSH32 (pending its A/B).  The alternatives
-// measured slower or neutral are gone from the source; DESIGN.md §9 lists them with their numbers.
+// counters by design, never in the product build) plus DPT_SC_BUILD (the self-copy experiment, its own
+// library).  The alternatives measured slower or neutral are gone from the source; DESIGN.md §9 lists
+// them with their numbers.
 
 // ------------------------------------------------------------------ wave primitives
 
@@ -2059,28 +2060,18 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                         fin2[j + 1u] = f;
                         kcarry = f.y;
                     }
-#ifndef PUSH32
-#define PUSH32 0   // A/B knob: 1 = the span mask walked as two 32-bit halves (one v_ffbl and 32-bit arithmetic per edge)
-#endif
-                    if (PUSH32) {
+                    // the span mask as two 32-bit halves: one v_ffbl and 32-bit arithmetic per edge
+                    // (BLOOM 21.5 -> 22.1 GB/s against the 64-bit walk, r04l)
 #pragma unroll
-                        for (int hh = 0; hh < 2; hh++) {
-                            uint32_t m32 = hh == 0 ? ((uint32_t)sm & ~1u) : (uint32_t)(sm >> 32);
-                            while (m32) {
-                                const unsigned dd = ffbl(m32) + 32u * (unsigned)hh;
-                                m32 &= m32 - 1u;
-                                uint2 f = fin2[j + 1u + dd];   // <= re: no token crosses a cut
-                                upd(f, dd);
-                                fin2[j + 1u + dd] = f;
-                            }
+                    for (int hh = 0; hh < 2; hh++) {
+                        uint32_t m32 = hh == 0 ? ((uint32_t)sm & ~1u) : (uint32_t)(sm >> 32);
+                        while (m32) {
+                            const unsigned dd = ffbl(m32) + 32u * (unsigned)hh;
+                            m32 &= m32 - 1u;
+                            uint2 f = fin2[j + 1u + dd];   // <= re: no token crosses a cut
+                            upd(f, dd);
+                            fin2[j + 1u + dd] = f;
                         }
-                        continue;
-                    }
-                    for (uint64_t m = sm & ~1ull; m; m &= m - 1ull) {
-                        const unsigned dd = (unsigned)__builtin_ctzll(m);
-                        uint2 f = fin2[j + 1u + dd];   // <= re: no token crosses a cut
-                        upd(f, dd);
-                        fin2[j + 1u + dd] = f;
                     }
                 }
                 if (DPT_STOP == 26) return;   // diagnostic: + the recurrence
