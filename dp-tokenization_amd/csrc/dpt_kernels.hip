@@ -2708,7 +2708,7 @@ tokenize_kernel(KernArgs ka) {
 
 // ------------------------------------------------------------------ finish: offsets + CSR ids in one pass
 
-constexpr unsigned FIN_U = 16;                // loads in flight per thread of the copy
+constexpr unsigned FIN_U = 8;                 // loads in flight per thread of the copy (8 / 12 beat 4, 16 and 32: r04n)
 constexpr unsigned FIN_THREADS = 512;         // threads per finish block (>= FIN_BATCH): all of them copy
 constexpr unsigned SCAN_THREADS = 1024;       // threads of the batch-scan block
 constexpr uint64_t FIN_TARGET_BLOCKS = 2048;  // small batches: each batch's copy is split over slices until the grid has this many blocks
