@@ -39,4 +39,4 @@ for f in $(ls $out/bench.json $out/bench_*.json $out/strong_*.json 2>/dev/null);
   python3 -c "import json; d=json.loads(open('$f').read()); print('$f', '%.2f GB/s' % (d['value']/1e9), 'ms/step %.4f' % d['ms_per_step'], 'exact', d['exact_match']['rate'], d['exact_match']['sample'], 'tok ms %.4f' % d['stage_ms_per_step']['tokenize'], 'frac %.4f' % d['roofline']['frac'], 'traffic', d['roofline'].get('traffic'))"
 done
 cat $out/percall.json
-find $out/trace -name "*kernel_stats.csv" | head -1 | xargs cat | cut -c1-150 | head -8
+[ -d $out/trace ] && find $out/trace -name "*kernel_stats.csv" | head -1 | xargs cat | cut -c1-150 | head -8 || true
