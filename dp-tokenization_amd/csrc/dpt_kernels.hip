@@ -3155,8 +3155,8 @@ constexpr int BIG_CH = 2048;    // the 2048-byte pass's
 // The 2048-byte pass and the unbounded pass as ONE launch (they used to be two, ~5 us each on every call
 // although their lists are usually empty).  Each block takes a ticket: the first n_big tickets run the
 // 2048-byte pass (tokenize_body), the others the unbounded pass (lng::long_body) once every 2048-byte
-// block has finished -- that pass appends to the unbounded pass's list.  The blocks a ticket makes wait
-// wait only for blocks that hold earlier tickets, so are running (no dispatch-order assumption).  The
+// block has finished -- that pass appends to the unbounded pass's list.  A waiting block waits only for
+// blocks that hold earlier tickets, so are running (no dispatch-order assumption).  The
 // list's entries are published like any inter-workgroup hand-off on MI355X (per-XCD L2s): an agent-scope
 // release by each 2048-byte block that stored any, a relaxed done counter, one acquire on the other side.
 struct FallbackArgs {
@@ -3194,8 +3194,6 @@ __global__ void __launch_bounds__(64) fallback_kernel(FallbackArgs fa) {
 }
 
 // ------------------------------------------------------------------ launchers
-
-
 
 static_assert(block_lds_bytes<SMALL_CH, 16>() <= 64 * 1024, "small LDS");
 static_assert(block_lds_bytes<SMALL_CH, 64>() <= 64 * 1024, "small LDS");
