@@ -1,0 +1,18 @@
+#!/bin/bash
+# round 4: the machine scheduler for the kernels (HEAD = iterative-ilp; sdef = the default, smaxilp =
+# max-ilp, smaxocc = max-memory-clause) on cfg2, cfg4 and BLOOM; two interleaved rounds
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+out=gpurun_out/r04q; mkdir -p $out
+B=dp-tokenization_amd/csrc/build
+for r in 1 2; do
+  for v in head sdef smaxilp smaxocc; do
+    for args in "--workload cfg2" "--workload cfg4" "--workload bloom"; do
+      tag=${v}_$(echo $args | tr -d ' -')_$r
+      lib=""; [ $v != head ] && lib="DPT_LIB=$PWD/$B/var_$v/libdpt.so"
+      env $lib timeout -k 10 400 python bench.py $args --steps 10 --warmup 3 --no-cpu-baseline --exact-sample 65536 > $out/bench_$tag.log 2>&1 || { tail -5 $out/bench_$tag.log; exit 1; }
+      tail -1 $out/bench_$tag.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$tag', 'GB/s %.2f' % (d['value']/1e9), 'ms %.4f' % d['ms_per_step'], 'exact', d['exact_match']['rate'], 'tok', round(d['stage_ms_per_step']['tokenize'],4))"
+    done
+  done
+done
