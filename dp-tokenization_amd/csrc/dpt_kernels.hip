@@ -2754,15 +2754,33 @@ __global__ void __launch_bounds__(SCAN_THREADS) batch_scan_kernel(uint64_t n_str
     const uint64_t nb = (n_str + FIN_BATCH - 1) / FIN_BATCH;
     const uint64_t per = (nb + SCAN_THREADS - 1) / SCAN_THREADS;
     const uint64_t c0 = (uint64_t)tid * per < nb ? (uint64_t)tid * per : nb, c1 = c0 + per < nb ? c0 + per : nb;
-    uint64_t sum = 0;
-    for (uint64_t k = c0; k < c1; k++) sum += bsum[k * BS_LINE] & BS_SUM_MASK;
-    uint64_t total;
-    uint64_t run = block_incl_scan_add64<SCAN_THREADS>(sum, s_w, &total) - sum;
-    for (uint64_t k = c0; k < c1; k++) {
-        const uint64_t b = bsum[k * BS_LINE] & BS_SUM_MASK;
-        bpre[k] = run;
-        bsum[k * BS_LINE] = 0;
-        run += b;
+    uint64_t sum = 0, total;
+    constexpr unsigned PER_REG = 8;   // up to 8 x 1024 batches (2M strings): the sums stay in registers, read once
+    if (per <= PER_REG) {   // (all loads issued before the first is used: one round trip, not per batches)
+        uint64_t v[PER_REG];
+#pragma unroll
+        for (unsigned u = 0; u < PER_REG; u++) {
+            v[u] = c0 + u < c1 ? bsum[(c0 + u) * BS_LINE] & BS_SUM_MASK : 0ull;
+            sum += v[u];
+        }
+        uint64_t run = block_incl_scan_add64<SCAN_THREADS>(sum, s_w, &total) - sum;
+#pragma unroll
+        for (unsigned u = 0; u < PER_REG; u++) {
+            if (c0 + u < c1) {
+                bpre[c0 + u] = run;
+                bsum[(c0 + u) * BS_LINE] = 0;
+            }
+            run += v[u];
+        }
+    } else {
+        for (uint64_t k = c0; k < c1; k++) sum += bsum[k * BS_LINE] & BS_SUM_MASK;
+        uint64_t run = block_incl_scan_add64<SCAN_THREADS>(sum, s_w, &total) - sum;
+        for (uint64_t k = c0; k < c1; k++) {
+            const uint64_t b = bsum[k * BS_LINE] & BS_SUM_MASK;
+            bpre[k] = run;
+            bsum[k * BS_LINE] = 0;
+            run += b;
+        }
     }
     if (tid == 0) reset_counters(ctr, ctr_snap);
 }

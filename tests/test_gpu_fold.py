@@ -49,3 +49,30 @@ def test_batch_prefix_paths_in_sequence(vocabs):
         h = hist.cpu().numpy()
         assert h[n_bins] == counts.sum() and h[n_bins + 1] == n, (k, n, h[n_bins:])
         assert np.array_equal(h[:n_bins - 1], np.bincount(np.minimum(counts, n_bins - 1), minlength=n_bins)[:n_bins - 1]), (k, n)
+
+
+def test_scan_of_more_than_8192_batches(vocabs):
+    """More than 8 x 1024 batches (2,200,000 short strings): the batch-scan block's loop path (up to 8 per
+    thread it keeps the sums in registers), offsets and ids vs the C oracle."""
+    torch = pytest.importorskip("torch")
+    from dptok import Encoder, Vocab, synth
+    from oracle import oracle
+    t2i = vocabs["llama32k"]
+    n = 2_200_000
+    text, offs = synth.random_ascii_corpus(n, 3, seed=77)
+    enc = Encoder(Vocab(t2i, 0))
+    s = torch.cuda.current_stream().cuda_stream
+    dt = torch.from_numpy(text).cuda()
+    do = torch.from_numpy(offs.view(np.int64)).cuda()
+    ids = torch.empty(max(len(text), 1), dtype=torch.int32, device="cuda")
+    id_off = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    st = torch.empty(n, dtype=torch.int32, device="cuda")
+    for _ in range(2):   # (the second call starts from the zeroed batch lines the first left)
+        enc.encode_device(dt.data_ptr(), len(text), do.data_ptr(), n, ids.data_ptr(), max(len(text), 1),
+                          id_off.data_ptr(), st.data_ptr(), stream=s)
+        torch.cuda.synchronize()
+        rids, roff, rst, _ = oracle.OracleVocab(t2i).encode_csr(text, offs, nthreads=16)
+        off_h = id_off.cpu().numpy().view(np.uint64)
+        assert np.array_equal(off_h, roff)
+        assert np.array_equal(ids[: int(off_h[-1])].cpu().numpy(), rids)
+        assert np.array_equal(st.cpu().numpy(), rst)
