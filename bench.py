@@ -270,7 +270,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     scaling = args.scaling or "strong"   # N = 1: strong and weak are the same run
-    from dptok import Encoder, Vocab, synth
+    from dptok import Encoder, Vocab, synth, _lib
     from dptok import dist as ddist
     bloom = args.workload == "bloom"
     if bloom:
@@ -591,7 +591,8 @@ def main():
                                      "next step's tokenize passes; every step's outputs complete inside the timed region",
                              "ms_per_step_ordinary_calls": ms_off},
             "self_copy": {"strings_copied_by_first_pass": sc_copied, "strings": M, "batches_copied_whole": sc_batches,
-                          "batches": sc_nb, "enabled": os.environ.get("DPT_SELF_COPY") == "1"},
+                          "batches": sc_nb, "enabled": os.environ.get("DPT_SELF_COPY") == "1" and bool(_lib.lib().dpt_self_copy_available()),
+                          "note": "experiment: opt-in (DPT_SELF_COPY=1) in the csrc/Makefile `sc` build only, DESIGN.md 9"},
             "padded_layout": {"api": "dpt_encode_padded (ids at each string's byte offset + per-string counts, no CSR pass); encode only, no histogram",
                               "ms_per_step": dtp / args.steps * 1e3, "bytes_per_s": bytes_all * args.steps / dtp,
                               "counts_and_status_equal_csr": padded_same},
