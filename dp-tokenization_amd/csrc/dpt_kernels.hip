@@ -3187,6 +3187,15 @@ struct FallbackArgs {
 template <bool WIDE, bool RAW>
 __global__ void __launch_bounds__(64) fallback_kernel(FallbackArgs fa) {
     const unsigned lane = lane_id();
+    // Both lists are final here (the first pass ran before this launch): when both are empty -- nearly
+    // every call -- no block takes a ticket or waits for the 2048-byte blocks (the same-address ticket and
+    // done-counter atomics and the waits were most of the empty launch's ~10 us)
+    if (*fa.k.ea.work_count == 0 && *fa.l.list_count == 0) {
+        const auto &e = fa.k.ea;
+        if (e.hist_zero && blockIdx.x == 0)
+            for (uint32_t b = lane; b < e.n_hist; b += 64u) e.hist_zero[b] = 0;
+        return;
+    }
     unsigned t = 0;
     if (lane == 0) t = atomicAdd(fa.ticket, 1u);
     t = __builtin_amdgcn_readfirstlane(t);
