@@ -3258,7 +3258,17 @@ static void launch_tok(const EncodeArgs &a, const TrieView &tv, uint64_t n_units
         // at the occupancy limit of 22, 250k and more are fastest at 22 (profiles/r02_ab_issue_model.log)
         const uint64_t want = (n_units + 7ull * n_cu - 1) / (7ull * n_cu);   // n_units = strings / 4
         const uint64_t lo = wpc < 16u ? wpc : 16u;
-        if (want < wpc) wpc = want > lo ? want : lo;
+        if (want < wpc) {
+            // of the wave counts from lo up, the one with the fewest slot-rounds w * ceil(rounds) -- the
+            // work plus the idle part of the last round -- the smallest on ties (100k strings: 16 waves
+            // per CU ran 6.1 rounds, a last round 10 % full; 125k keeps 18)
+            uint64_t best = lo, bc = ~0ull;
+            for (uint64_t w = lo; w <= wpc; w++) {
+                const uint64_t c = w * ((n_units + w * n_cu - 1) / (w * n_cu));
+                if (c < bc) { bc = c; best = w; }
+            }
+            wpc = best;
+        }
     }
     uint64_t blocks = (uint64_t)n_cu * wpc;
     if (blocks > (uint64_t)n_cu * 64u) blocks = (uint64_t)n_cu * 64u;   // the scratch is sized for 64 per CU
