@@ -13,8 +13,12 @@ Strong scaling (the default for N > 1): ONE global corpus of --s
 takes [r*N/W, (r+1)*N/W) -- and `value` = the corpus bytes / max-over-ranks time.
 --scaling weak gives every rank its own --strings strings instead (labelled "weak").
 
-Launch: python bench.py --gpus 1 --steps K --warmup W
-        python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+Launch: python bench.py --gpus N --steps K --warmup W
+  N = 1 runs in this process.  N > 1 without WORLD_SIZE in the environment: this process starts
+  `python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 ...
+  bench.py <the same arguments>` as a CHILD (before anything here touches the GPU; never an exec)
+  and exits with its return code -- rank 0's JSON line goes to the same stdout.  Under torchrun
+  (WORLD_SIZE set) --gpus must equal WORLD_SIZE (else exit 2).
 """
 from __future__ import annotations
 
@@ -24,6 +28,8 @@ import json
 import multiprocessing as mp
 import os
 import signal
+import socket
+import subprocess
 import sys
 import time
 
@@ -39,7 +45,8 @@ N_BINS = 258                # tokens-per-string histogram (<= 256 ids for 256-by
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks) of the job; default: WORLD_SIZE under torchrun, else 1")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=["cfg1", "cfg2", "cfg4", "cfg5", "bloom"], default="cfg2",
@@ -63,9 +70,6 @@ def parse():
                          "that follows forks)")
     ap.add_argument("--cpu-budget", type=float, default=25.0, help="seconds of CPU-baseline wall time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pipeline", action="store_true",
-                    help="pipelined calls (dpt_ctx_pipeline): each step's CSR pass on a second stream beside the next "
-                         "step's tokenize passes (measured slower than ordinary calls, DESIGN.md 9; default off)")
     ap.add_argument("--host-path", action="store_true",
                     help="instead of the headline line: the drop-in surface the reference's callers use "
                          "(dp_tokenize(str) per call and dp_tokenize.batch, raw and llama mode, cfg2 and cfg4)")
@@ -259,10 +263,45 @@ def host_path(args):
     print(json.dumps(out), flush=True)
 
 
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def resolve_world(args, env=os.environ) -> int:
+    """The job's rank count: --gpus, checked against WORLD_SIZE when torchrun started this process.
+    Returns 0 when this process must launch the ranks itself (--gpus > 1, no WORLD_SIZE); raises
+    SystemExit(2) on a mismatch (a silently smaller job would mis-measure the scaling run)."""
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        g = 1 if args.gpus is None else args.gpus
+        if g < 1:
+            raise SystemExit("bench: --gpus must be >= 1")
+        return 0 if g > 1 else 1
+    if args.gpus is not None and args.gpus != int(ws):
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={ws}: refusing to run a job of another size",
+              file=sys.stderr, flush=True)
+        raise SystemExit(2)
+    return int(ws)
+
+
+def spawn_ranks(args, argv) -> int:
+    """--gpus N > 1 from a plain `python bench.py`: one rank per GPU through torch.distributed.run, as a
+    child process (this process has not touched the GPU); its exit code is ours."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    log("launching %d ranks: %s" % (args.gpus, " ".join(cmd)))
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
     if args.host_path:
         return host_path(args)
+    if resolve_world(args) == 0:
+        raise SystemExit(spawn_ranks(args, sys.argv[1:]))
     import torch
     import torch.distributed as dist
 
@@ -270,7 +309,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     scaling = args.scaling or "strong"   # N = 1: strong and weak are the same run
-    from dptok import Encoder, Vocab, synth, _lib
+    from dptok import Encoder, Vocab, synth
     from dptok import dist as ddist
     bloom = args.workload == "bloom"
     if bloom:
@@ -372,12 +411,6 @@ def main():
     d_hists = [torch.zeros(N_BINS + 8, dtype=torch.int64, device=dev) for _ in range(2)]
     pending = [None, None]
     n_step = [0]
-    # pipelined calls (dpt_ctx_pipeline): step k's CSR pass (ids, offsets, histogram) runs on csr_stream
-    # beside step k+1's tokenize passes; its histogram's all-reduce is issued on that stream too
-    pipelined = args.pipeline
-    csr_stream = torch.cuda.Stream(dev) if pipelined else None
-    if pipelined:
-        enc.pipeline(csr_stream.cuda_stream)
     enc.reserve(n_bytes, M)
     stream = torch.cuda.current_stream(dev).cuda_stream
 
@@ -396,20 +429,13 @@ def main():
                           cut_ptr=d_cut.data_ptr() if bloom else 0, mode="atoms" if bloom else "raw")
         if coll:   # the single collective: RCCL over xGMI with nccl, gloo in rehearsals
             if red_dev.type == "cpu":
-                if pipelined:
-                    enc.join(stream)   # (the histogram is complete once the CSR pass is)
                 hc = h.cpu()
                 ddist.allreduce_histogram(hc)
                 h.copy_(hc)
-            elif pipelined:
-                with torch.cuda.stream(csr_stream):   # ordered after this step's CSR pass
-                    pending[b] = ddist.allreduce_histogram(h, async_op=True)
             else:
                 pending[b] = ddist.allreduce_histogram(h, async_op=True)
 
-    def drain():   # every outstanding CSR pass and all-reduce is ordered before what the stream does next
-        if pipelined:
-            enc.join(stream)
+    def drain():   # every outstanding all-reduce is ordered before what the stream does next
         for b in range(2):
             if pending[b] is not None:
                 pending[b].wait()
@@ -447,35 +473,6 @@ def main():
         dt = float(t.item())
     ms_stage, launches = enc.profile_read()
     enc.profile(False)
-    # the same steps as ordinary calls (each CSR pass after its own tokenize passes), for the record
-    ms_off = None
-    if pipelined:
-        enc.pipeline(0)
-        pipelined = False
-        for _ in range(2):
-            step()
-        drain()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        t0o = time.perf_counter()
-        for _ in range(args.steps):
-            step()
-        drain()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        dto = time.perf_counter() - t0o
-        if world > 1:
-            t = torch.tensor([dto], dtype=torch.float64, device=red_dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            dto = float(t.item())
-        ms_off = dto / args.steps * 1e3
-        pipelined = True
-    # the last timed call's self-copy (dpt_ctx_copy_stats): strings its first pass copied into the CSR
-    # arrays itself, batches whose offsets it wrote (the finish pass copied the rest)
-    sc_copied, sc_batches, sc_nb = enc.copy_stats()
-
     # secondary: the encode alone through dpt_encode_padded (ids left at each string's byte offset,
     # per-string counts; no finish pass, no histogram) -- reported beside `value`, never as it
     d_pids = torch.empty(max(n_bytes, 1), dtype=torch.int32, device=dev)
@@ -586,13 +583,6 @@ def main():
                          "alg_bytes_staged_width": alg_staged, "staged_id_bytes": id_bytes,
                          "frac_staged_width": alg_staged / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
             "cpu_baseline": cpu,
-            "csr_pipeline": {"on": ms_off is not None, "api": "dpt_ctx_pipeline / dpt_ctx_join",
-                             "what": "each step's CSR pass (LDS-free finish_lite_kernel) on a second stream, beside the "
-                                     "next step's tokenize passes; every step's outputs complete inside the timed region",
-                             "ms_per_step_ordinary_calls": ms_off},
-            "self_copy": {"strings_copied_by_first_pass": sc_copied, "strings": M, "batches_copied_whole": sc_batches,
-                          "batches": sc_nb, "enabled": os.environ.get("DPT_SELF_COPY") == "1" and bool(_lib.lib().dpt_self_copy_available()),
-                          "note": "experiment: opt-in (DPT_SELF_COPY=1) in the csrc/Makefile `sc` build only, DESIGN.md 9"},
             "padded_layout": {"api": "dpt_encode_padded (ids at each string's byte offset + per-string counts, no CSR pass); encode only, no histogram",
                               "ms_per_step": dtp / args.steps * 1e3, "bytes_per_s": bytes_all * args.steps / dtp,
                               "counts_and_status_equal_csr": padded_same},

@@ -32,23 +32,6 @@ struct dpt_vocab {
 
 static uint64_t flag_words(uint64_t cap_batches) { return cap_batches * (2 * dpt::BS_LINE + 1); }
 
-// What a call's CSR pass reads or resets -- staged ids, counts, batch lines, the counter block (and the
-// retry lists with them): pipelined calls (dpt_ctx_pipeline) alternate between the ctx's own set and
-// a second one, so call k+1's first pass never writes what call k's CSR pass is still reading.
-struct WsSet {
-    int32_t *staging32 = nullptr;
-    uint64_t cap32 = 0;
-    int16_t *staging16 = nullptr;
-    uint64_t cap16 = 0;
-    uint64_t *counts = nullptr;
-    uint32_t *retry_list = nullptr;
-    uint64_t cap_str = 0;
-    unsigned long long *flags = nullptr;
-    uint64_t cap_batches = 0;
-    int flag_parity = 0;
-    uint32_t *retry_count = nullptr;
-};
-
 struct dpt_ctx {
     int device = 0;
     // workspace of the device path (ensure_workspace)
@@ -66,17 +49,13 @@ struct dpt_ctx {
                                       // counter at byte 32, ..., the first pass's partition counters at byte 256
     uint8_t *wsl_scratch = nullptr;   // word lists of the 256-byte pass (dpt::wsl_scratch_bytes)
     uint4 *pend = nullptr;            // pending residual tokens of the 256-byte pass (dpt::pend_scratch_bytes)
-    // two parity regions R0, R1 of batch lines (dpt::BS_LINE u64 per 256-string batch: its sum, self-copy
-    // prefix, copied count), then the batch prefixes of the scan path (cap_batches u64): the call of
-    // parity P uses R_P and -- fold and self-copy calls -- zeroes R_(1-P) for the next one (the parity
-    // flips); between calls R_parity is all zero.  See dpt_internal.h fin_fold and BS_LINE.
+    // two parity regions R0, R1 of batch lines (dpt::BS_LINE u64 per 256-string batch: its sum in the
+    // first), then the batch prefixes of the scan path (cap_batches u64): the call of parity P uses R_P
+    // and -- fold calls -- zeroes R_(1-P) for the next one (the parity flips); between calls R_parity
+    // is all zero.  See dpt_internal.h fin_fold and BS_LINE.
     unsigned long long *flags = nullptr;
     uint64_t cap_batches = 0;
     int flag_parity = 0;
-    uint4 *cq = nullptr;              // self-copy queues (dpt::cq_scratch_bytes)
-
-    unsigned long long *last_sc = nullptr;   // the last call's region when it self-copied (dpt_ctx_copy_stats) ...
-    uint64_t last_sc_nb = 0, last_sc_n = 0;  // ... and its batches and strings
     unsigned max_blocks = 0;
     // host path: one device buffer in (text | offsets | cut) and one out (id_off | status | capped |
     // counters | ids | edges), each mirrored by a pinned host buffer so every copy is one async DMA
@@ -87,12 +66,6 @@ struct dpt_ctx {
     int64_t *hist = nullptr;
     uint32_t hist_bins = 0;
     bool hist_overwrite = false;
-    // pipelined calls (dpt_ctx_pipeline): the CSR pass on `pipe`; the other workspace set; ev_fin[k]:
-    // recorded after the last CSR pass that read set k (cur: the set in the fields above)
-    hipStream_t pipe = nullptr;
-    WsSet other;
-    hipEvent_t ev_tok = nullptr, ev_fin[2] = {nullptr, nullptr};
-    int cur = 0;
     // profiling
     bool profile = false;
     std::vector<hipEvent_t> events;   // groups of 4 per call
@@ -162,17 +135,6 @@ uint64_t default_long_bytes(uint64_t n_bytes) {
 constexpr uint64_t ARENA_PER_BYTE = 20;   // uint4 rec + int32 stg (dpt_long.hip)
 constexpr size_t COUNTER_BYTES = 64;
 
-// Exchange the ctx's workspace set with the other one (pipelined calls)
-void swap_set(dpt_ctx *c) {
-    WsSet &o = c->other;
-    std::swap(c->staging32, o.staging32); std::swap(c->cap32, o.cap32);
-    std::swap(c->staging16, o.staging16); std::swap(c->cap16, o.cap16);
-    std::swap(c->counts, o.counts); std::swap(c->retry_list, o.retry_list); std::swap(c->cap_str, o.cap_str);
-    std::swap(c->flags, o.flags); std::swap(c->cap_batches, o.cap_batches); std::swap(c->flag_parity, o.flag_parity);
-    std::swap(c->retry_count, o.retry_count);
-    c->cur ^= 1;
-}
-
 // v == nullptr: both staging widths (the vocabulary is not known yet); staging = false: no staging
 // (dpt_encode_padded writes the ids into the caller's buffer)
 int ensure_workspace(dpt_ctx *c, const dpt_vocab *v, uint64_t n_bytes, uint64_t n_str, uint64_t long_bytes,
@@ -195,9 +157,6 @@ int ensure_workspace(dpt_ctx *c, const dpt_vocab *v, uint64_t n_bytes, uint64_t 
         uint64_t cap = c->cap_str, cap2 = 2 * c->cap_str;
         e = grow(&c->counts, &cap, n_str);
         if (e != hipSuccess) return hip_fail(e, "hipMalloc(counts)");
-        // (zeroed: the self-copy reads tagged counts, dpt_kernels.hip sc_copy_run)
-        if ((e = hipMemset(c->counts, 0, cap * sizeof(uint64_t))) != hipSuccess) return hip_fail(e, "hipMemset(counts)");
-        fresh = true;
         e = grow(&c->retry_list, &cap2, 2 * n_str);   // the 2048-byte pass's list, then the unbounded pass's
         if (e != hipSuccess) return hip_fail(e, "hipMalloc(retry_list)");
         cap2 /= 2;
@@ -224,10 +183,6 @@ int ensure_workspace(dpt_ctx *c, const dpt_vocab *v, uint64_t n_bytes, uint64_t 
     if (!c->pend) {
         e = hipMalloc((void **)&c->pend, dpt::pend_scratch_bytes(c->max_blocks));
         if (e != hipSuccess) return hip_fail(e, "hipMalloc(pend)");
-    }
-    if (!c->cq && dpt::self_copy_built()) {
-        e = hipMalloc((void **)&c->cq, dpt::cq_scratch_bytes(c->max_blocks));
-        if (e != hipSuccess) return hip_fail(e, "hipMalloc(cq)");
     }
     if (!c->retry_count) {
         // zeroed once here; every call's finish kernel resets it for the next call
@@ -508,18 +463,13 @@ int dpt_ctx_create(int device, dpt_ctx **out) {
 int dpt_ctx_destroy(dpt_ctx *c) {
     if (!c) return DPT_OK;
     DeviceGuard g(c->device);
-    if (c->pipe) (void)hipDeviceSynchronize();   // (a CSR pass may still read the sets)
-    const WsSet &o = c->other;
     void *ps[] = {c->staging32, c->staging16, c->arena, c->counts, c->retry_list, c->retry_count, c->wsl_scratch,
-                  c->pend, c->cq, c->flags, c->d_in, c->d_out, o.staging32, o.staging16, o.counts, o.retry_list,
-                  o.flags, o.retry_count};
+                  c->pend, c->flags, c->d_in, c->d_out};
     for (void *p : ps)
         if (p) (void)hipFree(p);
     if (c->p_in) (void)hipHostFree(c->p_in);
     if (c->p_out) (void)hipHostFree(c->p_out);
     for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
-    for (hipEvent_t e : {c->ev_tok, c->ev_fin[0], c->ev_fin[1]})
-        if (e) (void)hipEventDestroy(e);
     delete c;
     return DPT_OK;
 }
@@ -532,39 +482,9 @@ int dpt_ctx_reserve_vocab(dpt_ctx *c, const dpt_vocab *v, uint64_t n_bytes, uint
     if (!c) return fail(DPT_E_ARG, "null ctx");
     if (v && v->device != c->device) return fail(DPT_E_ARG, "ctx and vocab on different devices");
     DeviceGuard g(c->device);
-    int rc = ensure_workspace(c, v, n_bytes, n_str, long_bytes);
-    if (rc == DPT_OK && c->pipe) {   // both sets (the other one's last CSR pass has finished first)
-        if (c->ev_fin[c->cur ^ 1]) (void)hipEventSynchronize(c->ev_fin[c->cur ^ 1]);
-        swap_set(c);
-        rc = ensure_workspace(c, v, n_bytes, n_str, long_bytes);
-        swap_set(c);
-    }
+    const int rc = ensure_workspace(c, v, n_bytes, n_str, long_bytes);
     if (rc == DPT_OK && long_bytes) c->arena_reserved = true;
     return rc;
-}
-
-int dpt_ctx_pipeline(dpt_ctx *c, void *csr_stream) {
-    if (!c) return fail(DPT_E_ARG, "null ctx");
-    DeviceGuard g(c->device);
-    hipError_t e;
-    if (c->pipe && (e = hipDeviceSynchronize()) != hipSuccess) return hip_fail(e, "sync (pipeline change)");
-    c->pipe = (hipStream_t)csr_stream;
-    if (c->pipe && !c->ev_tok) {
-        for (hipEvent_t *ev : {&c->ev_tok, &c->ev_fin[0], &c->ev_fin[1]})
-            if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) return hip_fail(e, "hipEventCreate");
-    }
-    return DPT_OK;
-}
-
-int dpt_ctx_join(dpt_ctx *c, void *stream) {
-    if (!c) return fail(DPT_E_ARG, "null ctx");
-    if (!c->pipe) return DPT_OK;
-    DeviceGuard g(c->device);
-    for (int k = 0; k < 2; k++) {   // (an event never recorded is complete)
-        const hipError_t e = hipStreamWaitEvent((hipStream_t)stream, c->ev_fin[k], 0);
-        if (e != hipSuccess) return hip_fail(e, "hipStreamWaitEvent");
-    }
-    return DPT_OK;
 }
 
 int dpt_ctx_workspace_bytes(const dpt_ctx *c, uint64_t *device_path, uint64_t *host_path) {
@@ -573,35 +493,8 @@ int dpt_ctx_workspace_bytes(const dpt_ctx *c, uint64_t *device_path, uint64_t *h
         *device_path = c->cap16 * 2 + c->cap32 * 4 + c->arena_cap * ARENA_PER_BYTE + c->cap_str * (8 + 2 * 4) +
                        flag_words(c->cap_batches) * 8 + (c->wsl_scratch ? dpt::wsl_scratch_bytes(c->max_blocks) : 0) +
                        (c->pend ? dpt::pend_scratch_bytes(c->max_blocks) : 0) +
-                       (c->cq ? dpt::cq_scratch_bytes(c->max_blocks) : 0) +
                        (c->retry_count ? dpt::CTR_ALLOC_BYTES : 0);
-    if (device_path) {   // the second workspace set of pipelined calls (dpt_ctx_pipeline), once allocated
-        const WsSet &o = c->other;
-        *device_path += o.cap16 * 2 + o.cap32 * 4 + o.cap_str * (8 + 2 * 4) + flag_words(o.cap_batches) * 8 +
-                        (o.retry_count ? dpt::CTR_ALLOC_BYTES : 0);
-    }
     if (host_path) *host_path = c->cap_in + c->cap_out;
-    return DPT_OK;
-}
-
-int dpt_self_copy_available(void) { return dpt::self_copy_built() ? 1 : 0; }
-
-int dpt_ctx_copy_stats(dpt_ctx *c, uint64_t *copied, uint64_t *batches_whole, uint64_t *n_batches) {
-    if (!c || !copied || !batches_whole || !n_batches) return fail(DPT_E_ARG, "null argument");
-    *copied = *batches_whole = *n_batches = 0;
-    if (!c->last_sc || !c->last_sc_nb) return DPT_OK;
-    DeviceGuard g(c->device);
-    const uint64_t nb = c->last_sc_nb;
-    std::vector<unsigned long long> lines(nb * dpt::BS_LINE);
-    hipError_t e = hipMemcpy(lines.data(), c->last_sc, lines.size() * 8, hipMemcpyDeviceToHost);
-    if (e != hipSuccess) return hip_fail(e, "D2H copy stats");
-    for (uint64_t b = 0; b < nb; b++) {
-        const unsigned long long *l = lines.data() + b * dpt::BS_LINE;
-        const uint32_t cp = (uint32_t)l[dpt::BS_COPIED];
-        *copied += cp;
-        *batches_whole += cp == (b + 1 < nb ? dpt::FIN_BATCH : c->last_sc_n - b * dpt::FIN_BATCH) ? 1 : 0;
-    }
-    *n_batches = nb;
     return DPT_OK;
 }
 
@@ -643,25 +536,8 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
     if (n_str > 0x7FFFFFFFull) return fail(DPT_E_ARG, "too many strings for one call (max 2^31-1)");
     if (c->device != v->device) return fail(DPT_E_ARG, "ctx and vocab on different devices");
     DeviceGuard g(c->device);
-    // pipelined calls (dpt_ctx_pipeline, device path): the other workspace set, free once its last CSR
-    // pass has finished -- a wait on the call's stream, or on the host when the set must grow first
-    const bool piped = c->pipe && !padded && !edges && !ctr_snap;
-    if (piped) {
-        swap_set(c);
-        const uint64_t nbat = (n_str + dpt::FIN_BATCH - 1) / dpt::FIN_BATCH;
-        const bool grows = !c->counts || !c->flags || !c->retry_count || n_str > c->cap_str || nbat > c->cap_batches ||
-                           n_bytes + 8 > (v->ids16 ? c->cap16 : c->cap32);
-        if (grows) {
-            const hipError_t e = hipEventSynchronize(c->ev_fin[c->cur]);
-            if (e != hipSuccess) return hip_fail(e, "hipEventSynchronize (pipelined set)");
-        }
-    }
-    int rc = ensure_workspace(c, v, n_bytes, n_str, 0, !padded);
+    const int rc = ensure_workspace(c, v, n_bytes, n_str, 0, !padded);
     if (rc) return rc;
-    if (piped) {
-        const hipError_t e = hipStreamWaitEvent((hipStream_t)hip_stream, c->ev_fin[c->cur], 0);
-        if (e != hipSuccess) return hip_fail(e, "hipStreamWaitEvent (pipelined set)");
-    }
     hipStream_t st = (hipStream_t)hip_stream;
     dpt::EncodeLaunch p;
     p.mode = mode_flags;
@@ -687,24 +563,9 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
         const uint64_t cb = c->cap_batches, rl = cb * dpt::BS_LINE;
         unsigned long long *r = c->flags + (c->flag_parity ? rl : 0);
         p.flags = r;
-        p.inc = r + dpt::BS_INC;
-        p.copied = reinterpret_cast<uint32_t *>(r + dpt::BS_COPIED);
         p.zero_other = c->flags + (c->flag_parity ? 0 : rl);
         p.zero_n = cb;
         p.bpre = c->flags + 2 * rl;
-        p.cq = c->cq;
-        // self-copy: CSR calls of enough batches without edge outputs or length-only DPs
-        // (opt-in, read per call: "1" = on.  Measured slower than the finish pass's copy so far: the
-        // copy's round trips stall the latency-bound first pass -- DESIGN.md 9)
-        const char *sce = getenv("DPT_SELF_COPY");
-        // the tag of this call's counts: unique in the process (a count stored by an earlier call -- of
-        // any ctx: freed workspaces are reused -- never matches; the counts start zeroed, tag 0 unused)
-        static std::atomic<uint32_t> epoch{0};
-        uint32_t ep = ++epoch;
-        if (ep == 0) ep = ++epoch;
-        p.sc_epoch = ep;
-        p.self_copy = !piped && dpt::self_copy_built() && sce && !strcmp(sce, "1") && !padded && !edges && !(mode_flags & (DPT_FLAG_UNCAPPED | DPT_FLAG_LEN_ONLY)) &&
-                      (n_str + dpt::FIN_BATCH - 1) / dpt::FIN_BATCH >= dpt::SC_MIN_BATCHES;
     }
     p.max_blocks = c->max_blocks;
     p.arena = c->arena;
@@ -719,15 +580,9 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
     p.hist_overwrite = hist_overwrite;
     p.ctr_snap = ctr_snap;
     p.no_fallback = no_fallback;
-    if (piped) {
-        p.csr_stream = c->pipe;
-        p.ev_tok = c->ev_tok;
-        p.ev_fin = c->ev_fin[c->cur];
-    }
     p.n_bytes = n_bytes;
-    p.lite = piped || getenv("DPT_LITE");   // (DPT_LITE: the LDS-free CSR pass without the pipeline, for A/Bs)
     // (a per-string dp_tokenize call: one launch instead of two -- the finish kernel was 5 us of its 43)
-    p.solo = !getenv("DPT_NO_SOLO") && no_fallback && n_str == 1 && !padded && !edges && !hist && !c->profile && !p.self_copy && ctr_snap;
+    p.solo = !getenv("DPT_NO_SOLO") && no_fallback && n_str == 1 && !padded && !edges && !hist && !c->profile && ctr_snap;
     if (padded) {   // the ids go straight to their final place (int32), the counts to the caller's array
         p.staging = ids;
         p.staging16 = nullptr;
@@ -758,10 +613,7 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
         c->flag_parity = 0;
         return hip_fail(e, "encode launch");
     }
-    if (!padded && (dpt::fin_fold(n_str) || p.self_copy)) c->flag_parity ^= 1;   // the finish pass zeroed the other region
-    c->last_sc = p.self_copy ? p.flags : nullptr;
-    c->last_sc_nb = p.self_copy ? (n_str + dpt::FIN_BATCH - 1) / dpt::FIN_BATCH : 0;
-    c->last_sc_n = n_str;
+    if (!padded && dpt::fin_fold(n_str)) c->flag_parity ^= 1;   // the finish pass zeroed the other region
     return DPT_OK;
 }
 

@@ -34,20 +34,11 @@ struct EncodeLaunch {
     unsigned long long *flags;   // the batch lines (BS_LINE below): per FIN_BATCH-string batch, the sum of its counts,
                                  //   added by the tokenize passes as strings finish; zeroed for the next call
     unsigned long long *bpre;    // per batch (dense): its exclusive id prefix (batch_scan_kernel)
-    unsigned long long *inc;     // flags + BS_INC (self-copy): per batch SC_PUB + inclusive id prefix
-    uint32_t *copied;            // flags + BS_COPIED (self-copy): per batch, strings the first pass copied into place
-    unsigned long long *zero_other;   // fold / self-copy calls: the other parity's batch lines, zeroed for the next call ...
+    unsigned long long *zero_other;   // fold calls: the other parity's batch lines, zeroed for the next call ...
     uint64_t zero_n;             // ... (batches)
-    bool self_copy;              // the first pass copies its strings' ids into the CSR arrays (dpt_kernels.hip)
-    uint4 *cq;                   // self-copy: per wave, CQ_CAP queued {string, count, staging element}
-    uint32_t sc_epoch;           // self-copy: the call's tag for its counts (never 0)
     uint64_t *ctr_snap;          // nullable (host path): the counter block's first 64 bytes, copied here by its reset
     bool no_fallback;            // the host checked that no string needs the 2048-byte or unbounded pass: skip them
     uint64_t n_bytes = 0;        // the call's input bytes
-    bool lite = false;           // the CSR pass without LDS (finish_lite_kernel): it can run beside a first pass
-    hipStream_t csr_stream = nullptr;   // non-null (pipelined calls, dpt_ctx_pipeline): the CSR pass goes on this stream,
-    hipEvent_t ev_tok = nullptr, ev_fin = nullptr;   // after ev_tok (recorded on the call's stream after the other passes); ev_fin is
-                                 //   recorded after it (the workspace set it read is free again)
     bool solo;                   // one-string host-path call without fallbacks, histogram, edges or profiling: the first
                                  //   pass writes the CSR arrays itself (ids at 0.., id_off = {0, count}) and resets
                                  //   the counter block (its snapshot to ctr_snap); nothing else is launched
@@ -98,18 +89,8 @@ constexpr unsigned FIN_MAX_BINS = 1024;   // histogram bins the finish pass fold
 // Batch lines (EncodeLaunch::flags): one 128-byte line per batch, so the strings finishing in
 // neighbouring batches -- the first pass's partitions run through the batches side by side -- add to
 // different lines (16 batches' sums in one line serialised the adds: +0.05 ms at cfg2, +11 % at 125k
-// strings, profiles/r04d_ab.log).  u64 [BS_SUM]: the count sum in bits 0..39 (a batch holds < 2^40 ids)
-// and, from the first pass, its strings finished there in bits 40.. -- one atomic add per string;
-// [BS_INC] (self-copy): SC_PUB | the batch's inclusive id prefix once known; [BS_COPIED] (u32, self-copy):
-// strings the first pass copied into place.
-constexpr unsigned BS_LINE = 16, BS_INC = 1, BS_COPIED = 2;
-constexpr unsigned BS_FIN_SHIFT = 40;
-constexpr unsigned long long BS_SUM_MASK = (1ull << BS_FIN_SHIFT) - 1;
-constexpr unsigned long long SC_PUB = 1ull << 63;
-constexpr unsigned long long SC_VAL_MASK = (1ull << 56) - 1;
-constexpr unsigned CQ_CAP = 32;            // strings a wave's copy queue holds
-constexpr unsigned SC_MIN_QUEUE = 8;       // queued strings before a copy step (a step costs round trips)
-constexpr uint64_t SC_MIN_BATCHES = 8;     // calls of fewer batches take the finish pass's copy alone
+// strings, profiles/r04d_ab.log).  u64 [0]: the count sum -- one atomic add per finished string.
+constexpr unsigned BS_LINE = 16;
 constexpr size_t PART_CTR_OFFSET = 256;
 constexpr size_t CTR_ALLOC_BYTES = PART_CTR_OFFSET + (NPART_MAX + 1) * PART_STRIDE * 4;
 
@@ -213,8 +194,6 @@ struct LongLaunch {
 hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t ev[2]);
 size_t wsl_scratch_bytes(unsigned max_blocks);
 size_t pend_scratch_bytes(unsigned max_blocks);
-size_t cq_scratch_bytes(unsigned max_blocks);
-bool self_copy_built();   // the library was built with the first pass's self-copy (make sc)
 hipError_t launch_histogram(const uint64_t *id_off, const int32_t *status, uint64_t n_str, int64_t *hist,
                             uint32_t n_bins, hipStream_t stream);
 hipError_t kernel_init();

@@ -52,9 +52,9 @@
 namespace dpt {
 
 // Compile-time options are diagnostics only (DPT_STOP, DPT_C2STOP, DPT_STAMPS: wrong results or extra
-// counters by design, never in the product build) plus DPT_SC_BUILD (the self-copy experiment, its own
-// library).  The alternatives measured slower or neutral are gone from the source; DESIGN.md §9 lists
-// them with their numbers.
+// counters by design, never in the product build).  The alternatives measured slower or neutral are
+// gone from the source (the round-4 self-copy and pipelined CSR pass: git tag r04-experiments);
+// DESIGN.md §9 lists them with their numbers.
 
 // ------------------------------------------------------------------ wave primitives
 
@@ -271,7 +271,7 @@ struct SlotState {
     uint32_t abase;
     uint16_t wlen, n_atoms, n_words;
     uint8_t active, status, inval, capb;   // capb: some atom of the window is not a token by itself (the cap can bind)
-    uint8_t qh, qt;                        // SS[0] only: the wave's copy-queue head and tail (self-copy; mod 256)
+    uint8_t pad[2];
 };
 static_assert(sizeof(SlotState) == 48, "slot state layout");
 
@@ -356,13 +356,6 @@ struct EncodeArgs {
     int mode;                   // DPT_MODE_* | DPT_FLAG_*
     unsigned long long *hist_zero;   // 2048-byte pass, fin_fold calls with DPT_HIST_OVERWRITE: the histogram to
     uint32_t n_hist;                 //   zero before the finish pass adds to it (the scan kernel's duty otherwise)
-    // self-copy (first pass of CSR calls; inc == nullptr: off): see sc_step in tokenize_kernel
-    unsigned long long *inc;    // per batch (BS_LINE apart): SC_PUB | inclusive id prefix
-    uint32_t *copied;           // per batch (2 BS_LINE apart): strings copied into place
-    uint4 *cq;                  // per wave: CQ_CAP queued {string, count, staging element lo, hi} (ring; head / tail in
-                                //   slot 0's SlotState qh / qt)
-    uint32_t sc_epoch;          // the tag of this call's counts (sc_copy_run); never 0
-    uint32_t *route_c;          // ~(first batch holding a string routed to a later pass), 0: none (atomicMax)
     uint64_t *id_off;
     int32_t *ids;
     // one-string host-path calls (EncodeLaunch::solo): the string's ids go straight to ids (staging =
@@ -760,11 +753,6 @@ constexpr unsigned A_REFILL64 = 32;   // the same for the 64-lane kernels (8 / 1
                      // + lane-mode B's cut points / recurrence / transfer scan + fix-up, 3 = + B/C0/C1
 #define DPT_STOP 9
 #endif
-#ifdef DPT_SC_BUILD   // the first pass's self-copy (sc_prefix ..): compiled in only on request -- its cold code cost
-constexpr bool SC_ON = true;   // the first pass 1 % even when switched off (profiles/r04h_ab.log), and it is slower
-#else                          // than the finish pass's copy so far
-constexpr bool SC_ON = false;
-#endif
 #ifndef DPT_C2STOP   // diagnostic builds only (wrong results): C2 stops after its bulk pass (1) / hash pass (2)
 #define DPT_C2STOP 0
 #endif
@@ -799,7 +787,7 @@ __device__ __forceinline__ TrieView tv_of(ConstKernArgs *kp) {
 // Counter block (EncodeLaunch::retry_count, CTR_ALLOC_BYTES; zeroed once at allocation, then reset for
 // the next call by the batch scan or the finish pass -- or, in a one-string host-path call, by the lone
 // wave of the first pass): uint32 [0] retry count, [1] 2048-byte blocks done (fallback_kernel), [2]
-// 2048-byte pass work, [3] long count, [4] long work, [5] self-copy route mark, [6] fallback_kernel's
+// 2048-byte pass work, [3] long count, [4] long work, [5] unused, [6] fallback_kernel's
 // block ticket; uint64 [4] (byte
 // 32) the unbounded pass's claimed bytes, [5] (byte 40) the last call's claimed bytes
 // (dpt_ctx_long_need), [6] (byte 48) far edge pairs found, [7] (byte 56) the last call's far edge pairs
@@ -822,145 +810,6 @@ __device__ __forceinline__ void reset_counters(uint32_t *ctr, uint64_t *snap = n
     ctr[0] = 0; ctr[1] = 0; ctr[2] = 0; ctr[3] = 0; ctr[4] = 0; ctr[5] = 0; ctr[6] = 0;
     uint32_t *pc = ctr + PART_CTR_OFFSET / 4;
     for (unsigned q = 0; q <= NPART; q++) pc[q * PART_STRIDE] = 0;   // the partition counters and the mask
-}
-
-// ---- self-copy (first pass of CSR calls, a.inc != nullptr).  The finish pass used to copy every
-// staged id into the CSR arrays after this kernel (0.33 ms, 13 % of a cfg2 step, half its HBM
-// traffic).  Here the wave that finished a string copies its ids itself once the string's offset is
-// known: the string waits in the wave's copy queue (a.cq, CQ_CAP entries) until its FIN_BATCH-string
-// batch is complete and the batches before it are complete or published, which happens about a round
-// later since the partitions advance through the batch side by side.  Cross-wave data goes through
-// agent-scope atomics and sc1 loads / stores only (MI355X: per-XCD L2s are not coherent; 8-byte
-// granules need no ordering and no release fence):
-//   * a finishing string adds count | 1 << BS_FIN_SHIFT to its batch's sum (a batch is complete when
-//     all its strings have added: its sum is then final) and stores its count TAGGED with the call's
-//     epoch, a.sc_epoch << 32 | count (the in-batch offsets read the counts, and the tag says the store
-//     has landed);
-//   * a batch's exclusive prefix is the nearest published inclusive prefix before it (up to 63 back)
-//     plus the sums of the complete batches in between, all read by ONE wave-wide load; the wave that
-//     finds it publishes every prefix on the way (the same value whoever stores it: plain sc1 stores, no
-//     claim, no chain of round trips from batch to batch);
-//   * a queued string's ids are read from the wave's own staging (its own stores: only the L1 could be
-//     stale, so the loads are sc1) and stored at ids[prefix + the counts of the batch's strings before it].
-// Strings of a batch holding a string routed to a later pass never complete it here (a.route_c drops
-// the queues' strings from there on), and strings that do not fit the queue, stay for the finish pass:
-// it writes every id_off entry and copies every batch the first pass did not copy whole.  The id_off[s+1]
-// of a string is the CSR offset (tokenizer_utils.py:76-79: ids concatenated per string).
-// (Cold code, kept out of line: inlined into the tokenize loop it cost 8 SGPR + 8 VGPR spills.)
-__device__ __forceinline__ unsigned long long sc_ld(const unsigned long long *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void sc_st(unsigned long long *p, unsigned long long v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ unsigned long long sc_readlane64(unsigned long long v, unsigned l) {
-    return ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), l) << 32) |
-           (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, l);
-}
-__device__ __forceinline__ unsigned sc_size(uint64_t n_str, uint64_t b) {
-    const uint64_t rem = n_str - b * FIN_BATCH;
-    return rem < FIN_BATCH ? (unsigned)rem : FIN_BATCH;
-}
-// The ids before batch b (uniform), or ~0ull while b is incomplete or a batch between it and the nearest
-// published one (up to 63 back) is.  Lane l reads batch b - l's line; publishes what it computes.
-template <typename A>
-__device__ __forceinline__ unsigned long long sc_prefix(const A &a, unsigned b, unsigned lane) {
-    const int k = (int)b - (int)lane;
-    unsigned long long pv = SC_PUB, sv = 0;   // before batch 0: published, prefix 0
-    if (k >= 0) {
-        pv = sc_ld(a.inc + (size_t)k * BS_LINE);
-        sv = sc_ld(a.bsum + (size_t)k * BS_LINE);
-    }
-    const bool comp = k < 0 || (sv >> BS_FIN_SHIFT) == sc_size(a.n_str, (uint64_t)k);
-    const uint64_t cm = ballot(comp);
-    if (!(cm & 1ull)) return ~0ull;   // b itself is not complete
-    const unsigned long long x = comp ? (sv & BS_SUM_MASK) : 0ull;
-    uint64_t pm = ballot((pv & SC_PUB) != 0);
-    if (pm & 1ull) return (sc_readlane64(pv, 0) & SC_VAL_MASK) - sc_readlane64(x, 0);   // b is published
-    pm &= ~1ull;
-    if (!pm) return ~0ull;
-    const unsigned l0 = (unsigned)__builtin_ctzll(pm);
-    const uint64_t need = (1ull << l0) - 1ull;   // batches b - l0 + 1 .. b
-    if ((cm & need) != need) return ~0ull;
-    const unsigned long long xi = lane < l0 ? x : 0ull;
-    const unsigned long long sc = wave_incl_scan_add64(xi, lane);
-    const unsigned long long P0 = sc_readlane64(pv, l0) & SC_VAL_MASK, tot = sc_readlane64(sc, 63);
-    // batch b - lane's inclusive prefix: P0 + the sums of batches b - l0 + 1 .. b - lane
-    if (lane < l0) sc_st(a.inc + (size_t)k * BS_LINE, SC_PUB | (P0 + tot - sc + xi));
-    return P0 + tot - sc_readlane64(x, 0);
-}
-// The copy queue's n entries from qh: the head's batch prefix (*E), and the length of the run of entries
-// from the head in that batch (0: not ready yet; ~0u: drop the queue, a string before them went to a
-// later pass).
-__device__ __noinline__ unsigned sc_ready(ConstKernArgs *kp, unsigned bid, unsigned qh, unsigned n, unsigned lane,
-                                          unsigned long long *E) {
-    const auto &a = kp->ea;
-    unsigned s = 0;
-    if (lane < n) s = a.cq[(size_t)bid * CQ_CAP + ((qh + lane) % CQ_CAP)].x;
-    const unsigned bh = (unsigned)__builtin_amdgcn_readlane((int)s, 0) / FIN_BATCH;
-    if (const unsigned rc = uni(__hip_atomic_load(a.route_c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)); rc && bh >= ~rc) return ~0u;
-    const unsigned long long e = sc_prefix(a, bh, lane);
-    if (e == ~0ull) return 0;
-    *E = e;
-    const uint64_t run = ballot(lane < n && s / FIN_BATCH == bh);
-    return ~run ? (unsigned)__builtin_ctzll(~run) : 64u;
-}
-// Copy the queue's npop entries from qh (strings of one batch, whose first id is E): string s's cnt
-// staged ids (this wave's own stores, read sc1: only this CU's L1 could hold a stale line another wave
-// read) to ids[E + the counts of the batch's strings before s ..].  0: a count has not landed yet
-// (nothing copied).
-__device__ __noinline__ unsigned sc_copy_run(ConstKernArgs *kp, unsigned bid, unsigned qh, unsigned npop, unsigned lane,
-                                             bool w16, unsigned long long E) {
-    const auto &a = kp->ea;
-    uint4 e = make_uint4(0u, 0u, 0u, 0u);
-    if (lane < npop) e = a.cq[(size_t)bid * CQ_CAP + ((qh + lane) % CQ_CAP)];
-    const unsigned b = (unsigned)__builtin_amdgcn_readlane((int)e.x, 0) / FIN_BATCH;
-    const uint64_t s0 = (uint64_t)b * FIN_BATCH;
-    const unsigned nsz = sc_size(a.n_str, b);
-    const unsigned long long tag = (unsigned long long)a.sc_epoch << 32;
-    unsigned long long c[4], t = 0;
-    bool missing = false;
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-        const unsigned i = 4u * lane + (unsigned)u;
-        c[u] = i < nsz ? sc_ld(reinterpret_cast<const unsigned long long *>(a.counts) + s0 + i) : tag;
-        missing |= (c[u] & ~0xFFFFFFFFull) != tag;
-        c[u] &= 0xFFFFFFFFull;
-        t += c[u];
-    }
-    if (ballot(missing)) return 0;
-    const unsigned long long ex = wave_incl_scan_add64(t, lane) - t;   // ids of strings s0 .. s0 + 4 lane - 1
-    for (unsigned q = 0; q < npop; q++) {
-        const unsigned i = (unsigned)__builtin_amdgcn_readlane((int)e.x, q) - (unsigned)s0;
-        const unsigned cnt = __builtin_amdgcn_readlane(e.y, q);
-        const uint64_t src = ((uint64_t)__builtin_amdgcn_readlane(e.w, q) << 32) | (unsigned)__builtin_amdgcn_readlane(e.z, q);
-        const unsigned L = i >> 2, u = i & 3u;
-        uint64_t o0 = E + sc_readlane64(ex, L);
-        if (u > 0) o0 += sc_readlane64(c[0], L);
-        if (u > 1) o0 += sc_readlane64(c[1], L);
-        if (u > 2) o0 += sc_readlane64(c[2], L);
-        const uint8_t *sb = w16 ? reinterpret_cast<const uint8_t *>(a.staging16 + src) : reinterpret_cast<const uint8_t *>(a.staging + src);
-        const unsigned al = (unsigned)((uintptr_t)sb & 3u);   // (a dword-aligned resource base)
-        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)(sb - al), (short)0, (int)(al + cnt * (w16 ? 2u : 4u)), 0x00020000);
-        int32_t *dst = a.ids + o0;
-        for (unsigned k0 = 0; k0 < cnt; k0 += 256u) {
-            int32_t v[4];
-#pragma unroll
-            for (int u2 = 0; u2 < 4; u2++) {
-                const unsigned k = k0 + 64u * (unsigned)u2 + lane;
-                // aux 16: sc1 (past cnt the range check reads 0)
-                v[u2] = w16 ? (int32_t)(int16_t)__builtin_amdgcn_raw_buffer_load_b16(r, al + 2u * k, 0, 16)
-                            : (int32_t)__builtin_amdgcn_raw_buffer_load_b32(r, al + 4u * k, 0, 16);
-            }
-#pragma unroll
-            for (int u2 = 0; u2 < 4; u2++) {
-                const unsigned k = k0 + 64u * (unsigned)u2 + lane;
-                if (k < cnt) dst[k] = v[u2];
-            }
-        }
-    }
-    if (lane == 0) atomicAdd(a.copied + (size_t)b * (2 * BS_LINE), npop);
-    return npop;
 }
 
 // SW: staged id width 0 = by a.staging16, 1 = int16, 2 = int32; RAW: DPT_MODE_RAW as a compile-time
@@ -1004,9 +853,7 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
     // Strings are handed out by npart device counters (each in its own 256-byte line).  Partition p
     // holds the FIN_BATCH-string chunks p, p + npart, p + 2 npart, ... of the batch, in that order
     // (part_size / part_string): the partitions advance through the batch side by side, so strings
-    // finish roughly in batch order and the CSR offsets of a finished string become known about a
-    // round later (the first pass copies its own strings' ids into place: self_copy below).  A
-    // wave claims as many strings as it has free slots from its current partition (starting on
+    // finish roughly in batch order.  A wave claims as many strings as it has free slots from its current partition (starting on
     // blockIdx mod npart) and, when a claim reaches the partition's end, marks the partition in a
     // shared mask and moves to the next unmarked one.  Round 1's single counter (one same-address
     // atomic per refill) bound the whole kernel: a prep-only build ran 2.91 of the full build's 2.99
@@ -1095,34 +942,9 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
         }
     };
 
-    // ---- self-copy: see sc_ready / sc_copy_run above
-    auto sc_step = [&](bool draining) -> unsigned {   // strings copied (uniform)
-        const unsigned qh = uni(SSr(0).qh), qt = uni(SSr(0).qt);
-        const unsigned n = (qt - qh) & 0xFFu;
-        if (!n) return 0;
-        if (!draining && n < SC_MIN_QUEUE) return 0;   // (a step costs round trips: every few rounds)
-        unsigned long long E = 0;
-        unsigned npop = sc_ready(kp, bid, qh, n, lane, &E);
-        if (npop == ~0u) {   // a string before them went to a later pass: the finish pass copies the queue's strings
-            if (lane == 0) SSr(0).qh = (uint8_t)qt;
-            return 0;
-        }
-        if (!npop) return 0;
-        if constexpr (G == 16 && !BIG)
-            if (n_pend) {   // the strings' residual ids are still in the pending row
-                walk_pending(n_pend);
-                n_pend = 0;
-            }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's staging stores are out
-        npop = sc_copy_run(kp, bid, qh, npop, lane, SW == 1 || (SW == 0 && a.staging16 != nullptr), uni64(E));
-        if (lane == 0) SSr(0).qh = (uint8_t)(qh + npop);
-        return npop;
-    };
-    auto st_agent = [](unsigned long long *p, unsigned long long v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
     STAMP_DECL
 
     if (lane < (unsigned)NG) SSr(lane).active = 0;
-    if (lane == 0) { SSr(0).qh = 0; SSr(0).qt = 0; }
     wave_sync();
 
     for (;;) {
@@ -1205,19 +1027,7 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                     a.status[s] = (int32_t)status;
                     if (a.capped) a.capped[s] = status == 2 ? 0 : -1;
                     S.active = 0;
-                    if (!BIG && SC_ON && a.inc) {   // self-copy: finished with no ids (empty), or routed to a later pass
-                        const unsigned b = (unsigned)(s / FIN_BATCH);
-                        if (status == 3) {
-                            a.counts[s] = 0;
-                            atomicMax(a.route_c, ~b);
-                        } else {
-                            st_agent(reinterpret_cast<unsigned long long *>(a.counts) + s, (unsigned long long)a.sc_epoch << 32);
-                            atomicAdd(a.bsum + (size_t)b * BS_LINE, 1ull << BS_FIN_SHIFT);   // finished here
-                            atomicAdd(a.copied + (size_t)b * (2 * BS_LINE), 1u);           // nothing to copy
-                        }
-                    } else {
-                        a.counts[s] = 0;
-                    }
+                    a.counts[s] = 0;
                 }
                 refill = true;
             }
@@ -2609,9 +2419,6 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
 
         // ---------------------------------------------------------- advance slots, finish strings
         KREFRESH();
-        bool fq = false;            // self-copy: a string with ids finished here (queued below)
-        unsigned fq_s = 0, fq_n = 0;
-        uint64_t fq_sb = 0;
         if (lane < (unsigned)NG) {
             SlotState &S = SSr(lane);
             if (S.active && S.n_atoms > 0 && S.status == 0 && (S.inval & 2)) {
@@ -2619,7 +2426,6 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                 // unbounded pass redoes the whole string (and writes its status and count)
                 a.long_list[atomicAdd(a.long_count, 1u)] = S.s;
                 S.active = 0;
-                if (!BIG && SC_ON && a.inc) atomicMax(a.route_c, ~(S.s / FIN_BATCH));   // self-copy: routed to a later pass
             } else if (S.active && S.n_atoms > 0) {
                 S.capsum += S.wtok;
                 if (S.status == 0 && S.inval) S.status = 1;
@@ -2632,42 +2438,13 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                     a.status[s] = (int32_t)S.status;
                     if (a.capped) a.capped[s] = S.status == 3 ? -1 : (int32_t)S.capsum;
                     S.active = 0;
-                    // (self-copy: every string finished here counts, sc_prefix)
-                    const bool sc = !BIG && SC_ON && a.inc;
-                    if (a.bsum && (cnt || sc)) atomicAdd(a.bsum + (s / FIN_BATCH) * BS_LINE, cnt | (sc ? 1ull << BS_FIN_SHIFT : 0ull));
-                    if (sc) {
-                        // the count tagged with the call's epoch: the tag says it has landed (sc_copy_run)
-                        st_agent(reinterpret_cast<unsigned long long *>(a.counts) + s, ((unsigned long long)a.sc_epoch << 32) | cnt);
-                        if (!cnt) atomicAdd(a.copied + (s / FIN_BATCH) * (2 * BS_LINE), 1u);   // nothing to copy
-                        fq = cnt != 0;
-                        fq_s = (unsigned)s;
-                        fq_n = (unsigned)cnt;
-                        fq_sb = S.sb;
-                    } else {
-                        a.counts[s] = cnt;
-                    }
+                    if (a.bsum && cnt) atomicAdd(a.bsum + (s / FIN_BATCH) * BS_LINE, cnt);
+                    a.counts[s] = cnt;
                 }
             }
         }
         wave_sync();
         STAMP(4);
-        if (!BIG && SC_ON && a.inc) {
-            // queue the strings that finished with ids (the rest of a full queue stays for the finish pass),
-            // then one step of the queue
-            const uint64_t fm = ballot(fq);
-            if (fm) {
-                const unsigned qh = uni(SSr(0).qh), qt = uni(SSr(0).qt);
-                const unsigned room = CQ_CAP - ((qt - qh) & 0xFFu);
-                const unsigned rk = __builtin_amdgcn_mbcnt_hi((unsigned)(fm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)fm, 0u));
-                if (fq && rk < room)
-                    a.cq[(size_t)bid * CQ_CAP + ((qt + rk) % CQ_CAP)] = make_uint4(fq_s, fq_n, (uint32_t)fq_sb, (uint32_t)(fq_sb >> 32));
-                const unsigned nq = (unsigned)__builtin_popcountll(fm);
-                if (lane == 0) SSr(0).qt = (uint8_t)(qt + (nq < room ? nq : room));
-                wave_sync();
-            }
-            (void)sc_step(false);
-            wave_sync();
-        }
         STAMP(8);
     }
     if constexpr (G == 16 && !BIG)
@@ -2675,19 +2452,6 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
             walk_pending(n_pend);
             n_pend = 0;
         }
-    if (!BIG && SC_ON && a.inc) {
-        // the queue's last strings: their batches complete as the other waves finish (every string is
-        // claimed by now, by running waves); bounded -- what is left stays for the finish pass
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (uni(SSr(0).qh) != uni(SSr(0).qt)) {
-            if (sc_step(true)) {
-                wave_sync();
-                continue;
-            }
-            if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) break;   // 200 ms at 100 MHz
-            __builtin_amdgcn_s_sleep(8);
-        }
-    }
     if (!BIG && a.solo && lane == 0) {   // the call's only string, the grid's only wave
         a.id_off[0] = 0;
         reset_counters(a.retry_count, a.ctr_snap);
@@ -2760,7 +2524,7 @@ __global__ void __launch_bounds__(SCAN_THREADS) batch_scan_kernel(uint64_t n_str
         uint64_t v[PER_REG];
 #pragma unroll
         for (unsigned u = 0; u < PER_REG; u++) {
-            v[u] = c0 + u < c1 ? bsum[(c0 + u) * BS_LINE] & BS_SUM_MASK : 0ull;
+            v[u] = c0 + u < c1 ? bsum[(c0 + u) * BS_LINE] : 0ull;
             sum += v[u];
         }
         uint64_t run = block_incl_scan_add64<SCAN_THREADS>(sum, s_w, &total) - sum;
@@ -2773,10 +2537,10 @@ __global__ void __launch_bounds__(SCAN_THREADS) batch_scan_kernel(uint64_t n_str
             run += v[u];
         }
     } else {
-        for (uint64_t k = c0; k < c1; k++) sum += bsum[k * BS_LINE] & BS_SUM_MASK;
+        for (uint64_t k = c0; k < c1; k++) sum += bsum[k * BS_LINE];
         uint64_t run = block_incl_scan_add64<SCAN_THREADS>(sum, s_w, &total) - sum;
         for (uint64_t k = c0; k < c1; k++) {
-            const uint64_t b = bsum[k * BS_LINE] & BS_SUM_MASK;
+            const uint64_t b = bsum[k * BS_LINE];
             bpre[k] = run;
             bsum[k * BS_LINE] = 0;
             run += b;
@@ -2803,8 +2567,6 @@ struct FinishArgs {
     int hist_store;                   // ... stored, not added (DPT_HIST_OVERWRITE in a one-batch call) ...
     const int32_t *status;            // ... with the statuses it counts
     uint32_t n_bins;
-    unsigned long long *inc;          // self-copy calls (finish_kernel<ST, true>): per batch SC_PUB + prefix (BS_LINE apart)
-    const uint32_t *copied;           // ... and the strings the first pass copied into place (2 BS_LINE apart)
     uint64_t *ctr_snap;               // nullable: the counter block's first 64 bytes before the reset (reset_counters)
 };
 
@@ -2815,15 +2577,11 @@ struct FinishArgs {
 // per thread.  At 1M strings a batch is one block (3 907 blocks); small calls split each batch's copy
 // so the grid still has ~FIN_TARGET_BLOCKS blocks (a block's copy is a chain of dependent load rounds:
 // 125k strings were 489 blocks of 7 rounds each).
-// SC (self-copy calls): every batch takes its first id from a look-back -- the nearest prefix the first
-// pass or another block published, plus the final batch sums after it -- publishes its own and writes
-// its id_off entries; the ids of batches the first pass did not copy whole are copied here as usual.
-template <typename ST, bool SC = false>
+template <typename ST>
 __global__ void __launch_bounds__(FIN_THREADS) finish_kernel(FinishArgs f) {
     __shared__ uint64_t s_rel[FIN_BATCH + 1];   // ids of the batch's strings before string k, + the batch total
     __shared__ uint64_t s_src[FIN_BATCH];       // staging element of each string's first id
     __shared__ uint64_t s_w[FIN_THREADS / 64];
-    __shared__ unsigned s_pub;                  // SC look-back: the nearest published batch, as a distance
     const unsigned tid = threadIdx.x;
     const uint64_t t = blockIdx.x / f.slices;
     const unsigned sl = blockIdx.x % f.slices;
@@ -2832,48 +2590,16 @@ __global__ void __launch_bounds__(FIN_THREADS) finish_kernel(FinishArgs f) {
     const uint64_t s0 = t * FIN_BATCH;
     // the first FIN_BATCH threads hold one string each; every thread copies
     const bool has = tid < FIN_BATCH && tid < f.n_str - s0;
-    const uint64_t c = has ? f.counts[s0 + tid] & 0xFFFFFFFFull : 0ull;   // (self-copy calls tag the counts)
+    const uint64_t c = has ? f.counts[s0 + tid] : 0ull;
     const uint64_t src = has ? f.str_off[s0 + tid] - base_off : 0ull;
     uint64_t total;
     uint64_t o0 = 0;   // one batch: its first id is 0
-    bool done = false;   // SC: the first pass copied the whole batch
-    if constexpr (SC) {
-        for (uint64_t k = (uint64_t)blockIdx.x * FIN_THREADS + tid; k < f.fold_n; k += (uint64_t)gridDim.x * FIN_THREADS)
-            for (unsigned w = 0; w <= BS_COPIED; w++) f.fold_zero[k * BS_LINE + w] = 0;   // the other parity's lines, for the next call
-        const uint64_t nsz = f.n_str - s0 < FIN_BATCH ? f.n_str - s0 : FIN_BATCH;
-        done = f.copied[t * (2 * BS_LINE)] == nsz;
-        {
-            // look-back: the ids before batch t = the nearest published inclusive prefix + the sums after it
-            uint64_t acc = 0;
-            for (uint64_t top = t;;) {
-                const int64_t k = (int64_t)top - 1 - (int64_t)tid;
-                unsigned long long pv = SC_PUB;   // k < 0: before the first batch, prefix 0
-                if (k >= 0) pv = __hip_atomic_load(&f.inc[k * BS_LINE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (tid == 0) s_pub = FIN_THREADS;
-                __syncthreads();
-                if (pv & SC_PUB) atomicMin(&s_pub, tid);
-                __syncthreads();
-                const unsigned l0 = s_pub;
-                uint64_t part = 0, sum = 0;
-                if (tid < l0 && k >= 0) part = f.fold[k * BS_LINE] & BS_SUM_MASK;
-                (void)block_incl_scan_add64<FIN_THREADS>(part, s_w, &sum);
-                acc += sum;
-                if (l0 < FIN_THREADS) {
-                    if (tid == l0) s_w[0] = pv & SC_VAL_MASK;   // (s_w is free again after the scan)
-                    __syncthreads();
-                    o0 = acc + s_w[0];
-                    __syncthreads();
-                    break;
-                }
-                top -= FIN_THREADS;   // (top > FIN_THREADS here: k < 0 counts as published)
-            }
-        }
-    } else if (f.fold) {   // the batch's first id: the sums of the batches before it (t <= FIN_FOLD_MAX)
+    if (f.fold) {   // the batch's first id: the sums of the batches before it (t <= FIN_FOLD_MAX)
         uint64_t ps = 0;
-        for (uint64_t k = tid; k < t; k += FIN_THREADS) ps += f.fold[k * BS_LINE] & BS_SUM_MASK;
+        for (uint64_t k = tid; k < t; k += FIN_THREADS) ps += f.fold[k * BS_LINE];
         (void)block_incl_scan_add64<FIN_THREADS>(ps, s_w, &o0);
         for (uint64_t k = (uint64_t)blockIdx.x * FIN_THREADS + tid; k < f.fold_n; k += (uint64_t)gridDim.x * FIN_THREADS)
-            for (unsigned w = 0; w <= BS_COPIED; w++) f.fold_zero[k * BS_LINE + w] = 0;   // (a self-copy call's too)
+            f.fold_zero[k * BS_LINE] = 0;
     } else if (!f.bsum) {
         o0 = f.bpre[t];
     }
@@ -2913,8 +2639,6 @@ __global__ void __launch_bounds__(FIN_THREADS) finish_kernel(FinishArgs f) {
             else if (lh[b]) atomicAdd(&f.hist[b], lh[b]);
         }
     }
-    if (SC && sl == 0 && tid == 0)   // for the later batches' look-backs (the first pass may have stored the same)
-        __hip_atomic_store(&f.inc[t * BS_LINE], SC_PUB | (o0 + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (sl == 0) {
         if (has) f.id_off[s0 + tid + 1] = o0 + incl;
         if (t == 0 && tid == 0) {
@@ -2924,7 +2648,6 @@ __global__ void __launch_bounds__(FIN_THREADS) finish_kernel(FinishArgs f) {
             if (f.ctr) reset_counters(f.ctr, f.ctr_snap);
         }
     }
-    if (SC && done) return;   // the first pass copied the batch's ids
     const uint64_t k_beg = total * sl / f.slices, k_end = total * (sl + 1) / f.slices;
     constexpr unsigned U = FIN_U;
     // the string of this thread's first id: the last string whose start is <= it (binary search;
@@ -2957,164 +2680,6 @@ __global__ void __launch_bounds__(FIN_THREADS) finish_kernel(FinishArgs f) {
             if (k < k_end) f.ids[o0 + k] = v[u];
         }
     }
-}
-
-// The CSR pass without LDS (pipelined calls, dpt_ctx_pipeline): ONE wave per batch, at most 64 VGPRs,
-// so it fits beside a running first pass -- whose waves hold every CU's LDS and 80 VGPRs x 5.5 waves
-// per SIMD -- and runs under the next call's first pass instead of after it.  The wave holds strings
-// lane + 64 u (u < 4): counts, staging offsets, exclusive prefixes by four wave scans; the copy goes
-// in rounds of up to 16 chunks of <= 64 ids (chunk u's source, destination and length parked in lane
-// u), the next round's loads issued before the current round's stores (a load waits for every older
-// store of the wave: one round trip per round, not two).  The histogram: one atomic per distinct count
-// value of the batch (peeled by ballots) and per status value.  Batch prefixes as in finish_kernel:
-// bpre (the scan kernel) or the fold sums; one-batch calls and DPT_HIST_OVERWRITE one-batch stores
-// take finish_kernel.
-template <typename ST>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) finish_lite_kernel(FinishArgs f) {
-    const unsigned lane = threadIdx.x;
-    const uint64_t t = blockIdx.x, s0 = t * FIN_BATCH;
-    const unsigned nsz = (unsigned)(f.n_str - s0 < FIN_BATCH ? f.n_str - s0 : FIN_BATCH);
-    // (32-bit per-string values relative to the batch: the host sends batches of 4 GiB of text or more
-    // to finish_kernel)
-    const uint64_t sbase = f.str_off[s0] - f.str_off[0];   // the batch's first staged id
-    const ST *__restrict__ staging = reinterpret_cast<const ST *>(f.staging) + sbase;
-    uint32_t c[4], src[4], ex[4];
-    uint64_t carry = 0;
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-        const unsigned i = lane + 64u * (unsigned)u;
-        const bool has = i < nsz;
-        c[u] = has ? (uint32_t)f.counts[s0 + i] : 0u;
-        src[u] = has ? (uint32_t)(f.str_off[s0 + i] - f.str_off[s0]) : 0u;
-    }
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-        const uint64_t incl = wave_incl_scan_add64(c[u], lane);
-        ex[u] = (uint32_t)(carry + incl - c[u]);
-        carry += sc_readlane64(incl, 63);
-    }
-    const uint64_t total = carry;
-    uint64_t o0 = 0;
-    if (f.fold) {   // the sums of the batches before this one; the other parity's lines zeroed
-        uint64_t ps = 0;
-        for (uint64_t k = lane; k < t; k += 64u) ps += f.fold[k * BS_LINE] & BS_SUM_MASK;
-        o0 = sc_readlane64(wave_incl_scan_add64(ps, lane), 63);
-        for (uint64_t k = t * 64u + lane; k < f.fold_n; k += (uint64_t)gridDim.x * 64u)
-            for (unsigned w = 0; w <= BS_COPIED; w++) f.fold_zero[k * BS_LINE + w] = 0;
-    } else {
-        o0 = f.bpre[t];
-    }
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-        const unsigned i = lane + 64u * (unsigned)u;
-        if (i < nsz) f.id_off[s0 + i + 1] = o0 + ex[u] + c[u];
-    }
-    if (t == 0 && lane == 0) {
-        f.id_off[0] = 0;
-        if (f.ctr) reset_counters(f.ctr, f.ctr_snap);
-    }
-    if (f.hist) {
-        const uint32_t top = f.n_bins - 1;
-        uint32_t pend = 0;   // bit u: string lane + 64 u still to count
-#pragma unroll
-        for (int u = 0; u < 4; u++) pend |= (lane + 64u * (unsigned)u < nsz ? 1u : 0u) << u;
-        const uint32_t live = pend;
-        for (;;) {   // one atomic per distinct bin of the batch
-            uint32_t cand = 0xFFFFFFFFu;
-#pragma unroll
-            for (int u = 3; u >= 0; u--) cand = ((pend >> u) & 1u) ? min(c[u], top) : cand;
-            const uint64_t any = ballot(cand != 0xFFFFFFFFu);
-            if (!any) break;
-            const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)cand, (int)__builtin_ctzll(any));
-            unsigned n = 0;
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const bool hit = ((pend >> u) & 1u) && min(c[u], top) == v;
-                n += (unsigned)__builtin_popcountll(ballot(hit));
-                pend &= ~((hit ? 1u : 0u) << u);
-            }
-            if (lane == 0) atomicAdd(&f.hist[v], (unsigned long long)n);
-        }
-        int32_t st[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            st[u] = -1;
-            if ((live >> u) & 1u) {
-                st[u] = f.status[s0 + lane + 64u * (unsigned)u];
-                st[u] = st[u] >= 0 && st[u] <= 4 ? st[u] : 4;
-            }
-        }
-#pragma unroll
-        for (int v = 0; v < 5; v++) {
-            unsigned n = 0;
-#pragma unroll
-            for (int u = 0; u < 4; u++) n += (unsigned)__builtin_popcountll(ballot(st[u] == v));
-            if (lane == 0 && n) atomicAdd(&f.hist[f.n_bins + 2 + v], (unsigned long long)n);
-        }
-        if (lane == 0) {
-            atomicAdd(&f.hist[f.n_bins], (unsigned long long)total);
-            atomicAdd(&f.hist[f.n_bins + 1], (unsigned long long)nsz);
-        }
-    }
-    // ---- the copy: chunks of the batch's strings in order (string j, ids 64 m .. 64 m + 63)
-#define LITE_PICK(r, jj) ((uint32_t)__builtin_amdgcn_readlane((int)(((jj) >> 6) == 0 ? r[0] : (((jj) >> 6) == 1 ? r[1] : (((jj) >> 6) == 2 ? r[2] : r[3]))), (int)((jj) & 63u)))
-    unsigned j = 0, m = 0;
-    uint32_t cj = 0, sj = 0, dj = 0;   // the current string's count, staged and output offsets (batch-relative)
-    auto seek = [&]() __attribute__((always_inline)) {   // from j on: the first string with ids
-        for (; j < nsz; j++) {
-            cj = LITE_PICK(c, j);
-            if (cj) break;
-        }
-        if (j < nsz) {
-            sj = LITE_PICK(src, j);
-            dj = LITE_PICK(ex, j);
-        }
-    };
-    seek();
-    // rounds of up to RC chunks: lane u < n parks chunk u's source, destination and length; all the
-    // round's loads, then its stores (the next round's loads wait for those stores: two round trips
-    // per round of up to RC x 64 ids)
-    constexpr unsigned RC = 32;
-    int32_t *const out = f.ids + o0;
-    for (;;) {
-        unsigned n = 0;
-        uint32_t csrc = 0, cdst = 0, clim = 0;
-        while (n < RC && j < nsz) {
-            const uint32_t k = 64u * m;
-            if (lane == n) {
-                csrc = sj + k;
-                cdst = dj + k;
-                clim = cj - k < 64u ? cj - k : 64u;
-            }
-            n++;
-            m++;
-            if (64u * m >= cj) {
-                j++;
-                m = 0;
-                seek();
-            }
-        }
-        if (!n) break;
-        int32_t v[RC];
-#pragma unroll
-        for (unsigned u = 0; u < RC; u++) {
-            v[u] = 0;
-            if (u < n) {
-                const uint32_t sa = (uint32_t)__builtin_amdgcn_readlane((int)csrc, u);
-                const uint32_t lim = (uint32_t)__builtin_amdgcn_readlane((int)clim, u);
-                if (lane < lim) v[u] = (int32_t)staging[(uint64_t)sa + lane];
-            }
-        }
-#pragma unroll
-        for (unsigned u = 0; u < RC; u++) {
-            if (u < n) {
-                const uint32_t da = (uint32_t)__builtin_amdgcn_readlane((int)cdst, u);
-                const uint32_t lim = (uint32_t)__builtin_amdgcn_readlane((int)clim, u);
-                if (lane < lim) out[(uint64_t)da + lane] = v[u];
-            }
-        }
-    }
-#undef LITE_PICK
 }
 
 // dpt_encode_padded runs no finish pass: one lane resets the counter block after the tokenize passes
@@ -3294,9 +2859,6 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     a.pend = p.pend; a.ws_node = p.ws_node; a.ws_base = p.ws_base; a.ws_id = p.ws_id;
     a.long_span = p.long_span;
     a.hist_zero = nullptr; a.n_hist = 0;
-    // self-copy (the host decides: CSR calls of >= SC_MIN_BATCHES batches without edges or length-only DPs)
-    a.inc = p.self_copy ? p.inc : nullptr; a.copied = p.copied; a.cq = p.cq; a.sc_epoch = p.sc_epoch;
-    a.route_c = p.retry_count + 5;   // (counter block uint32 [5]: reset_counters zeroes it)
     a.id_off = p.id_off; a.ids = p.ids;
     a.solo = p.solo ? 1 : 0; a.ctr_snap = p.ctr_snap;
     const bool solo = p.solo && p.n_str == 1 && !p.padded;
@@ -3356,7 +2918,7 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
         EncodeArgs b = a;
         b.work_list = p.retry_list; b.work_count = p.retry_count;
         b.work_next = p.retry_count + 2;
-        if (!p.padded && !p.csr_stream && (fin_fold(p.n_str) || p.self_copy) && p.hist && p.hist_overwrite && p.hist_bins >= 2 &&
+        if (!p.padded && fin_fold(p.n_str) && p.hist && p.hist_overwrite && p.hist_bins >= 2 &&
             p.hist_bins <= FIN_MAX_BINS) {
             b.hist_zero = reinterpret_cast<unsigned long long *>(p.hist);   // (the finish pass adds to it)
             b.n_hist = p.hist_bins + 8u;
@@ -3409,33 +2971,19 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     }
     // batch prefixes (and the counter block's reset), then the CSR pass; a one-batch call (<= 256
     // strings: the drop-in's per-string calls) needs no prefix, and its finish block does the rest.
-    // Pipelined calls (dpt_ctx_pipeline): on the ctx's CSR stream, after the passes above
     hipStream_t fs = stream;
-    if (p.csr_stream) {
-        hipError_t e = hipEventRecord(p.ev_tok, stream);
-        if (e == hipSuccess) e = hipStreamWaitEvent(p.csr_stream, p.ev_tok, 0);
-        if (e != hipSuccess) return e;
-        fs = p.csr_stream;
-    }
     const uint64_t nb = (p.n_str + FIN_BATCH - 1) / FIN_BATCH;
     FinishArgs f;
     f.bsum = nullptr; f.ctr = nullptr; f.fold = nullptr; f.fold_zero = nullptr; f.fold_n = 0;
-    f.inc = p.inc; f.copied = p.copied; f.ctr_snap = p.ctr_snap;
-    const bool sc = p.self_copy;
-    const bool fold = !sc && fin_fold(p.n_str);
+    f.ctr_snap = p.ctr_snap;
+    const bool fold = fin_fold(p.n_str);
     const bool fold_hist = p.hist && p.hist_bins >= 2 && p.hist_bins <= FIN_MAX_BINS;
     f.hist = fold_hist ? reinterpret_cast<unsigned long long *>(p.hist) : nullptr;
     f.status = p.status;
     f.n_bins = p.hist_bins;
     f.hist_store = (fold_hist && p.hist_overwrite && nb <= 1) ? 1 : 0;
-    unsigned long long *hz = (fold_hist && p.hist_overwrite && nb > 1 && !fold && !sc && !p.csr_stream) ? f.hist : nullptr;
-    if (p.csr_stream && fold_hist && p.hist_overwrite && nb > 1) {
-        // pipelined: zeroed on the CSR stream, after the previous call's CSR pass (which may still be
-        // adding to the same buffer), not by this call's first passes on the other stream
-        const hipError_t e = hipMemsetAsync(f.hist, 0, ((size_t)p.hist_bins + 8u) * sizeof(unsigned long long), fs);
-        if (e != hipSuccess) return e;
-    }
-    if (fold || sc) { f.fold = p.flags; f.fold_zero = p.zero_other; f.fold_n = p.zero_n; f.ctr = p.retry_count; }
+    unsigned long long *hz = (fold_hist && p.hist_overwrite && nb > 1 && !fold) ? f.hist : nullptr;
+    if (fold) { f.fold = p.flags; f.fold_zero = p.zero_other; f.fold_n = p.zero_n; f.ctr = p.retry_count; }
     else if (nb > 1) hipLaunchKernelGGL(batch_scan_kernel, dim3(1), dim3(SCAN_THREADS), 0, fs, p.n_str, p.flags, p.bpre, p.retry_count,
                                         hz, p.hist_bins + 8u, p.ctr_snap);
     else { f.bsum = p.flags; f.ctr = p.retry_count; }
@@ -3445,13 +2993,7 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     uint64_t sls = (FIN_TARGET_BLOCKS + nb - 1) / nb;
     f.slices = (unsigned)(sls < 1 ? 1 : (sls > FIN_MAX_SLICES ? FIN_MAX_SLICES : sls));
     const uint64_t fb = nb * f.slices;
-    if (sc) {
-        if (p.staging16) hipLaunchKernelGGL((finish_kernel<int16_t, true>), dim3((unsigned)fb), dim3(FIN_THREADS), 0, fs, f);
-        else hipLaunchKernelGGL((finish_kernel<int32_t, true>), dim3((unsigned)fb), dim3(FIN_THREADS), 0, fs, f);
-    } else if (p.lite && nb > 1 && !f.hist_store && p.n_bytes < (1ull << 32)) {   // the LDS-free CSR pass (one wave per batch)
-        if (p.staging16) hipLaunchKernelGGL(finish_lite_kernel<int16_t>, dim3((unsigned)nb), dim3(64), 0, fs, f);
-        else hipLaunchKernelGGL(finish_lite_kernel<int32_t>, dim3((unsigned)nb), dim3(64), 0, fs, f);
-    } else if (p.staging16) {
+    if (p.staging16) {
         hipLaunchKernelGGL(finish_kernel<int16_t>, dim3((unsigned)fb), dim3(FIN_THREADS), 0, fs, f);
     } else {
         hipLaunchKernelGGL(finish_kernel<int32_t>, dim3((unsigned)fb), dim3(FIN_THREADS), 0, fs, f);
@@ -3462,12 +3004,10 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
             return eh;
         eh = launch_histogram(p.id_off, p.status, p.n_str, p.hist, p.hist_bins, fs);
     }
-    if (eh == hipSuccess && p.csr_stream) eh = hipEventRecord(p.ev_fin, fs);   // the set is free again after it
     return eh;
 }
 
 size_t pend_scratch_bytes(unsigned max_blocks) { return (size_t)max_blocks * 64 * sizeof(uint4); }
-size_t cq_scratch_bytes(unsigned max_blocks) { return (size_t)max_blocks * CQ_CAP * sizeof(uint4); }
 
 size_t wsl_scratch_bytes(unsigned max_blocks) {
     return (size_t)max_blocks * 4 * GroupLDS<SMALL_CH, 16>::WSL_STRIDE;   // NG x stride covers both G at CH = 256
@@ -3506,7 +3046,6 @@ hipError_t kernel_init() {
 }
 
 int small_window_bytes() { return SMALL_CH; }
-bool self_copy_built() { return SC_ON; }
 int big_window_bytes() { return BIG_CH; }
 
 #ifdef DPT_STAMPS

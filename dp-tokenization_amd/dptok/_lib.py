@@ -64,41 +64,22 @@ def lib():
     L.dpt_ctx_reserve_vocab.argtypes = [P, P, U64, U64, U64]
     L.dpt_ctx_workspace_bytes.argtypes = [P, ctypes.POINTER(U64), ctypes.POINTER(U64)]
     L.dpt_ctx_long_need.argtypes = [P, ctypes.POINTER(U64), ctypes.POINTER(U64)]
-    if os.environ.get("DPT_LIB") and not hasattr(L, "dpt_ctx_copy_stats"):
-        # an older library named for an A/B (tools/build_rev.sh): it has no self-copy to report
-        L.dpt_ctx_copy_stats = _no_copy_stats
-    else:
-        L.dpt_ctx_copy_stats.argtypes = [P, ctypes.POINTER(U64), ctypes.POINTER(U64), ctypes.POINTER(U64)]
-        L.dpt_ctx_copy_stats.restype = I32
     L.dpt_encode.argtypes = [P, P, I32, P, U64, P, P, U64, P, U64, P, P, P, P]
     L.dpt_encode_host.argtypes = [P, P, I32, P, U64, P, P, U64, P, U64, P, P, P]
     L.dpt_encode_padded.argtypes = [P, P, I32, P, U64, P, P, U64, P, U64, P, P, P, P]
     L.dpt_dp_host.argtypes = [P, P, I32, P, U64, P, P, U64, P, P, P]
     L.dpt_dp_host_far.argtypes = [P, P, I32, P, U64, P, P, U64, P, P, P, P, U64, P]
     L.dpt_token_histogram.argtypes = [P, P, U64, P, ctypes.c_uint32, P]
-    if hasattr(L, "dpt_self_copy_available"):
-        L.dpt_self_copy_available.restype = I32
-    else:   # an older library named for an A/B (DPT_LIB)
-        L.dpt_self_copy_available = lambda: 0
-    L.dpt_ctx_pipeline.argtypes = [P, P]
-    L.dpt_ctx_join.argtypes = [P, P]
     L.dpt_ctx_set_histogram.argtypes = [P, P, ctypes.c_uint32]
     L.dpt_ctx_set_histogram_ex.argtypes = [P, P, ctypes.c_uint32, I32]
     L.dpt_ctx_profile.argtypes = [P, I32]
     L.dpt_ctx_profile_read.argtypes = [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(U64)]
     for name in ("dpt_vocab_create", "dpt_vocab_destroy", "dpt_vocab_stats_get", "dpt_ctx_create", "dpt_ctx_destroy",
                  "dpt_ctx_reserve", "dpt_ctx_reserve_vocab", "dpt_ctx_workspace_bytes", "dpt_ctx_long_need", "dpt_encode", "dpt_encode_padded", "dpt_encode_host", "dpt_dp_host", "dpt_dp_host_far", "dpt_token_histogram",
-                 "dpt_ctx_set_histogram", "dpt_ctx_set_histogram_ex", "dpt_ctx_profile", "dpt_ctx_pipeline", "dpt_ctx_join",
-                 "dpt_ctx_profile_read"):
+                 "dpt_ctx_set_histogram", "dpt_ctx_set_histogram_ex", "dpt_ctx_profile", "dpt_ctx_profile_read"):
         getattr(L, name).restype = I32
     _lib = L
     return L
-
-
-def _no_copy_stats(handle, a, b, c) -> int:
-    for x in (a, b, c):
-        x._obj.value = 0
-    return DPT_OK
 
 
 def check(rc: int, what: str = "") -> None:
@@ -109,7 +90,7 @@ def check(rc: int, what: str = "") -> None:
 
 EXPORTED = ["dpt_last_error", "dpt_abi_version", "dpt_vocab_create", "dpt_vocab_destroy", "dpt_vocab_stats_get",
             "dpt_ctx_create", "dpt_ctx_destroy", "dpt_ctx_reserve", "dpt_ctx_reserve_vocab", "dpt_ctx_workspace_bytes",
-            "dpt_ctx_long_need", "dpt_ctx_copy_stats", "dpt_self_copy_available", "dpt_ctx_pipeline", "dpt_ctx_join",
+            "dpt_ctx_long_need",
             "dpt_encode", "dpt_encode_padded", "dpt_encode_host",
             "dpt_dp_host", "dpt_dp_host_far", "dpt_token_histogram", "dpt_ctx_set_histogram", "dpt_ctx_set_histogram_ex",
             "dpt_ctx_profile", "dpt_ctx_profile_read"]

@@ -421,25 +421,6 @@ class Encoder:
         check(_lib.lib().dpt_ctx_long_need(self.handle, ctypes.byref(a), ctypes.byref(b)), "dpt_ctx_long_need")
         return a.value, b.value
 
-    def copy_stats(self) -> Tuple[int, int, int]:
-        """(strings the last call's first pass copied into the CSR arrays itself, batches whose offsets
-        it wrote, the call's 256-string batches) -- all 0 when it did not self-copy; call after the
-        encode's stream has completed (dpt_ctx_copy_stats)."""
-        a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
-        check(_lib.lib().dpt_ctx_copy_stats(self.handle, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)),
-              "dpt_ctx_copy_stats")
-        return a.value, b.value, c.value
-
-    def pipeline(self, csr_stream: int) -> None:
-        """Pipelined device calls (dpt_ctx_pipeline): each later encode_device puts its CSR pass on
-        ``csr_stream`` (a stream handle, e.g. ``torch.cuda.Stream().cuda_stream``; 0 turns it off), where
-        it runs beside the next call's tokenize passes.  Outputs are complete after ``join``."""
-        check(_lib.lib().dpt_ctx_pipeline(self.handle, ctypes.c_void_p(csr_stream or None)), "dpt_ctx_pipeline")
-
-    def join(self, stream: int = 0) -> None:
-        """``stream`` waits for every CSR pass issued so far (dpt_ctx_join)."""
-        check(_lib.lib().dpt_ctx_join(self.handle, ctypes.c_void_p(stream or None)), "dpt_ctx_join")
-
     def set_histogram(self, hist_ptr: int, n_bins: int, overwrite: bool = False) -> None:
         """Fold the token-count histogram into the next encode on this engine (dpt_ctx_set_histogram_ex:
         its finish pass adds to hist, device int64[n_bins + 8], or with ``overwrite`` replaces it -- the

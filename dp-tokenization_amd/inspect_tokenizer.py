@@ -14,6 +14,8 @@
   packaged DP, e.g. ``babaaa`` -> ``['ba','baaa']`` with ``baaa`` not in V); this drop-in
   returns the well-formed shortest tokenizations of the packaged DP when its capped length
   equals the minimum, else ``[]``.  Callers use only the length (dialect_arabic.py:79-81).
+  An empty input raises ``IndexError`` like the reference (``segment_index_dp[-1]`` of ``[]``,
+  :132); lengths and exceptions are pinned by ``tests/golden/inspect_cst_cases.json.gz``.
 * ``obtain_token_compositions(token_str, vocab, merges)`` (reference :17-42): merge-tree
   decompositions, host-side recursion over the merge list (no DP).
 """
@@ -74,8 +76,8 @@ def compute_shortest_tokenizations(base_representation_s, vocabulary, disregard_
     if disregard_word_initial_marker:
         vocabulary = {token.lstrip(word_initial_marker) for token in vocabulary}
     atoms = list(base_representation_s)
-    if not atoms:
-        return [], 0
+    if not atoms:   # the reference indexes segment_index_dp[-1] of an empty list (:112, :132)
+        raise IndexError("list index out of range")
     length = _uncapped_min(atoms, vocabulary)
     if length == float("inf"):
         return [], length

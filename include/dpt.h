@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define DPT_ABI_VERSION 3
+#define DPT_ABI_VERSION 4
 
 /* return codes */
 #define DPT_OK 0
@@ -113,27 +113,6 @@ int dpt_ctx_workspace_bytes(const dpt_ctx *c, uint64_t *device_path, uint64_t *h
  * strings its unbounded pass took (*need) and the arena's capacity (*cap).  need > cap: the strings that
  * did not fit have status DPT_STATUS_TOO_LONG -- reserve long_bytes >= need and call again. */
 int dpt_ctx_long_need(dpt_ctx *c, uint64_t *need, uint64_t *cap);
-/* ABI 3.  After the ctx's last dpt_encode / dpt_encode_host has completed (synchronise its stream
- * first): the strings whose ids the first tokenize pass copied into the CSR arrays itself (*copied,
- * strings without ids included; the finish pass copies the others), the 256-string batches it
- * copied whole (*batches_whole) and the call's batches (*n_batches).  All 0 when the call did not
- * self-copy: it is opt-in (DPT_SELF_COPY=1 in the environment, read per call) in a library built with
- * it (dpt_self_copy_available), and never for calls of fewer than 8 batches, dpt_encode_padded or
- * dpt_dp_host*.  Measured slower than the finish pass's copy: an experiment, off by default. */
-int dpt_ctx_copy_stats(dpt_ctx *c, uint64_t *copied, uint64_t *batches_whole, uint64_t *n_batches);
-/* 1 when the library was built with the first pass's self-copy (csrc/Makefile `sc`), else 0. */
-int dpt_self_copy_available(void);
-/* ABI 3.  Pipelined calls: with csr_stream non-null, every later dpt_encode of the ctx runs its tokenize
- * passes on its own stream as usual but its CSR pass (batch prefixes, id_off, ids, the histogram) on
- * csr_stream, after them -- without making the call's stream wait -- and with a CSR pass that needs no
- * LDS, so it runs beside the NEXT call's tokenize passes instead of after them.  Two workspace sets
- * alternate between calls (dpt_ctx_workspace_bytes counts both once used).  A call's outputs are
- * complete once csr_stream has passed its CSR pass: dpt_ctx_join(ctx, s) makes stream s wait for every
- * CSR pass issued so far (or synchronise csr_stream).  The ctx's calls must come from one host thread,
- * in order.  csr_stream = NULL returns to ordinary calls (after a device synchronisation).  The host
- * path and dpt_encode_padded are never pipelined. */
-int dpt_ctx_pipeline(dpt_ctx *c, void *csr_stream);
-int dpt_ctx_join(dpt_ctx *c, void *stream);
 
 /*
  * Tokenize n_str strings, CSR-packed: string s is text[str_off[s]-str_off[0] .. str_off[s+1]-str_off[0]),

@@ -92,3 +92,31 @@ def test_words_of_atoms_round_trip():
     t2i = {"ab": 0, "Ġc": 1, "é": 2, "x": 3, "ĠĠ": 4, "😀z": 5, "q": 6, "a": 7, "b": 8, "Ġ": 9}
     assert ref_port.dp_tokenize_word_atoms(strings[0], t2i) == ([0, 1, 2], 0)
     assert ref_port.dp_tokenize_word_atoms(strings[2], t2i) == ([4, 5, 6], 0)
+
+
+def test_gpus_flag_against_world_size():
+    """--gpus N: run here at N = 1, launch the ranks (0) at N > 1 without torchrun, and refuse a
+    torchrun job of another size (a silently smaller job would mis-measure the scaling run)."""
+    import argparse
+    import pytest
+    ns = lambda g: argparse.Namespace(gpus=g)   # noqa: E731
+    assert bench.resolve_world(ns(None), {}) == 1
+    assert bench.resolve_world(ns(1), {}) == 1
+    assert bench.resolve_world(ns(8), {}) == 0
+    assert bench.resolve_world(ns(None), {"WORLD_SIZE": "4"}) == 4
+    assert bench.resolve_world(ns(4), {"WORLD_SIZE": "4"}) == 4
+    with pytest.raises(SystemExit) as e:
+        bench.resolve_world(ns(8), {"WORLD_SIZE": "1"})
+    assert e.value.code == 2
+    with pytest.raises(SystemExit):
+        bench.resolve_world(ns(2), {"WORLD_SIZE": "8"})
+
+
+def test_bench_refuses_world_size_mismatch_in_a_child():
+    """The refusal as a process: `WORLD_SIZE=1 python bench.py --gpus 8` exits 2 before any GPU work."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--no-cpu-baseline"],
+                         env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 2, out.stderr[-2000:]
+    assert "WORLD_SIZE" in out.stderr and out.stdout.strip() == ""

@@ -231,3 +231,54 @@ def test_dp_tokenize_bloom_key_error_outside_vocab():
         with pytest.raises(KeyError):
             dp_tokenize("lazy")
         assert dp_tokenize("") == []
+
+
+# ------------------------------------------------------------------ inspect_tokenizer.compute_shortest_tokenizations
+
+@pytest.fixture(scope="module")
+def inspect_cst():
+    return load_golden("inspect_cst_cases.json.gz")["cases"]
+
+
+def test_inspect_cst_exceptions_match_reference(inspect_cst):
+    """Every input the reference's inspect_tokenizer.compute_shortest_tokenizations (:88-146) rejects --
+    the empty one: IndexError at :132 -- the drop-in rejects with the same exception type, before any
+    device work (no GPU needed)."""
+    import inspect_tokenizer as it
+    bad = [c for c in inspect_cst if c["error"]]
+    assert len(bad) >= 3 and any(not c["atoms"] for c in bad)
+    for c in bad:
+        with pytest.raises(Exception) as e:
+            it.compute_shortest_tokenizations(list(c["atoms"]), set(c["vocab"]), c["disregard"], c["marker"])
+        assert type(e.value).__name__ == c["error"], c
+
+
+def test_inspect_cst_lengths_pinned_by_the_oracle(inspect_cst):
+    """The reference's lengths (its inf-initialised DP, :109-129) equal the CPU restatement's
+    (oracle/ref_port.min_tokens_for_string, test infrastructure) after the marker rule (:106-107) --
+    the checker the GPU test below relies on agrees with the reference on every case."""
+    from oracle import ref_port
+    good = [c for c in inspect_cst if not c["error"]]
+    assert len(good) >= 200 and sum(c["length"] == "inf" for c in good) < len(good) // 2
+    for c in good:
+        vocab = set(c["vocab"])
+        if c["disregard"]:
+            vocab = {t.lstrip(c["marker"]) for t in vocab}
+        want = math.inf if c["length"] == "inf" else c["length"]
+        assert ref_port.min_tokens_for_string(list(c["atoms"]), vocab) == want, c
+
+
+@pytest.mark.gpu
+def test_inspect_cst_lengths_match_reference(inspect_cst):
+    """The drop-in's length (GPU, uncapped DP) equals the reference's on every case; its list is the
+    packaged DP's well-formed one (documented deviation), so only its shape is checked."""
+    import inspect_tokenizer as it
+    for c in inspect_cst:
+        if c["error"]:
+            continue
+        toks, n = it.compute_shortest_tokenizations(list(c["atoms"]), set(c["vocab"]), c["disregard"], c["marker"])
+        want = math.inf if c["length"] == "inf" else c["length"]
+        assert n == want, c
+        assert all(len(t) == n for t in toks), c
+        if want == math.inf:
+            assert toks == [] == c["tokenizations"]

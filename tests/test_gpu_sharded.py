@@ -39,20 +39,43 @@ def _env(**kw):
     return env
 
 
+ARGS = ["--strings", str(N), "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
+
+
+@pytest.fixture(scope="module")
+def one_rccl_rank():
+    return _bench_line([sys.executable, "bench.py", "--gpus", "1"] + ARGS, _env(DPT_BENCH_COLL="1", MASTER_PORT="29563"))
+
+
+def _check(line, world):
+    assert line["n_gpus"] == world and line["scaling"] == "strong"
+    assert line["config"]["strings_total"] == N
+    assert line["exact_match"]["rate"] == 1.0 and line["exact_match"]["sample"] == N
+    h = line["histogram"]
+    assert h["total_strings"] == N and h["status"][0] == N   # cfg2 strings all tokenize (status 0)
+
+
 @pytest.mark.timeout(600)
-def test_cfg3_two_gloo_ranks_match_one_rccl_rank():
-    args = ["--strings", str(N), "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
+def test_cfg3_two_gloo_ranks_match_one_rccl_rank(one_rccl_rank):
     two = _bench_line([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
                        "--master-addr=127.0.0.1", "--master-port=29561", "bench.py", "--gpus", "2",
-                       "--dist-backend", "gloo"] + args, _env())
-    one = _bench_line([sys.executable, "bench.py", "--gpus", "1"] + args,
-                      _env(DPT_BENCH_COLL="1", MASTER_PORT="29563"))
-    for line, world in ((two, 2), (one, 1)):
-        assert line["n_gpus"] == world and line["scaling"] == "strong"
-        assert line["config"]["strings_total"] == N
-        assert line["exact_match"]["rate"] == 1.0 and line["exact_match"]["sample"] == N
-        h = line["histogram"]
-        assert h["total_strings"] == N and h["status"][0] == N   # cfg2 strings all tokenize (status 0)
+                       "--dist-backend", "gloo"] + ARGS, _env())
+    _check(two, 2)
+    _check(one_rccl_rank, 1)
     assert two["config"]["strings_per_gpu"] == N // 2
     # the two-rank reduced histogram is the one-rank histogram of the whole corpus
-    assert two["histogram"] == one["histogram"]
+    assert two["histogram"] == one_rccl_rank["histogram"]
+
+
+@pytest.mark.timeout(600)
+def test_bench_gpus_flag_launches_the_ranks(one_rccl_rank):
+    """`python bench.py --gpus 2` WITHOUT torchrun (the driver's scaling-run form): bench.py starts the two
+    ranks itself as a torch.distributed.run child and relays rank 0's line -- n_gpus 2, both shards
+    exact, the same reduced histogram as one rank over the whole corpus."""
+    env = _env()
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    two = _bench_line([sys.executable, "bench.py", "--gpus", "2", "--dist-backend", "gloo"] + ARGS, env)
+    _check(two, 2)
+    assert two["config"]["strings_per_gpu"] == N // 2
+    assert two["histogram"] == one_rccl_rank["histogram"]
