@@ -261,7 +261,13 @@ struct GroupLDS {
     // the window's input bytes (expanded on the fly); the dword reads of the last atoms run up to
     // 12 bytes past the end, into the next group or the slot states -- masked off, never used
     alignas(16) uint8_t bytes[CH];
+    // G = 64, 256-byte windows, non-raw modes (no expansions: a token's bytes are the window's): per byte
+    // position p <= wlen, byte[p] | BF_ATOM (an atom starts at p, or p == wlen) | BF_STOP (a word starts
+    // at p, or p == wlen) -- phase A's byte-stream walker reads ONE u16 per trie step
+    static constexpr bool BSTREAM = G == 64 && CH == 256;
+    uint16_t bf[BSTREAM ? CH + 2 : 1];
 };
+constexpr unsigned BF_ATOM = 0x100u, BF_STOP = 0x200u;
 
 // strings are < 4 GiB (dpt.h); abase: atoms of the string's earlier windows
 // (48 bytes: LDS per slot is what bounds the resident waves)
@@ -663,6 +669,8 @@ __device__ bool prep_window(GroupLDS<CH, G> &L, uint8_t *gw, const WinRegs<CH> &
             ast[u] = as; wst[u] = wsf; cpl[u] = cl;
             hi_byte |= in && (b & 0x80u) != 0;
             a_sum += as; w_sum += wsf; cp_sum += cl;
+            if constexpr (GroupLDS<CH, G>::BSTREAM)
+                if (!raw && in) L.bf[k] = (uint16_t)(b | (as ? BF_ATOM : 0u) | (wsf ? BF_STOP : 0u));
         }
         // one packed scan: atoms (9 bits) | words (9 bits) << 9 | code points (14 bits) << 18
         const unsigned v = a_sum | (w_sum << 9) | (cp_sum << 18);
@@ -704,6 +712,8 @@ __device__ bool prep_window(GroupLDS<CH, G> &L, uint8_t *gw, const WinRegs<CH> &
         cp_tot += tot >> 18;
     }
     if (lane == 0) {
+        if constexpr (GroupLDS<CH, G>::BSTREAM)
+            if (!raw) L.bf[wlen] = (uint16_t)(BF_ATOM | BF_STOP);
         L.aoff[n_atoms] = (typename GroupLDS<CH, G>::Idx)wlen;
         if constexpr (G == 16) reinterpret_cast<uint32_t *>(L.rec)[n_atoms] = 0xFFFF0000u | cp_tot | CP_WS;
         else L.rec[n_atoms].cpos = (uint16_t)(cp_tot | CP_WS);
@@ -747,12 +757,19 @@ __device__ __forceinline__ unsigned part_size(unsigned n, unsigned npart, unsign
 __device__ __forceinline__ unsigned part_string(unsigned npart, unsigned p, unsigned v) {
     return ((v / FIN_BATCH) * npart + p) * FIN_BATCH + v % FIN_BATCH;
 }
+#ifndef DPT_NEAR_CUT   // A/B knob: lane-mode B snaps chunk starts to the nearest cut point (else the next one)
+#define DPT_NEAR_CUT 1
+#endif
+constexpr bool NEAR_CUT = DPT_NEAR_CUT != 0;
 constexpr unsigned A_REFILL = 32;     // phase A: idle lanes needed before a batched refill (1/8/16/32 within 2 %)
 constexpr unsigned A_REFILL64 = 32;   // the same for the 64-lane kernels (8 / 1: neutral / -0.5 %, r03aa)
 #ifndef DPT_STOP     // diagnostic builds only (wrong results): 1 = prep only, 21 = + A0, 2 = + A, 25 / 26 / 27 =
                      // + lane-mode B's cut points / recurrence / transfer scan + fix-up, 3 = + B/C0/C1
 #define DPT_STOP 9
 #endif
+#ifndef DPT_DIAG_PREP   // diagnostic builds only (cfg2-shaped input): 1 = static claims (no counter atomics),
+#define DPT_DIAG_PREP 0  // 2 = offsets computed as 256 s (no str_off loads), 3 = both, 4 = a second dependent claim
+#endif                   // atomic, 8 = no batch-sum atomics (wrong CSR offsets) -- the refill chain's and the atomics' cost
 #ifndef DPT_C2STOP   // diagnostic builds only (wrong results): C2 stops after its bulk pass (1) / hash pass (2)
 #define DPT_C2STOP 0
 #endif
@@ -860,7 +877,8 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
     // ms, every wave queued behind ~5.6k others' atomics (profiles/r02_phase_diag.txt).  No string is
     // claimed ahead of a free slot: strings held in reserve by one wave left others idle at the end
     // of multi-window batches (cfg4 4.35 -> 4.56 ms with 4-string claims).
-    const unsigned npart = BIG ? 1u : (unsigned)min((uint64_t)NPART, max((uint64_t)1, n_work / 4096u));
+    const unsigned npart = (BIG || (DPT_DIAG_PREP & 1)) ? 1u : (unsigned)min((uint64_t)NPART, max((uint64_t)1, n_work / 4096u));
+    [[maybe_unused]] uint64_t diag_k = 0;   // DPT_DIAG_PREP & 1: the wave's claims so far
     unsigned part = BIG ? 0u : bid % npart;
     bool exhausted = false, claimed_all = false;
     unsigned n_pend = 0;   // 16-lane first pass: residual tokens waiting in the wave's pending row
@@ -871,7 +889,19 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
             uint32_t *ctr = BIG ? a.work_next : a.part_ctr + part * PART_STRIDE;
             const uint64_t hi = BIG ? n_work : part_size((unsigned)n_work, npart, part);
             unsigned b = 0;
-            if (lane == 0) b = atomicAdd(ctr, req);
+            if constexpr (!BIG && (DPT_DIAG_PREP & 1)) {   // diagnostic: wave bid's k-th claim, blocks of 4
+                b = (unsigned)((diag_k * gridDim.x + bid) * 4u);
+                diag_k++;
+            } else {
+                if (lane == 0) b = atomicAdd(ctr, req);
+                if constexpr (!BIG && (DPT_DIAG_PREP & 4)) {   // diagnostic: one more dependent atomic round trip
+                    unsigned x = 0;
+                    asm volatile("" : "+v"(b));
+                    if (lane == 0) x = atomicAdd(ctr + (b >> 31), 0u);
+                    asm volatile("" : "+v"(x));
+                    b |= (x >> 31) << 31;
+                }
+            }
             cp = __builtin_amdgcn_readfirstlane(part);
             nb = __builtin_amdgcn_readlane(b, 0);
             ne = nb < hi ? (nb + req < hi ? nb + req : hi) : nb;
@@ -962,18 +992,17 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                 // claims until every free slot has a string or every partition is used up (a claim
                 // that reaches a partition's end may return fewer strings than asked)
                 unsigned rem = need;
-                while (rem && !claimed_all) {
-                    const unsigned n_need = (unsigned)__builtin_popcount(rem);
-                    uint64_t nb = 0, ne = 0;
-                    unsigned cp = 0;
-                    claim(n_need, nb, ne, cp);
+                // partition-local strings [nb, ne) of partition cp into the free slots of rem, in order
+                auto assign = [&](uint64_t nb, uint64_t ne, unsigned cp) {
                     const unsigned got = (unsigned)(ne - nb);
                     if (lane < (unsigned)NG && ((rem >> lane) & 1u)) {
                         const unsigned k = (unsigned)__builtin_popcount(rem & ((1u << lane) - 1u));
                         if (k < got) {
                             const uint64_t idx = nb + k;
-                                                        const uint64_t s = BIG ? (uint64_t)a.work_list[idx] : part_string(npart, cp, (unsigned)idx);
-                            const uint64_t o0 = a.str_off[s], o1 = a.str_off[s + 1];
+                            const uint64_t s = BIG ? (uint64_t)a.work_list[idx] : part_string(npart, cp, (unsigned)idx);
+                            uint64_t o0, o1;
+                            if constexpr (!BIG && (DPT_DIAG_PREP & 2)) { o0 = s * 256u; o1 = o0 + 256u; }   // diagnostic (cfg2)
+                            else { o0 = a.str_off[s]; o1 = a.str_off[s + 1]; }
                             SlotState &S = SSr(lane);
                             S.s = (uint32_t)s; S.sb = o0 - base_off; S.slen = (uint32_t)(o1 - o0); S.pos = 0; S.active = 1;
                             S.status = o1 == o0 ? 2u : 0u;  // pretokenize_raw('') == [[]] -> IndexError
@@ -981,6 +1010,13 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                         }
                     }
                     for (unsigned q = 0; q < got; q++) rem &= rem - 1u;   // those slots are filled
+                };
+                while (rem && !claimed_all) {
+                    const unsigned n_need = (unsigned)__builtin_popcount(rem);
+                    uint64_t nb = 0, ne = 0;
+                    unsigned cp = 0;
+                    claim(n_need, nb, ne, cp);
+                    assign(nb, ne, cp);
                 }
                 if (claimed_all) exhausted = true;
                 wave_sync();
@@ -1342,6 +1378,89 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                     }
                 }
             }
+            // Byte-stream walker (the 64-lane 256-byte kernel, non-raw modes -- BLOOM-scale byte-level
+            // vocabularies): no expansions, so a walk from atom j consumes the window's bytes from
+            // aoff[j] on, and one u16 of bf[] per step says which byte comes next and whether an atom
+            // ends (or the word) before it.  The first two bytes go through the root table; each later
+            // step is one 8-byte trie load plus that one LDS read under it (the generic walker below reads
+            // the next atom's descriptor and bytes -- four LDS reads and the expansion logic -- per step).
+            if constexpr (GL::BSTREAM && !BIG) {
+                if (!raw && nstart[0] > 0) {
+                    const unsigned tot = nstart[0];
+                    nstart[0] = 0;   // (the generic walker gets nothing)
+                    const GL &L = grp(0);
+                    const unsigned wl = uni(SSr(0).wlen);
+                    const int32_t rb = tv.root_base;
+                    const unsigned nsl = tv.n_slots;
+                    unsigned bj = 0, bp = 0, blen = 0, bcur = 0;
+                    int32_t bnode = 0, bnb = 0;
+                    bool bisr = false, bact = false;
+                    uint64_t bmask = 0;
+                    // a start: p = aoff[j]; two bytes of the word: the root table, else one root step
+                    auto bstart = [&](unsigned jj) {
+                        bj = jj;
+                        const unsigned p = L.aoff[jj];
+                        const unsigned f1 = L.bf[p + 1u];   // p + 1 <= wlen
+                        const unsigned b0 = L.bf[p] & 0xFFu;
+                        bisr = (f1 & BF_STOP) == 0;         // the word has a second byte
+                        bcur = bisr ? (nsl + (b0 << 8) + (f1 & 0xFFu)) : (unsigned)rb + b0;
+                        bp = p;
+                        bnode = 0; bnb = rb; blen = 0; bmask = 0;
+                    };
+                    unsigned nxt2 = DPT_STOP == 21 ? tot : 0u;
+                    for (;;) {
+                        {
+                            const uint64_t im = ballot(!bact);
+                            const unsigned nidle = (unsigned)__builtin_popcountll(im);
+                            if (nxt2 < tot && (nidle >= A_REFILL64 || tot - nxt2 <= nidle)) {
+                                if (!bact) {
+                                    const unsigned uu = nxt2 + __builtin_amdgcn_mbcnt_hi((unsigned)(im >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)im, 0u));
+                                    if (uu < tot) { bact = true; bstart(uu); }
+                                }
+                                nxt2 += nidle;
+                            }
+                        }
+                        if (!ballot(bact)) break;
+                        const int2 e2 = trie_slot(tv, (int32_t)bcur);
+                        // under the load: the flags (and byte) after this step's last byte
+                        const unsigned q = bp + (bisr ? 2u : 1u);   // <= wlen
+                        const unsigned fq = L.bf[q];
+                        const unsigned fq1 = bisr ? (unsigned)L.bf[bp + 1u] : 0u;
+                        const unsigned av = bact ? 1u : 0u;
+                        const unsigned y = (unsigned)e2.y;
+                        unsigned ok;
+                        if (bisr) {
+                            // root table: .y = node after two bytes | first byte exists << 30 | it ends a token << 31
+                            const unsigned tok1 = av & (unsigned)((fq1 & BF_ATOM) != 0) & (y >> 30) & (y >> 31);
+                            bmask |= (uint64_t)tok1;
+                            blen = (fq1 & BF_ATOM) ? 1u : 0u;
+                            ok = av & (y >> 30) & (unsigned)((y & 0x3FFFFFFFu) != 0);
+                            bnode = (int32_t)(y & 0x3FFFFFFFu);
+                        } else {
+                            ok = av & (unsigned)(e2.y == bnode);
+                            bnode = (int32_t)bcur;
+                        }
+                        bnb = e2.x & BASE_MASK;
+                        const unsigned leaf = ((unsigned)e2.x >> 30) & 1u;
+                        const unsigned aend = ok & (unsigned)((fq & BF_ATOM) != 0);
+                        blen += aend;
+                        const unsigned term = aend & ((unsigned)e2.x >> 31);
+                        bmask |= term ? 1ull << (blen - 1u) : 0ull;
+                        const unsigned stop = aend & (unsigned)((fq & BF_STOP) != 0);
+                        const unsigned done = av & ((ok ^ 1u) | leaf | stop | (unsigned)(blen == (unsigned)G));
+                        bcur = (unsigned)bnb + (fq & 0xFFu);
+                        bp = q;
+                        bisr = false;
+                        if (done) {
+                            GL &Lw = grp(0);
+                            Lw.rec[bj].smask = bmask;
+                        }
+                        capm |= done & (((unsigned)bmask & 1u) ^ 1u);
+                        bact = bact && !done;
+                    }
+                    (void)wl;
+                }
+            }
             unsigned pre[NG + 1];
             pre[0] = 0;
 #pragma unroll
@@ -1620,6 +1739,20 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                 rs = min(rs, (unsigned)__builtin_amdgcn_update_dpp((int)na, (int)rs, 0x102, 0xF, 0xF, false));
                 rs = min(rs, (unsigned)__builtin_amdgcn_update_dpp((int)na, (int)rs, 0x104, 0xF, 0xF, false));
                 rs = min(rs, (unsigned)__builtin_amdgcn_update_dpp((int)na, (int)rs, 0x108, 0xF, 0xF, false));
+                if constexpr (NEAR_CUT) {
+                    // the NEAREST cut to c0 instead of the first one after it: snapping up made the longest
+                    // chunk of a wave ~2x the mean on cfg4's long words (a 256-atom window: 36.7 ends
+                    // against C = 17), and the wave steps as long as its longest chunk; nearest-cut
+                    // rounding is monotone in c0, so the chunks still tile (0, na]
+                    const unsigned lastc = cut ? c0 + (31u - (unsigned)__builtin_clz(cut)) : 0u;   // (0 is a cut)
+                    unsigned pm = lastc;   // max over the lanes <= d of the row, then shifted: lanes < d
+                    pm = max(pm, (unsigned)__builtin_amdgcn_update_dpp(0, (int)pm, 0x111, 0xF, 0xF, false));   // row_shr:1
+                    pm = max(pm, (unsigned)__builtin_amdgcn_update_dpp(0, (int)pm, 0x112, 0xF, 0xF, false));   // row_shr:2
+                    pm = max(pm, (unsigned)__builtin_amdgcn_update_dpp(0, (int)pm, 0x114, 0xF, 0xF, false));   // row_shr:4
+                    pm = max(pm, (unsigned)__builtin_amdgcn_update_dpp(0, (int)pm, 0x118, 0xF, 0xF, false));   // row_shr:8
+                    const unsigned prevc = (unsigned)__builtin_amdgcn_update_dpp(0, (int)pm, 0x111, 0xF, 0xF, false);
+                    rs = (c0 - prevc < rs - c0) ? prevc : rs;
+                }
                 const unsigned re = (unsigned)__builtin_amdgcn_update_dpp((int)na, (int)rs, 0x101, 0xF, 0xF, false);
                 if (DPT_STOP == 25) return;   // diagnostic: cut points only
 
@@ -2058,7 +2191,6 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
         }
         wave_sync();
         STAMP(3);
-
         // ---------------------------------------------------------- C2: ids (lanes over all slots' tokens)
         KREFRESH();
         if (DPT_RUN_C2) {
@@ -2438,7 +2570,8 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                     a.status[s] = (int32_t)S.status;
                     if (a.capped) a.capped[s] = S.status == 3 ? -1 : (int32_t)S.capsum;
                     S.active = 0;
-                    if (a.bsum && cnt) atomicAdd(a.bsum + (s / FIN_BATCH) * BS_LINE, cnt);
+                    if (!(DPT_DIAG_PREP & 8))
+                        if (a.bsum && cnt) atomicAdd(a.bsum + (s / FIN_BATCH) * BS_LINE, cnt);
                     a.counts[s] = cnt;
                 }
             }

@@ -7,6 +7,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "dp-tokenization_amd"), os.path.join(RO
 from oracle import ref_port
 
 FRESH = 31
+NEAR_CUT = True   # mirrors dpt_kernels.hip DPT_NEAR_CUT
 
 def relax(sj, span):
     a1 = sj + 64
@@ -58,8 +59,15 @@ def model(text, vocab, verbose=False):
         c0 = lanes[d]["c0"]; lcut = lanes[d]["lcut"]
         cut = 0 if S < c0 else (lcut if S - c0 >= 16 else lcut & ((2 << (S - c0)) - 1))
         lanes[d]["fc"] = c0 + ((cut & -cut).bit_length() - 1) if cut else na
+        lanes[d]["lc"] = c0 + cut.bit_length() - 1 if cut else 0   # the lane's last cut
     for d in range(16):
         lanes[d]["rs"] = min([l["fc"] for l in lanes[d:]])
+    if NEAR_CUT:   # the kernel's DPT_NEAR_CUT: the nearest cut to c0 (ties: the later one)
+        for d in range(16):
+            c0 = lanes[d]["c0"]
+            prev = max([l["lc"] for l in lanes[:d]] + [0])
+            if c0 - prev < lanes[d]["rs"] - c0:
+                lanes[d]["rs"] = prev
     for d in range(16):
         lanes[d]["re"] = lanes[d + 1]["rs"] if d < 15 else na
     # B loop
