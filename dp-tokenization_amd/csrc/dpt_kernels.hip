@@ -266,6 +266,8 @@ struct GroupLDS {
     // at p, or p == wlen) -- phase A's byte-stream walker reads ONE u16 per trie step
     static constexpr bool BSTREAM = G == 64 && CH == 256;
     uint16_t bf[BSTREAM ? CH + 2 : 1];
+    // ... and per atom: 1 = it starts a word that is one vocabulary token (the whole-word shortcut)
+    uint8_t scf[BSTREAM ? CH + 2 : 1];
 };
 constexpr unsigned BF_ATOM = 0x100u, BF_STOP = 0x200u;
 
@@ -550,6 +552,7 @@ __device__ __forceinline__ bool token_hash_long(const uint8_t *bytes, unsigned p
 
 // ------------------------------------------------------------------ prep: one slot's window
 
+
 // The bytes (and cut-mask bytes) of a window, in registers: lane l holds bytes
 // [256c + 4l, 256c + 4l + 4) of chunk c, little-endian; *_end is the byte at CH (the probe
 // for the last word start when the string continues past the window).
@@ -761,6 +764,8 @@ __device__ __forceinline__ unsigned part_string(unsigned npart, unsigned p, unsi
 #define DPT_NEAR_CUT 1
 #endif
 constexpr bool NEAR_CUT = DPT_NEAR_CUT != 0;
+// (the 64-lane push recurrence keeps the next cut: nearest measured 0.9 % slower on BLOOM, r05e)
+constexpr bool NEAR_CUT64 = false;
 constexpr unsigned A_REFILL = 32;     // phase A: idle lanes needed before a batched refill (1/8/16/32 within 2 %)
 constexpr unsigned A_REFILL64 = 32;   // the same for the 64-lane kernels (8 / 1: neutral / -0.5 %, r03aa)
 #ifndef DPT_STOP     // diagnostic builds only (wrong results): 1 = prep only, 21 = + A0, 2 = + A, 25 / 26 / 27 =
@@ -1384,81 +1389,92 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
             // ends (or the word) before it.  The first two bytes go through the root table; each later
             // step is one 8-byte trie load plus that one LDS read under it (the generic walker below reads
             // the next atom's descriptor and bytes -- four LDS reads and the expansion logic -- per step).
+            // Whole-word shortcut (not when edges are an output): a word that is ONE vocabulary token has
+            // cost 1 and that token as its only shortest tokenization (every other split costs >= 2:
+            // dp_tokenize.py:24-47 then selects it); the walk from its first atom reaching the word's end
+            // on a token marks it (scf[]) and B pushes only that edge (forward_lanes64).  (Walking the word
+            // starts first, to skip the other atoms of such words, left the 64 lanes idle behind the
+            // longest walks: BLOOM 4.90 -> 5.45 ms, r05f.)
             if constexpr (GL::BSTREAM && !BIG) {
                 if (!raw && nstart[0] > 0) {
-                    const unsigned tot = nstart[0];
+                    const unsigned na_ = nstart[0];
                     nstart[0] = 0;   // (the generic walker gets nothing)
-                    const GL &L = grp(0);
-                    const unsigned wl = uni(SSr(0).wlen);
+                    GL &L = grp(0);
+                    const bool wsc = a.edges == nullptr;
                     const int32_t rb = tv.root_base;
                     const unsigned nsl = tv.n_slots;
-                    unsigned bj = 0, bp = 0, blen = 0, bcur = 0;
-                    int32_t bnode = 0, bnb = 0;
-                    bool bisr = false, bact = false;
-                    uint64_t bmask = 0;
-                    // a start: p = aoff[j]; two bytes of the word: the root table, else one root step
-                    auto bstart = [&](unsigned jj) {
-                        bj = jj;
-                        const unsigned p = L.aoff[jj];
-                        const unsigned f1 = L.bf[p + 1u];   // p + 1 <= wlen
-                        const unsigned b0 = L.bf[p] & 0xFFu;
-                        bisr = (f1 & BF_STOP) == 0;         // the word has a second byte
-                        bcur = bisr ? (nsl + (b0 << 8) + (f1 & 0xFFu)) : (unsigned)rb + b0;
-                        bp = p;
-                        bnode = 0; bnb = rb; blen = 0; bmask = 0;
-                    };
-                    unsigned nxt2 = DPT_STOP == 21 ? tot : 0u;
-                    for (;;) {
-                        {
-                            const uint64_t im = ballot(!bact);
-                            const unsigned nidle = (unsigned)__builtin_popcountll(im);
-                            if (nxt2 < tot && (nidle >= A_REFILL64 || tot - nxt2 <= nidle)) {
-                                if (!bact) {
-                                    const unsigned uu = nxt2 + __builtin_amdgcn_mbcnt_hi((unsigned)(im >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)im, 0u));
-                                    if (uu < tot) { bact = true; bstart(uu); }
+                    for (unsigned jj = lane; jj < na_; jj += 64u) L.scf[jj] = 0;
+                    {
+                        const unsigned tot = na_;
+                        unsigned bj = 0, bp = 0, blen = 0, bcur = 0;
+                        int32_t bnode = 0, bnb = 0;
+                        bool bisr = false, bact = false, bws = false;
+                        uint64_t bmask = 0;
+                        // a start: p = aoff[j]; two bytes of the word: the root table, else one root step
+                        auto bstart = [&](unsigned jj) {
+                            bj = jj;
+                            const unsigned p = L.aoff[jj];
+                            const unsigned f1 = L.bf[p + 1u];   // p + 1 <= wlen
+                            const unsigned f0 = L.bf[p];
+                            const unsigned b0 = f0 & 0xFFu;
+                            bws = wsc && (f0 & BF_STOP) != 0;   // a word's first atom
+                            bisr = (f1 & BF_STOP) == 0;         // the word has a second byte
+                            bcur = bisr ? (nsl + (b0 << 8) + (f1 & 0xFFu)) : (unsigned)rb + b0;
+                            bp = p;
+                            bnode = 0; bnb = rb; blen = 0; bmask = 0;
+                        };
+                        unsigned nxt2 = DPT_STOP == 21 ? tot : 0u;
+                        for (;;) {
+                            {
+                                const uint64_t im = ballot(!bact);
+                                const unsigned nidle = (unsigned)__builtin_popcountll(im);
+                                if (nxt2 < tot && (nidle >= A_REFILL64 || tot - nxt2 <= nidle)) {
+                                    if (!bact) {
+                                        const unsigned uu = nxt2 + __builtin_amdgcn_mbcnt_hi((unsigned)(im >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)im, 0u));
+                                        if (uu < tot) { bact = true; bstart(uu); }
+                                    }
+                                    nxt2 += nidle;
                                 }
-                                nxt2 += nidle;
                             }
+                            if (!ballot(bact)) break;
+                            const int2 e2 = trie_slot(tv, (int32_t)bcur);
+                            // under the load: the flags (and byte) after this step's last byte
+                            const unsigned q = bp + (bisr ? 2u : 1u);   // <= wlen
+                            const unsigned fq = L.bf[q];
+                            const unsigned fq1 = bisr ? (unsigned)L.bf[bp + 1u] : 0u;
+                            const unsigned av = bact ? 1u : 0u;
+                            const unsigned y = (unsigned)e2.y;
+                            unsigned ok;
+                            if (bisr) {
+                                // root table: .y = node after two bytes | first byte exists << 30 | it ends a token << 31
+                                const unsigned tok1 = av & (unsigned)((fq1 & BF_ATOM) != 0) & (y >> 30) & (y >> 31);
+                                bmask |= (uint64_t)tok1;
+                                blen = (fq1 & BF_ATOM) ? 1u : 0u;
+                                ok = av & (y >> 30) & (unsigned)((y & 0x3FFFFFFFu) != 0);
+                                bnode = (int32_t)(y & 0x3FFFFFFFu);
+                            } else {
+                                ok = av & (unsigned)(e2.y == bnode);
+                                bnode = (int32_t)bcur;
+                            }
+                            bnb = e2.x & BASE_MASK;
+                            const unsigned leaf = ((unsigned)e2.x >> 30) & 1u;
+                            const unsigned aend = ok & (unsigned)((fq & BF_ATOM) != 0);
+                            blen += aend;
+                            const unsigned term = aend & ((unsigned)e2.x >> 31);
+                            bmask |= term ? 1ull << (blen - 1u) : 0ull;
+                            const unsigned stop = aend & (unsigned)((fq & BF_STOP) != 0);
+                            const unsigned done = av & ((ok ^ 1u) | leaf | stop | (unsigned)(blen == (unsigned)G));
+                            bcur = (unsigned)bnb + (fq & 0xFFu);
+                            bp = q;
+                            bisr = false;
+                            if (done) {
+                                L.rec[bj].smask = bmask;
+                                if (bws && (stop & term)) L.scf[bj] = 1;   // the word is one token
+                            }
+                            capm |= done & (((unsigned)bmask & 1u) ^ 1u);
+                            bact = bact && !done;
                         }
-                        if (!ballot(bact)) break;
-                        const int2 e2 = trie_slot(tv, (int32_t)bcur);
-                        // under the load: the flags (and byte) after this step's last byte
-                        const unsigned q = bp + (bisr ? 2u : 1u);   // <= wlen
-                        const unsigned fq = L.bf[q];
-                        const unsigned fq1 = bisr ? (unsigned)L.bf[bp + 1u] : 0u;
-                        const unsigned av = bact ? 1u : 0u;
-                        const unsigned y = (unsigned)e2.y;
-                        unsigned ok;
-                        if (bisr) {
-                            // root table: .y = node after two bytes | first byte exists << 30 | it ends a token << 31
-                            const unsigned tok1 = av & (unsigned)((fq1 & BF_ATOM) != 0) & (y >> 30) & (y >> 31);
-                            bmask |= (uint64_t)tok1;
-                            blen = (fq1 & BF_ATOM) ? 1u : 0u;
-                            ok = av & (y >> 30) & (unsigned)((y & 0x3FFFFFFFu) != 0);
-                            bnode = (int32_t)(y & 0x3FFFFFFFu);
-                        } else {
-                            ok = av & (unsigned)(e2.y == bnode);
-                            bnode = (int32_t)bcur;
-                        }
-                        bnb = e2.x & BASE_MASK;
-                        const unsigned leaf = ((unsigned)e2.x >> 30) & 1u;
-                        const unsigned aend = ok & (unsigned)((fq & BF_ATOM) != 0);
-                        blen += aend;
-                        const unsigned term = aend & ((unsigned)e2.x >> 31);
-                        bmask |= term ? 1ull << (blen - 1u) : 0ull;
-                        const unsigned stop = aend & (unsigned)((fq & BF_STOP) != 0);
-                        const unsigned done = av & ((ok ^ 1u) | leaf | stop | (unsigned)(blen == (unsigned)G));
-                        bcur = (unsigned)bnb + (fq & 0xFFu);
-                        bp = q;
-                        bisr = false;
-                        if (done) {
-                            GL &Lw = grp(0);
-                            Lw.rec[bj].smask = bmask;
-                        }
-                        capm |= done & (((unsigned)bmask & 1u) ^ 1u);
-                        bact = bact && !done;
                     }
-                    (void)wl;
                 }
             }
             unsigned pre[NG + 1];
@@ -1967,9 +1983,32 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                     }
                     return res;
                 };
+                // the last cut at or before c (0 is a cut)
+                auto prevcut = [&](unsigned c) -> unsigned {
+                    unsigned res = 0;
+#pragma unroll
+                    for (int r = 0; r < (CH + 64) / 64; r++) {
+                        const unsigned lo = 64u * (unsigned)r;
+                        const uint64_t keep = c < lo ? 0ull : (c >= lo + 63u ? ~0ull : (~0ull >> (63u - (c - lo))));
+                        const uint64_t m = cm[r] & keep;
+                        res = m ? lo + 63u - (unsigned)__builtin_clzll(m) : res;
+                    }
+                    return res;
+                };
+                // chunk bounds snapped to the NEAREST cut (as forward_lanes, DPT_NEAR_CUT): monotone in c, so
+                // lane l's end is lane l+1's start
+                auto snap = [&](unsigned c) -> unsigned {
+                    const unsigned nx = nextcut(c);
+                    if constexpr (!NEAR_CUT64) return nx;
+                    const unsigned pv = prevcut(c);
+                    return (c - pv < nx - c) ? pv : nx;
+                };
                 const unsigned C = (na + 63u) >> 6;   // (odd chunk lengths: -0.5 %, r03ad)
                 const unsigned c0 = min(lane * C, na), c1 = min(c0 + C, na);
-                const unsigned rs = nextcut(c0), re = nextcut(c1);
+                const unsigned rs = snap(c0);
+                // (c1 = the next lane's c0: its start, by wave_shl:1; lane 63 ends at na)
+                const unsigned re = (unsigned)__builtin_amdgcn_update_dpp((int)na, (int)rs, 0x130, 0xF, 0xF, false);
+                (void)c1;
                 if (DPT_STOP == 25) return;   // diagnostic: cut points only
                 // ---- the chunk's entries: no candidate yet, cp(i) in the high half; pe = its first word end
                 unsigned pe = 0;
@@ -1997,6 +2036,18 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                         f.x = (kk <= f.y) ? ((f.x & ~0x7Fu) | dd) : f.x;                            // dg
                         f.y = kk < f.y ? kk : f.y;
                     };
+                    if (!raw && L.scf[j]) {
+                        // a word that is one token (phase A's whole-word shortcut): only that edge, whose key
+                        // (cost 1) is final at the word end; its inner positions are never read (C0/C1 read
+                        // word ends, C1 walks from them; no cut lies inside the word)
+                        const unsigned dd = 63u - (unsigned)__builtin_clzll(sm);   // the longest token from j
+                        uint2 f = fin2[j + 1u + dd];
+                        upd(f, dd);
+                        fin2[j + 1u + dd] = f;
+                        kcarry = f.y;
+                        j += dd;
+                        continue;
+                    }
                     {   // the j -> j+1 edge (bit 0): j+1's final key
                         uint2 f = fin2[j + 1u];
                         upd(f, 0u);

@@ -8,6 +8,7 @@ from oracle import ref_port
 
 FRESH = 31
 NEAR_CUT = True   # mirrors dpt_kernels.hip DPT_NEAR_CUT
+NEAR_CUT64 = False   # ... and NEAR_CUT64 (the 64-lane push recurrence)
 
 def relax(sj, span):
     a1 = sj + 64
@@ -202,12 +203,20 @@ def model64(text, vocab, verbose=False):
         if p < na:
             run = max(run, p + sm[p].bit_length())
     nextcut = lambda c: next(p for p in range(c, na + 1) if cut[p])
+    prevcut = lambda c: max(p for p in range(0, min(c, na) + 1) if cut[p])
+
+    def snap(c):   # the kernel's nearest-cut rule (DPT_NEAR_CUT), else the next cut
+        nx = nextcut(c)
+        if not NEAR_CUT64:
+            return nx
+        pv = prevcut(c)
+        return pv if c - pv < nx - c else nx
     C = (na + 63) >> 6
     fx = [0] * (na + 2); fy = [0] * (na + 2)
     lanes = []
     for d in range(64):
         c0 = min(d * C, na); c1 = min(c0 + C, na)
-        rs, re = nextcut(c0), nextcut(c1)
+        rs, re = snap(c0), snap(c1)
         pe = 0
         for i in range(rs + 1, re + 1):
             fx[i] = cpos[i] << 16; fy[i] = 0xFFFFFFFF

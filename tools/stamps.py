@@ -38,7 +38,7 @@ for _ in range(reps):
 dt = (time.time() - t0) / reps
 lib.dpt_debug_stamps(buf, 0)
 names = ["prep", "A_match", "B_forward", "C0/C1_select", "finish", "C2_bulk", "C2_hash", "C2_pend+walk",
-         "sc_queue+step", "sc_drain"]
+         "(unused)", "tail"]
 tot = sum(buf[k] for k in range(10))
 print(f"{gen} n={n} wall={dt*1e3:.1f} ms (host path incl. copies)")
 for k in (0, 1, 2, 3, 5, 6, 7, 4, 8, 9):
