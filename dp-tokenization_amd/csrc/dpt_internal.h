@@ -71,11 +71,7 @@ constexpr unsigned NPART_MAX = 32;
 constexpr unsigned PAIR16_N = 65536 + 256;
 // strings per finish batch (the batch arrays are sized one per 64 strings, two arrays)
 constexpr unsigned FIN_BATCH = 256;
-#ifndef PART_STRIDE_DEF   // A/B knob (the counter block is sized for strides up to PART_STRIDE_MAX)
-#define PART_STRIDE_DEF 64
-#endif
-constexpr unsigned PART_STRIDE = PART_STRIDE_DEF, PART_STRIDE_MAX = 1024;
-static_assert(PART_STRIDE <= PART_STRIDE_MAX, "PART_STRIDE");
+constexpr unsigned PART_STRIDE = 64;   // (counters 4 KB apart measured the same, r05i)
 // Calls of 2..FIN_FOLD_MAX batches run no batch_scan_kernel: each finish block sums the batch sums
 // before its own batch (<= FIN_FOLD_MAX / FIN_THREADS loads per thread), zeroes the OTHER array for
 // the next call (the two arrays swap roles: dpt_ctx's flag parity) and block 0 resets the counter
@@ -96,7 +92,7 @@ constexpr unsigned FIN_MAX_BINS = 1024;   // histogram bins the finish pass fold
 // strings, profiles/r04d_ab.log).  u64 [0]: the count sum -- one atomic add per finished string.
 constexpr unsigned BS_LINE = 16;
 constexpr size_t PART_CTR_OFFSET = 256;
-constexpr size_t CTR_ALLOC_BYTES = PART_CTR_OFFSET + (NPART_MAX + 1) * PART_STRIDE_MAX * 4;
+constexpr size_t CTR_ALLOC_BYTES = PART_CTR_OFFSET + (NPART_MAX + 1) * PART_STRIDE * 4;
 
 // child filter bit of next byte b (slots4[].w, host and device): XOR with b >> 5 permutes the
 // low five bits inside each 32-byte block, so the 26 lowercase letters get distinct bits

@@ -1394,7 +1394,8 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
             // dp_tokenize.py:24-47 then selects it); the walk from its first atom reaching the word's end
             // on a token marks it (scf[]) and B pushes only that edge (forward_lanes64).  (Walking the word
             // starts first, to skip the other atoms of such words, left the 64 lanes idle behind the
-            // longest walks: BLOOM 4.90 -> 5.45 ms, r05f.)
+            // longest walks: BLOOM 4.90 -> 5.45 ms, r05f; and so did one pass over a word-starts-first list that
+            // skips the starts inside words already known to be one token: +2 %, r05k.)
             if constexpr (GL::BSTREAM && !BIG) {
                 if (!raw && nstart[0] > 0) {
                     const unsigned na_ = nstart[0];
