@@ -5,9 +5,11 @@ Usage: python tools/phase_table.py <log> [workload-suffix]"""
 import re
 import sys
 
-names = {"var_stop1": "prep", "var_stop21": "+A0", "var_stop2": "+A walkers", "var_stop3": "+B, C0/C1",
+names = {"var_stop1": "prep", "var_stop21": "+A0", "var_stop2": "+A walkers", "var_stop25": "+B cut points",
+         "var_stop26": "+B chunk recurrence", "var_stop27": "+B transfer + fix-up", "var_stop3": "+C1 (lane walks)",
          "var_c2s1": "+C2 bulk", "var_c2s2": "+C2 hash", "dptok": "+C2 rest (full kernel)"}
-order = ["var_stop1", "var_stop21", "var_stop2", "var_stop3", "var_c2s1", "var_c2s2", "dptok"]
+order = ["var_stop1", "var_stop21", "var_stop2", "var_stop25", "var_stop26", "var_stop27", "var_stop3", "var_c2s1", "var_c2s2",
+         "dptok"]
 suffix = sys.argv[2] if len(sys.argv) > 2 else None
 rows, cur, kern = {}, None, False
 for line in open(sys.argv[1]):
@@ -16,7 +18,9 @@ for line in open(sys.argv[1]):
         tag = m.group(1)
         base, _, wl = tag.rpartition("_")
         cur = None
-        if suffix is None or wl == suffix:
+        if suffix is None:   # (gpu_phase_wl.sh logs: the tag is the build's directory)
+            cur = rows.setdefault(tag, {})
+        elif wl == suffix:
             cur = rows.setdefault(base, {})
         kern = False
         continue
