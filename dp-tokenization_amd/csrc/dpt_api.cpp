@@ -367,6 +367,8 @@ int dpt_vocab_create(const uint8_t *utf8_blob, const uint64_t *tok_off, const in
                                             e2 ? filt[s2] : 0u);
         }
         pair16[65536 + b0] = (int16_t)(e1 ? da.id[s1] : -1);
+        // a raw '\n' after b0 is "<0x0A>": A0 looks (b0, '\n') up as it reads and finds (b0, '<')'s entry
+        a0[(b0 << 8) + '\n'] = a0[(b0 << 8) + '<'];
     }
     e = hipMalloc((void **)&v->d_slots, sizeof(int2) * slots.size());
     if (e == hipSuccess) e = hipMalloc((void **)&v->d_slots4, sizeof(int4) * slots4.size());

@@ -766,6 +766,10 @@ __device__ __forceinline__ unsigned part_string(unsigned npart, unsigned p, unsi
 constexpr bool NEAR_CUT = DPT_NEAR_CUT != 0;
 // (the 64-lane push recurrence keeps the next cut: nearest measured 0.9 % slower on BLOOM, r05e)
 constexpr bool NEAR_CUT64 = false;
+#ifndef DPT_A0_SWAR     // A/B knob: phase A0's per-byte flags four bytes per VALU op (bit 7 of each byte)
+#define DPT_A0_SWAR 1
+#endif
+constexpr bool A0_SWAR = DPT_A0_SWAR != 0;
 constexpr unsigned A_REFILL = 32;     // phase A: idle lanes needed before a batched refill (1/8/16/32 within 2 %)
 constexpr unsigned A_REFILL64 = 32;   // the same for the 64-lane kernels (8 / 1: neutral / -0.5 %, r03aa)
 #ifndef DPT_STOP     // diagnostic builds only (wrong results): 1 = prep only, 21 = + A0, 2 = + A, 25 / 26 / 27 =
@@ -1172,6 +1176,77 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                         const unsigned gbase = (unsigned)g * GSTR;
                         const uint32_t *b32 = reinterpret_cast<const uint32_t *>(grp(g).bytes);
                         const unsigned k0 = 4u * lane;
+                        if constexpr (A0_SWAR) {
+                            // The lane's four bytes as one 32-bit word (SWAR): every per-byte flag is bit 7 of
+                            // its byte, so one VALU op tests four bytes.  Views: w0 = bytes k0..k0+3 (b), n1w =
+                            // k0+1.. (the next byte), n2w = k0+2.. (the one after).
+                            constexpr uint32_t H = 0x80808080u;
+                            const uint32_t w0 = b32[lane], w1 = b32[lane + 1u];
+                            const uint32_t n1w = __builtin_amdgcn_alignbyte(w1, w0, 1u);
+                            const uint32_t n2w = __builtin_amdgcn_alignbyte(w1, w0, 2u);
+                            // lookups at (b, n1) as read: the table holds (b, '<')'s entry at (b, '\n') too,
+                            // and (b, END)'s flags of b are (b, anything)'s (dpt_api.cpp)
+                            uint2 ent[4];
+#pragma unroll
+                            for (int u = 0; u < 4; u++)
+                                ent[u] = reinterpret_cast<const uint2 *>(tv.pair16 + PAIR16_N)[
+                                    __builtin_amdgcn_perm(w0, n1w, 0x0C0C0000u | ((4u + (unsigned)u) << 8) | (unsigned)u)];
+                            // bytes past the window (END): byte q of the 8 is valid while q < nv
+                            const unsigned nv = wl > k0 ? min(wl - k0, 8u) : 0u;
+                            const uint64_t vm = nv >= 8u ? ~0ull : ((1ull << (8u * nv)) - 1ull);
+                            const uint32_t vlo = (uint32_t)vm, vhi = (uint32_t)(vm >> 32);
+                            const uint32_t v0 = vlo & H, v1 = __builtin_amdgcn_alignbyte(vhi, vlo, 1u) & H,
+                                           v2 = __builtin_amdgcn_alignbyte(vhi, vlo, 2u) & H;
+                            auto eq80 = [](uint32_t x, uint32_t c) -> uint32_t {   // bit 7 of each byte of x equal to c's
+                                const uint32_t t = x ^ c;
+                                return ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
+                            };
+                            const uint32_t sp0 = eq80(w0, 0x20202020u), sp1w = eq80(w1, 0x20202020u);
+                            const uint32_t nl0 = eq80(w0, 0x0A0A0A0Au), nl1w = eq80(w1, 0x0A0A0A0Au);
+                            const uint32_t sp1 = __builtin_amdgcn_alignbyte(sp1w, sp0, 1u), sp2 = __builtin_amdgcn_alignbyte(sp1w, sp0, 2u);
+                            const uint32_t nl1 = __builtin_amdgcn_alignbyte(nl1w, nl0, 1u), nl2 = __builtin_amdgcn_alignbyte(nl1w, nl0, 2u);
+                            const uint32_t special = sp0 | nl0 | ((first && lane == 0) ? 0x80u : 0u);   // the walker's
+                            const uint32_t norm = v0 & ~special;
+                            const uint32_t cont = v1 & ~sp1;   // n1 is in the word
+                            // the entries' flag bytes side by side (bit 0 root child, 1 b a token, 2 node b n1,
+                            // 3 it ends a token, 4 it is a leaf) and their child-filter bits for n2
+                            const uint32_t xs = __builtin_amdgcn_perm(ent[1].x, ent[0].x, 0x0C0C0400u) |
+                                                (__builtin_amdgcn_perm(ent[3].x, ent[2].x, 0x0C0C0400u) << 16);
+                            const uint32_t cb = n2w ^ ((n2w >> 5) & 0x07070707u);   // child_bit(byte) in each byte's low 5 bits
+                            const uint32_t f0 = ent[0].y >> (cb & 31u), f1 = ent[1].y >> ((cb >> 8) & 31u),
+                                           f2 = ent[2].y >> ((cb >> 16) & 31u), f3 = ent[3].y >> ((cb >> 24) & 31u);
+                            const uint32_t fb = (__builtin_amdgcn_perm(f1, f0, 0x0C0C0400u) |
+                                                 (__builtin_amdgcn_perm(f3, f2, 0x0C0C0400u) << 16)) << 7;
+                            const uint32_t tok1 = (xs << 7) & (xs << 6);
+                            const uint32_t has2 = norm & cont & (xs << 5);
+                            // go on past two bytes: n2 in the word with a child for it; '\n' at n1 or n2 ("<0x0A>")
+                            // always (the walker redoes such starts whole)
+                            const uint32_t more = has2 & ~(xs << 3) & (nl1 | (v2 & (nl2 | (~sp2 & fb))));
+                            const uint32_t tk1 = norm & tok1;                  // a one-atom token ends at k0+1+u
+                            const uint32_t tk2 = has2 & ~nl1 & (xs << 4);      // a two-atom token ends at k0+2+u
+                            const uint32_t mk = ((v0 & special) | more) & H;   // walker starts
+                            const uint32_t t2e = (tk2 << 8) | wave_shift_in(tk2 >> 24, 0u);
+                            // end k0+1+u: bit 0 of byte u of d a one-atom token, bit 1 a two-atom one
+                            const uint32_t d = ((tk1 & H) >> 7) | ((t2e & H) >> 6);
+                            uint32_t *r32 = reinterpret_cast<uint32_t *>(smem + gbase);
+                            if (ballot(d != 0)) {
+#pragma unroll
+                                for (int u = 0; u < 4; u++)
+                                    __hip_atomic_fetch_and(&r32[k0 + 1u + u], ~(((d >> (8 * u)) & 3u) << 16),
+                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            }
+                            if (ballot((norm & ~tok1) != 0) && lane == 0) SSr(g).capb = 1;
+                            // the slot's marked atoms, in order, into its fin[] (free until phase B)
+                            const unsigned c = (unsigned)__builtin_popcount(mk);
+                            const unsigned incl = wave_incl_scan_add(c);
+                            unsigned o = incl - c;
+                            GL &Lg = grp(g);
+#pragma unroll
+                            for (int u = 0; u < 4; u++)
+                                if ((mk >> (8 * u + 7)) & 1u) Lg.fin[o++].v = (uint8_t)(k0 + (unsigned)u);
+                            nstart[g] = __builtin_amdgcn_readlane(incl, 63);
+                            continue;
+                        }
                         // bytes k0 .. k0+7 (past the window: masked by wl below)
                         const uint64_t w = (uint64_t)b32[lane] | ((uint64_t)b32[lane + 1u] << 32);
                         auto byte_at = [&](unsigned q) -> unsigned {   // byte k0+q, END past the window
