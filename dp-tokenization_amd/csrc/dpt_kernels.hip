@@ -788,7 +788,10 @@ constexpr unsigned A_REFILL64 = 32;   // the same for the 64-lane kernels (8 / 1
 // Waves per SIMD by VGPRs (<= 80 VGPRs each).  The 256-byte 16-lane rows: LDS (22 waves per CU) then
 // binds (96 VGPRs / 5 waves: no scratch spills, cfg2 -1.9 %, r03e).  The 256-byte 64-lane kernel: BLOOM
 // 17.4 -> 19.8 GB/s against no cap (95 VGPRs, 20 waves; 7 or 8 waves spill more: r03aa, r03ac).
-constexpr int WPE16 = 6;
+#ifndef DPT_WPE16
+#define DPT_WPE16 6
+#endif
+constexpr int WPE16 = DPT_WPE16;
 constexpr int WPE64 = 6;
 // The kernel's arguments, as one struct at the start of the kernarg segment
 struct KernArgs {
