@@ -2737,6 +2737,11 @@ tokenize_kernel(KernArgs ka) {
 
 constexpr unsigned FIN_U = 8;                 // loads in flight per thread of the copy (8 / 12 beat 4, 16 and 32: r04n)
 constexpr unsigned FIN_THREADS = 512;         // threads per finish block (>= FIN_BATCH): all of them copy
+#ifndef DPT_FIN_MAP     // A/B knob: the finish copy finds each element's string from a per-row map
+#define DPT_FIN_MAP 1
+#endif
+constexpr bool FIN_MAP = DPT_FIN_MAP != 0;
+constexpr unsigned FIN_MAP_ROWS = 8192;       // map entries (u8 string index): rows of 64 ids, coarser past 512k ids
 constexpr unsigned SCAN_THREADS = 1024;       // threads of the batch-scan block
 constexpr uint64_t FIN_TARGET_BLOCKS = 2048;  // small batches: each batch's copy is split over slices until the grid has this many blocks
 constexpr uint64_t FIN_MAX_SLICES = 8;
@@ -2845,6 +2850,9 @@ __global__ void __launch_bounds__(FIN_THREADS) finish_kernel(FinishArgs f) {
     __shared__ uint64_t s_rel[FIN_BATCH + 1];   // ids of the batch's strings before string k, + the batch total
     __shared__ uint64_t s_src[FIN_BATCH];       // staging element of each string's first id
     __shared__ uint64_t s_w[FIN_THREADS / 64];
+    // the string holding id r << gs of the batch, per row r (FIN_MAP): a copy element finds its
+    // string from its row's in one or two LDS reads, all of a thread's elements independently
+    __shared__ uint8_t s_map[FIN_MAP ? FIN_MAP_ROWS : 1];
     const unsigned tid = threadIdx.x;
     const uint64_t t = blockIdx.x / f.slices;
     const unsigned sl = blockIdx.x % f.slices;
@@ -2870,6 +2878,14 @@ __global__ void __launch_bounds__(FIN_THREADS) finish_kernel(FinishArgs f) {
     if (tid < FIN_BATCH) {
         s_rel[tid] = incl - c;
         s_src[tid] = src;
+    }
+    unsigned gs = 6;   // rows of 64 ids, coarser when the batch has more than FIN_MAP_ROWS of them
+    if constexpr (FIN_MAP) {
+        while ((total >> gs) >= FIN_MAP_ROWS) gs++;
+        if (has && c) {   // the rows starting inside this string's ids [incl - c, incl)
+            const uint64_t rb = (incl - c + (1ull << gs) - 1u) >> gs, re = (incl - 1u) >> gs;
+            for (uint64_t r = rb; r <= re; r++) s_map[r] = (uint8_t)tid;
+        }
     }
     if (tid == FIN_BATCH - 1) s_rel[FIN_BATCH] = incl;
     __syncthreads();
@@ -2916,7 +2932,7 @@ __global__ void __launch_bounds__(FIN_THREADS) finish_kernel(FinishArgs f) {
     // the string of this thread's first id: the last string whose start is <= it (binary search;
     // then monotone in k)
     unsigned j = 0;
-    if (k_beg + tid < k_end) {
+    if (!FIN_MAP && k_beg + tid < k_end) {
         const uint64_t k = k_beg + tid;
         unsigned lo = 0, hi = FIN_BATCH;   // s_rel[lo] <= k < s_rel[hi]
         while (hi - lo > 1) {
@@ -2928,6 +2944,31 @@ __global__ void __launch_bounds__(FIN_THREADS) finish_kernel(FinishArgs f) {
     }
     for (uint64_t k0 = k_beg; k0 < k_end; k0 += FIN_THREADS * U) {
         int32_t v[U];
+        if constexpr (FIN_MAP) {
+            // each element's string: its row's, then past the string starts inside the row (rounds
+            // of U independent LDS reads instead of one chain through all of them)
+            unsigned jj[U];
+#pragma unroll
+            for (unsigned u = 0; u < U; u++) {
+                const uint64_t k = k0 + (uint64_t)u * FIN_THREADS + tid;
+                jj[u] = k < k_end ? s_map[k >> gs] : 0u;
+            }
+#pragma unroll
+            for (unsigned u = 0; u < U; u++) {
+                const uint64_t k = k0 + (uint64_t)u * FIN_THREADS + tid;
+                jj[u] += (k < k_end && s_rel[jj[u] + 1] <= k) ? 1u : 0u;
+            }
+#pragma unroll
+            for (unsigned u = 0; u < U; u++) {
+                const uint64_t k = k0 + (uint64_t)u * FIN_THREADS + tid;
+                while (k < k_end && s_rel[jj[u] + 1] <= k) jj[u]++;   // (strings shorter than a row)
+            }
+#pragma unroll
+            for (unsigned u = 0; u < U; u++) {
+                const uint64_t k = k0 + (uint64_t)u * FIN_THREADS + tid;
+                v[u] = k < k_end ? (int32_t)staging[s_src[jj[u]] + (k - s_rel[jj[u]])] : 0;
+            }
+        } else {
 #pragma unroll
         for (unsigned u = 0; u < U; u++) {
             const uint64_t k = k0 + (uint64_t)u * FIN_THREADS + tid;
@@ -2936,6 +2977,7 @@ __global__ void __launch_bounds__(FIN_THREADS) finish_kernel(FinishArgs f) {
                 while (s_rel[j + 1] <= k) j++;
                 v[u] = (int32_t)staging[s_src[j] + (k - s_rel[j])];
             }
+        }
         }
 #pragma unroll
         for (unsigned u = 0; u < U; u++) {
