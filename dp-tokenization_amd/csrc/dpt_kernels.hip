@@ -915,7 +915,7 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                 }
             }
             cp = __builtin_amdgcn_readfirstlane(part);
-            nb = __builtin_amdgcn_readlane(b, 0);
+            nb = (uint32_t)__builtin_amdgcn_readlane(b, 0);
             ne = nb < hi ? (nb + req < hi ? nb + req : hi) : nb;
             if (nb + req >= hi) {   // the partition is used up (by this claim or earlier ones)
                 if (BIG) {
@@ -2737,11 +2737,11 @@ tokenize_kernel(KernArgs ka) {
 
 constexpr unsigned FIN_U = 8;                 // loads in flight per thread of the copy (8 / 12 beat 4, 16 and 32: r04n)
 constexpr unsigned FIN_THREADS = 512;         // threads per finish block (>= FIN_BATCH): all of them copy
-#ifndef DPT_FIN_MAP     // A/B knob: the finish copy finds each element's string from a per-row map
-#define DPT_FIN_MAP 1
+constexpr unsigned FIN_MAP_ROWS = 8192;       // s_map entries (u8 string index): rows of 64 ids, coarser past 512k ids
+#ifndef DPT_FIN_PIPE    // A/B knob: the finish copy issues round r+1's loads before round r's stores
+#define DPT_FIN_PIPE 1
 #endif
-constexpr bool FIN_MAP = DPT_FIN_MAP != 0;
-constexpr unsigned FIN_MAP_ROWS = 8192;       // map entries (u8 string index): rows of 64 ids, coarser past 512k ids
+constexpr bool FIN_PIPE = DPT_FIN_PIPE != 0;
 constexpr unsigned SCAN_THREADS = 1024;       // threads of the batch-scan block
 constexpr uint64_t FIN_TARGET_BLOCKS = 2048;  // small batches: each batch's copy is split over slices until the grid has this many blocks
 constexpr uint64_t FIN_MAX_SLICES = 8;
@@ -2850,9 +2850,9 @@ __global__ void __launch_bounds__(FIN_THREADS) finish_kernel(FinishArgs f) {
     __shared__ uint64_t s_rel[FIN_BATCH + 1];   // ids of the batch's strings before string k, + the batch total
     __shared__ uint64_t s_src[FIN_BATCH];       // staging element of each string's first id
     __shared__ uint64_t s_w[FIN_THREADS / 64];
-    // the string holding id r << gs of the batch, per row r (FIN_MAP): a copy element finds its
-    // string from its row's in one or two LDS reads, all of a thread's elements independently
-    __shared__ uint8_t s_map[FIN_MAP ? FIN_MAP_ROWS : 1];
+    // the string holding id r << gs of the batch, per row r: a copy element finds its string from
+    // its row's in one or two LDS reads, all of a thread's elements independently
+    __shared__ uint8_t s_map[FIN_MAP_ROWS];
     const unsigned tid = threadIdx.x;
     const uint64_t t = blockIdx.x / f.slices;
     const unsigned sl = blockIdx.x % f.slices;
@@ -2880,12 +2880,10 @@ __global__ void __launch_bounds__(FIN_THREADS) finish_kernel(FinishArgs f) {
         s_src[tid] = src;
     }
     unsigned gs = 6;   // rows of 64 ids, coarser when the batch has more than FIN_MAP_ROWS of them
-    if constexpr (FIN_MAP) {
-        while ((total >> gs) >= FIN_MAP_ROWS) gs++;
-        if (has && c) {   // the rows starting inside this string's ids [incl - c, incl)
-            const uint64_t rb = (incl - c + (1ull << gs) - 1u) >> gs, re = (incl - 1u) >> gs;
-            for (uint64_t r = rb; r <= re; r++) s_map[r] = (uint8_t)tid;
-        }
+    while ((total >> gs) >= FIN_MAP_ROWS) gs++;
+    if (has && c) {   // the rows starting inside this string's ids [incl - c, incl)
+        const uint64_t rb = (incl - c + (1ull << gs) - 1u) >> gs, re = (incl - 1u) >> gs;
+        for (uint64_t r = rb; r <= re; r++) s_map[r] = (uint8_t)tid;
     }
     if (tid == FIN_BATCH - 1) s_rel[FIN_BATCH] = incl;
     __syncthreads();
@@ -2929,60 +2927,96 @@ __global__ void __launch_bounds__(FIN_THREADS) finish_kernel(FinishArgs f) {
     }
     const uint64_t k_beg = total * sl / f.slices, k_end = total * (sl + 1) / f.slices;
     constexpr unsigned U = FIN_U;
-    // the string of this thread's first id: the last string whose start is <= it (binary search;
-    // then monotone in k)
-    unsigned j = 0;
-    if (!FIN_MAP && k_beg + tid < k_end) {
-        const uint64_t k = k_beg + tid;
-        unsigned lo = 0, hi = FIN_BATCH;   // s_rel[lo] <= k < s_rel[hi]
-        while (hi - lo > 1) {
-            const unsigned mid = (lo + hi) >> 1;
-            if (s_rel[mid] <= k) lo = mid;
-            else hi = mid;
-        }
-        j = lo;
-    }
-    for (uint64_t k0 = k_beg; k0 < k_end; k0 += FIN_THREADS * U) {
-        int32_t v[U];
-        if constexpr (FIN_MAP) {
-            // each element's string: its row's, then past the string starts inside the row (rounds
-            // of U independent LDS reads instead of one chain through all of them)
-            unsigned jj[U];
-#pragma unroll
-            for (unsigned u = 0; u < U; u++) {
-                const uint64_t k = k0 + (uint64_t)u * FIN_THREADS + tid;
-                jj[u] = k < k_end ? s_map[k >> gs] : 0u;
-            }
-#pragma unroll
-            for (unsigned u = 0; u < U; u++) {
-                const uint64_t k = k0 + (uint64_t)u * FIN_THREADS + tid;
-                jj[u] += (k < k_end && s_rel[jj[u] + 1] <= k) ? 1u : 0u;
-            }
-#pragma unroll
-            for (unsigned u = 0; u < U; u++) {
-                const uint64_t k = k0 + (uint64_t)u * FIN_THREADS + tid;
-                while (k < k_end && s_rel[jj[u] + 1] <= k) jj[u]++;   // (strings shorter than a row)
-            }
-#pragma unroll
-            for (unsigned u = 0; u < U; u++) {
-                const uint64_t k = k0 + (uint64_t)u * FIN_THREADS + tid;
-                v[u] = k < k_end ? (int32_t)staging[s_src[jj[u]] + (k - s_rel[jj[u]])] : 0;
-            }
-        } else {
+    // a round: U ids per thread, FIN_THREADS apart (every store a coalesced row); each id's string
+    // from its row's (s_map), then past the string starts inside the row -- rounds of U independent
+    // LDS reads, not one chain through the batch's offsets
+    auto gather = [&](uint64_t k0, int32_t (&v)[U]) {
+        unsigned jj[U];
 #pragma unroll
         for (unsigned u = 0; u < U; u++) {
             const uint64_t k = k0 + (uint64_t)u * FIN_THREADS + tid;
-            v[u] = 0;
-            if (k < k_end) {
-                while (s_rel[j + 1] <= k) j++;
-                v[u] = (int32_t)staging[s_src[j] + (k - s_rel[j])];
-            }
+            jj[u] = k < k_end ? s_map[k >> gs] : 0u;
         }
+#pragma unroll
+        for (unsigned u = 0; u < U; u++) {
+            const uint64_t k = k0 + (uint64_t)u * FIN_THREADS + tid;
+            jj[u] += (k < k_end && s_rel[jj[u] + 1] <= k) ? 1u : 0u;
         }
+#pragma unroll
+        for (unsigned u = 0; u < U; u++) {
+            const uint64_t k = k0 + (uint64_t)u * FIN_THREADS + tid;
+            while (k < k_end && s_rel[jj[u] + 1] <= k) jj[u]++;   // (strings shorter than a row)
+        }
+#pragma unroll
+        for (unsigned u = 0; u < U; u++) {
+            const uint64_t k = k0 + (uint64_t)u * FIN_THREADS + tid;
+            v[u] = k < k_end ? (int32_t)staging[s_src[jj[u]] + (k - s_rel[jj[u]])] : 0;
+        }
+    };
+    auto put = [&](uint64_t k0, const int32_t (&v)[U]) {
 #pragma unroll
         for (unsigned u = 0; u < U; u++) {
             const uint64_t k = k0 + (uint64_t)u * FIN_THREADS + tid;
             if (k < k_end) f.ids[o0 + k] = v[u];
+        }
+    };
+    constexpr uint64_t STEP = (uint64_t)FIN_THREADS * U;
+    if (FIN_PIPE && f.slices > 1 && total < (1ull << 30)) {
+        // Calls split into slices (under ~512k strings, the strong-scaling shards): the next round's
+        // loads go out before this round's stores -- a load waits for every older vector-memory op of
+        // the wave, stores included, so loads behind the stores put a store's latency on every round.
+        // Branch-free rounds (ids past the slice re-read its last one; buffer stores past the slice's
+        // ids are dropped by the range check) let the waits count: the stores wait only for the older
+        // round's loads.  32-bit batch-relative ids (total < 2^30).  125k strings -2.4 %; at 1M (one
+        // slice, 13 rounds per block, the copy at HBM's pace) it measured +2.2 % (r05w), so one-slice
+        // calls keep the plain rounds.
+        // (the slice's bounds are block-uniform: readfirstlane keeps the store resource in SGPRs)
+        const unsigned kb = uni((unsigned)k_beg);
+        const unsigned n = uni((unsigned)(k_end - k_beg)), kl = kb + n - 1u;
+        const uint64_t ob = (uint64_t)(uintptr_t)(f.ids + o0 + k_beg);
+        const uint64_t obu = uni64(ob);   // (uni: unsigned halves -- a raw readfirstlane is int and sign-extends)
+        const __amdgpu_buffer_rsrc_t out = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(uintptr_t)obu, (short)0, (int)(n * 4u), 0x00020000);
+        auto gather32 = [&](unsigned r0, int32_t (&v)[U]) {   // ids kb + r0 + u * FIN_THREADS + tid
+            unsigned kk[U], jj[U];
+#pragma unroll
+            for (unsigned u = 0; u < U; u++) {
+                kk[u] = min(kb + r0 + u * FIN_THREADS + tid, kl);
+                jj[u] = s_map[kk[u] >> gs];
+            }
+#pragma unroll
+            for (unsigned u = 0; u < U; u++) jj[u] += (unsigned)s_rel[jj[u] + 1] <= kk[u] ? 1u : 0u;
+#pragma unroll
+            for (unsigned u = 0; u < U; u++)
+                while ((unsigned)s_rel[jj[u] + 1] <= kk[u]) jj[u]++;   // (strings shorter than a row)
+#pragma unroll
+            for (unsigned u = 0; u < U; u++) v[u] = (int32_t)staging[s_src[jj[u]] + (kk[u] - (unsigned)s_rel[jj[u]])];
+        };
+        auto put32 = [&](unsigned r0, const int32_t (&v)[U]) {
+#pragma unroll
+            for (unsigned u = 0; u < U; u++)
+                __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v[u], out, (r0 + u * FIN_THREADS + tid) * 4u, 0, 0);
+        };
+        if (n) {
+            // two register sets in turn (a copy between them would wait for the loads)
+            int32_t va[U], vb[U];
+            gather32(0, va);
+            for (unsigned r0 = 0;;) {
+                if (r0 + STEP >= n) { put32(r0, va); break; }
+                gather32(r0 + (unsigned)STEP, vb);
+                put32(r0, va);
+                r0 += (unsigned)STEP;
+                if (r0 + STEP >= n) { put32(r0, vb); break; }
+                gather32(r0 + (unsigned)STEP, va);
+                put32(r0, vb);
+                r0 += (unsigned)STEP;
+            }
+        }
+    } else {
+        for (uint64_t k0 = k_beg; k0 < k_end; k0 += STEP) {
+            int32_t v[U];
+            gather(k0, v);
+            put(k0, v);
         }
     }
 }

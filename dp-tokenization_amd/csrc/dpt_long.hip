@@ -218,7 +218,9 @@ __device__ __forceinline__ void long_body(const Args &a) {
         // the string's scratch range in the arena
         unsigned long long ao = 0;
         if (lane == 0) ao = atomicAdd(a.arena_used, (unsigned long long)(o1 - o0));
-        ao = ((unsigned long long)__builtin_amdgcn_readlane((unsigned)(ao >> 32), 0) << 32) | __builtin_amdgcn_readlane((unsigned)ao, 0);
+        // (each half through uint32_t: readlane returns int, and a low half >= 2^31 would sign-extend)
+        ao = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((unsigned)(ao >> 32), 0) << 32) |
+             (unsigned long long)(uint32_t)__builtin_amdgcn_readlane((unsigned)ao, 0);
         if (ao + (o1 - o0) > a.arena_cap) {
             // does not fit: status 3 (dpt_encode_host / dpt_dp_host grow the arena and rerun)
             if (lane == 0) {
@@ -415,8 +417,9 @@ __device__ __forceinline__ void long_body(const Args &a) {
                             if (hm) {
                                 unsigned long long base = 0;
                                 if (lane == 0) base = atomicAdd(a.far_count, (unsigned long long)__builtin_popcountll(hm));
-                                base = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(base >> 32)) << 32) |
-                                       __builtin_amdgcn_readfirstlane((unsigned)base);
+                                // (each half through uint32_t: readfirstlane returns int, whose sign would extend)
+                                base = ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)(base >> 32)) << 32) |
+                                       (unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)base);
                                 const uint64_t k = base + __builtin_amdgcn_mbcnt_hi((unsigned)(hm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)hm, 0u));
                                 if (hit && k < a.far_cap) {
                                     a.far[2 * k] = sb + i - 1;

@@ -179,6 +179,34 @@ def test_device_path_and_histogram(engines, oracles):
     assert np.array_equal(h[:257], np.bincount(np.minimum(counts, 257), minlength=258)[:257])
 
 
+def test_device_path_output_at_high_addresses(engines, oracles):
+    """The CSR ids written where a pointer's low 32 bits are >= 2^31: a 64-bit address put together
+    from two readfirstlane halves sign-extends its low half unless each goes through uint32 (round 5:
+    the finish copy's store resource did, and faulted the GPU)."""
+    torch = pytest.importorskip("torch")
+    from dptok import synth
+    n = 20000
+    text, offs = synth.random_ascii_corpus(n, 256, seed=23)
+    enc = engines["llama32k"]
+    dt = torch.from_numpy(text).cuda()
+    do = torch.from_numpy(offs.view(np.int64)).cuda()
+    big = torch.empty((1 << 30) + len(text), dtype=torch.int32, device="cuda")   # 4 GiB + the ids
+    lo = big.data_ptr() & 0xFFFFFFFF
+    e = ((0x80001000 - lo) & 0xFFFFFFFF) // 4   # the view's address has low word 0x80001000
+    ids = big[e: e + len(text)]
+    assert (ids.data_ptr() & 0xFFFFFFFF) >= 0x80000000
+    id_off = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    st = torch.empty(n, dtype=torch.int32, device="cuda")
+    enc.encode_device(dt.data_ptr(), len(text), do.data_ptr(), n, ids.data_ptr(), len(text), id_off.data_ptr(),
+                      st.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    rids, roff, rst, _ = oracles["llama32k"].encode_csr(text, offs)
+    off_h = id_off.cpu().numpy().view(np.uint64)
+    assert np.array_equal(off_h, roff)
+    assert np.array_equal(ids[: int(off_h[-1])].cpu().numpy(), rids)
+    del big
+
+
 @pytest.mark.parametrize("n,n_bins", [(50000, 258), (257, 258), (100, 2), (3000, 1500), (1, 16)])
 def test_histogram_folded_into_encode(n, n_bins, engines):
     """dpt_ctx_set_histogram: the finish pass's histogram (one call; n_bins > 1024 takes the separate
