@@ -264,10 +264,12 @@ struct GroupLDS {
     // G = 64, 256-byte windows, non-raw modes (no expansions: a token's bytes are the window's): per byte
     // position p <= wlen, byte[p] | BF_ATOM (an atom starts at p, or p == wlen) | BF_STOP (a word starts
     // at p, or p == wlen) -- phase A's byte-stream walker reads ONE u16 per trie step
+    // (zero-length when unused: one spare byte here rounded the 16-lane group up 16 bytes -- 21 resident
+    // waves per CU instead of 22, and the slots' bank interleaving off; the static_assert below holds it)
     static constexpr bool BSTREAM = G == 64 && CH == 256;
-    uint16_t bf[BSTREAM ? CH + 2 : 1];
+    uint16_t bf[BSTREAM ? CH + 2 : 0];
     // ... and per atom: 1 = it starts a word that is one vocabulary token (the whole-word shortcut)
-    uint8_t scf[BSTREAM ? CH + 2 : 1];
+    uint8_t scf[BSTREAM ? CH + 2 : 0];
 };
 constexpr unsigned BF_ATOM = 0x100u, BF_STOP = 0x200u;
 
@@ -293,6 +295,7 @@ constexpr int group_lds_bytes() { return (int)((sizeof(GroupLDS<CH, G>) + 15) & 
 // 2-way bank conflicts; interleaved, the same bytes are conflict-free.
 template <int CH, int G>
 constexpr int group_stride() { return group_lds_bytes<CH, G>() + (int)sizeof(SlotState); }
+static_assert(group_stride<256, 16>() == 1856, "16-lane group stride: 22 waves per CU, slots 16 dwords mod 32 apart");
 template <int CH, int G>
 constexpr int block_lds_bytes() { return (64 / G) * group_stride<CH, G>(); }
 
