@@ -60,7 +60,13 @@ def main():
     bids = np.array([t2i[t] for t in toks], dtype=np.int32)
     stream = torch.cuda.current_stream(dev).cuda_stream
     runs = []
-    for path in libs:
+    # per-library switches (comma lists, one entry per library): AB_HIST=1 folds the 258-bin token
+    # histogram into every encode (DPT_HIST_OVERWRITE, as bench.py's step), AB_PROF=1 turns the
+    # context's stage profiling on (bench.py's events around the passes)
+    hist_on = [x == "1" for x in os.environ.get("AB_HIST", "").split(",")] if os.environ.get("AB_HIST") else []
+    prof_on = [x == "1" for x in os.environ.get("AB_PROF", "").split(",")] if os.environ.get("AB_PROF") else []
+    hists = []
+    for li, path in enumerate(libs):
         L = ctypes.CDLL(os.path.abspath(path))
         L.dpt_vocab_create.argtypes = [P, P, P, ctypes.c_uint32, ctypes.c_int, ctypes.POINTER(P)]
         L.dpt_ctx_create.argtypes = [ctypes.c_int, ctypes.POINTER(P)]
@@ -71,11 +77,22 @@ def main():
         assert L.dpt_vocab_create(blob.ctypes.data, boff.ctypes.data, bids.ctypes.data, len(boff) - 1, 0, ctypes.byref(v)) == 0, L.dpt_last_error()
         assert L.dpt_ctx_create(0, ctypes.byref(c)) == 0
         assert L.dpt_ctx_reserve_vocab(c, v, nb, n, 0) == 0
+        hp = None
+        if li < len(hist_on) and hist_on[li]:
+            h = torch.zeros(258 + 8, dtype=torch.int64, device=dev)
+            hists.append(h)
+            hp = P(h.data_ptr())
+            L.dpt_ctx_set_histogram_ex.argtypes = [P, P, ctypes.c_uint32, ctypes.c_int]
+        if li < len(prof_on) and prof_on[li]:
+            L.dpt_ctx_profile.argtypes = [P, ctypes.c_int]
+            assert L.dpt_ctx_profile(c, 1) == 0
         ids = torch.empty(nb, dtype=torch.int32, device=dev)
         io = torch.empty(n + 1, dtype=torch.int64, device=dev)
         st = torch.empty(n, dtype=torch.int32, device=dev)
 
-        def enc(L=L, v=v, c=c, ids=ids, io=io, st=st):
+        def enc(L=L, v=v, c=c, ids=ids, io=io, st=st, hp=hp):
+            if hp is not None:
+                assert L.dpt_ctx_set_histogram_ex(c, hp, 258, 1) == 0
             rc = L.dpt_encode(c, v, mode, P(dt.data_ptr()), nb, P(do.data_ptr()), P(dc.data_ptr() if dc is not None else None), n,
                               P(ids.data_ptr()), nb, P(io.data_ptr()), P(st.data_ptr()), None, P(stream))
             assert rc == 0, L.dpt_last_error()
