@@ -773,6 +773,14 @@ constexpr bool NEAR_CUT64 = false;
 #define DPT_A0_SWAR 1
 #endif
 constexpr bool A0_SWAR = DPT_A0_SWAR != 0;
+#ifndef DPT_A0_R2       // A/B knob: A0's third-byte round for walks that go on past two bytes
+#define DPT_A0_R2 1
+#endif
+constexpr bool A0_R2 = DPT_A0_R2 != 0;
+#ifndef DPT_A0_R2_MIN   // ... taken when at least this many lanes of the slot have such a walk
+#define DPT_A0_R2_MIN 24
+#endif
+constexpr int A0_R2_MIN = DPT_A0_R2_MIN;
 constexpr unsigned A_REFILL = 32;     // phase A: idle lanes needed before a batched refill (1/8/16/32 within 2 %)
 constexpr unsigned A_REFILL64 = 32;   // the same for the 64-lane kernels (8 / 1: neutral / -0.5 %, r03aa)
 #ifndef DPT_STOP     // diagnostic builds only (wrong results): 1 = prep only, 21 = + A0, 2 = + A, 25 / 26 / 27 =
@@ -1230,7 +1238,51 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                             const uint32_t more = has2 & ~(xs << 3) & (nl1 | (v2 & (nl2 | (~sp2 & fb))));
                             const uint32_t tk1 = norm & tok1;                  // a one-atom token ends at k0+1+u
                             const uint32_t tk2 = has2 & ~nl1 & (xs << 4);      // a two-atom token ends at k0+2+u
-                            const uint32_t mk = ((v0 & special) | more) & H;   // walker starts
+                            uint32_t mk = ((v0 & special) | more) & H;   // walker starts
+                            if constexpr (A0_R2) {
+                                // Third-byte round: a walk that goes on past two plain bytes of the word takes
+                                // its root-table step (the node after the pair) and its third step here,
+                                // byte-parallel, and stays for the walker only if it goes on past three
+                                // (cfg4: ~97 % of these walks end there).  The three-atom token, if any, is
+                                // recorded here.  Slots with few such walks leave them to the walker.
+                                const uint32_t r2 = more & ~nl1 & ~nl2 & H;
+                                if (__builtin_popcountll(ballot(r2 != 0)) >= A0_R2_MIN) {
+                                    const uint32_t v3 = __builtin_amdgcn_alignbyte(vhi, vlo, 3u) & H;
+                                    const uint32_t sp3 = __builtin_amdgcn_alignbyte(sp1w, sp0, 3u);
+                                    const uint32_t nl3 = __builtin_amdgcn_alignbyte(nl1w, nl0, 3u);
+                                    const uint32_t n3w = __builtin_amdgcn_alignbyte(w1, w0, 3u);
+                                    constexpr int32_t OOB = 0x7FFFFFF;   // past the table: the buffer load returns zeros
+                                    int4 e2r[4], e3[4];
+#pragma unroll
+                                    for (int u = 0; u < 4; u++)   // the root table's entry of (b, n1)
+                                        e2r[u] = trie_slotA(tv, ((r2 >> (8 * u + 7)) & 1u) ? (int32_t)(tv.n_slots +
+                                                 __builtin_amdgcn_perm(w0, n1w, 0x0C0C0000u | ((4u + (unsigned)u) << 8) | (unsigned)u)) : OOB);
+#pragma unroll
+                                    for (int u = 0; u < 4; u++)   // the node after n2
+                                        e3[u] = trie_slotA(tv, ((r2 >> (8 * u + 7)) & 1u) ?
+                                                (int32_t)((e2r[u].x & BASE_MASK) + ((n2w >> (8 * u)) & 0xFFu)) : OOB);
+                                    uint32_t c3 = 0, t3 = 0;
+#pragma unroll
+                                    for (int u = 0; u < 4; u++) {
+                                        const unsigned n3 = (n3w >> (8 * u)) & 0xFFu;
+                                        const unsigned ok3 = ((r2 >> (8 * u + 7)) & 1u) & (unsigned)(e3[u].y == (e2r[u].y & 0x3FFFFFFF));
+                                        const unsigned leaf3 = ((unsigned)e3[u].x >> 30) & 1u;
+                                        const unsigned in3 = ((v3 & ~sp3) >> (8 * u + 7)) & 1u;
+                                        const unsigned ch3 = (((unsigned)e3[u].w >> child_bit(n3)) & 1u) | ((nl3 >> (8 * u + 7)) & 1u);
+                                        t3 |= (ok3 & ((unsigned)e3[u].x >> 31)) << (8 * u + 7);
+                                        c3 |= (ok3 & (leaf3 ^ 1u) & in3 & ch3) << (8 * u + 7);
+                                    }
+                                    mk = ((v0 & special) | (more & ~r2) | c3) & H;
+                                    if (ballot(t3 != 0)) {   // a three-atom token ends at k0+3+u
+                                        uint32_t *q32 = reinterpret_cast<uint32_t *>(smem + gbase);
+#pragma unroll
+                                        for (int u = 0; u < 4; u++)
+                                            __hip_atomic_fetch_and(&q32[k0 + 3u + u],
+                                                                   ~(((t3 >> (8 * u + 7)) & 1u) << 18),
+                                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                                    }
+                                }
+                            }
                             const uint32_t t2e = (tk2 << 8) | wave_shift_in(tk2 >> 24, 0u);
                             // end k0+1+u: bit 0 of byte u of d a one-atom token, bit 1 a two-atom one
                             const uint32_t d = ((tk1 & H) >> 7) | ((t2e & H) >> 6);
