@@ -230,7 +230,7 @@ std::vector<uint32_t> build_token_hash(const uint8_t *blob, const uint64_t *off,
     auto khash = [](const Key &k, uint32_t seed, uint32_t &h, uint32_t &fp) {
         const unsigned nd = k.len <= 16 ? 4u : (k.len + 3u) / 4u;
         dpt::TokHashState a = dpt::tokhash_start(k.len, seed);
-        for (unsigned q = 0; q < nd; q++) a = dpt::tokhash_step(a, k.w[q], q, q + 1 == nd);
+        for (unsigned q = 0; q < nd; q++) a = dpt::tokhash_step(a, k.w[q], q);
         dpt::tokhash_end(a, h, fp);
     };
     std::vector<uint32_t> none(4, 0u);

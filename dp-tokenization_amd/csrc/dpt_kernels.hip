@@ -453,6 +453,9 @@ __device__ __forceinline__ uint64_t atom_from_info(const uint8_t *bytes, uint32_
     return seq;
 }
 
+#ifndef DPT_KEY_NONL    // timing diagnostic (wrong ids on text with newlines): 1 = no newline scan in C2's keys
+#define DPT_KEY_NONL 0
+#endif
 // C2's hash key of the token of `nbytes` window bytes from p0 (dpt_internal.h tokhash): its expanded
 // bytes -- raw mode: the string's first atom is '\u2581' + its bytes, a leading ' ' is '\u2581' -- as
 // four little-endian dwords, zero past the expanded length E.  False (the walkers take the token) when
@@ -478,13 +481,15 @@ __device__ __forceinline__ bool token_key(const uint8_t *bytes, unsigned p0, uns
     if (raw) {
         uint32_t nl = 0;
         const uint32_t x[4] = {r0, r1, r2, r3};
+        if (DPT_KEY_NONL == 0) {
 #pragma unroll
-        for (unsigned k = 0; k < 4; k++) {
-            // bytes outside [fi, nbytes) read as 0xFF (never '\n'); haszero over x ^ '\n'
-            uint32_t v = x[k] | ~keep(nbytes, k);
-            if (k == 0) v |= fi ? 0xFFu : 0u;
-            v ^= 0x0A0A0A0Au;
-            nl |= (v - 0x01010101u) & ~v & 0x80808080u;
+            for (unsigned k = 0; k < 4; k++) {
+                // bytes outside [fi, nbytes) read as 0xFF (never '\n'); haszero over x ^ '\n'
+                uint32_t v = x[k] | ~keep(nbytes, k);
+                if (k == 0) v |= fi ? 0xFFu : 0u;
+                v ^= 0x0A0A0A0Au;
+                nl |= (v - 0x01010101u) & ~v & 0x80808080u;
+            }
         }
         if (nl) return false;
         if (fi | sp) {
@@ -546,7 +551,7 @@ __device__ __forceinline__ bool token_hash_long(const uint8_t *bytes, unsigned p
         }
         const unsigned lo = 4u * k;
         w &= E >= lo + 4u ? 0xFFFFFFFFu : (E <= lo ? 0u : (1u << (8u * (E - lo))) - 1u);
-        a = tokhash_step(a, w, k, k + 1 == nd);
+        a = tokhash_step(a, w, k);
     }
     if (nl) return false;
     tokhash_end(a, h, fp);
@@ -773,6 +778,9 @@ constexpr bool NEAR_CUT64 = false;
 #define DPT_A0_SWAR 1
 #endif
 constexpr bool A0_SWAR = DPT_A0_SWAR != 0;
+#ifndef DPT_HP_U        // A/B knob: C2 hash-pass token rounds of 64 per iteration (loads before stores)
+#define DPT_HP_U 2
+#endif
 #ifndef DPT_A0_R2       // A/B knob: A0's third-byte round for walks that go on past two bytes
 #define DPT_A0_R2 1
 #endif
@@ -2446,7 +2454,7 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                     (void *)(hbase + sizeof(TokHashHeader)), (short)0, (int)((hh.mask + 1u) * 16u), 0x00020000);
                 // token rounds of 64 per iteration, their loads before any store (a load waits for every
                 // older store of the wave; 1 or 4 rounds measured slower, r03)
-                constexpr int HP_U = 2;
+                constexpr int HP_U = DPT_HP_U;
                 unsigned r2 = 0;
                 for (unsigned i0 = 0; i0 < n; i0 += 64u * HP_U) {
                     unsigned tt[HP_U], hh2[HP_U], fpv[HP_U];
