@@ -237,39 +237,61 @@ std::vector<uint32_t> build_token_hash(const uint8_t *blob, const uint64_t *off,
     if (keys.empty()) return none;
     uint32_t nb = 1;
     while (nb < keys.size()) nb <<= 1;   // buckets of two entries: load <= 1/2
+    const uint32_t mask = nb - 1;
+    std::vector<uint32_t> H(keys.size()), F(keys.size());
     for (uint32_t seed = 0x2545F491u, tries = 0; tries < 8; tries++, seed = seed * 0x9E3779B9u + 0x7F4A7C15u) {
+        for (size_t q = 0; q < keys.size(); q++) {
+            khash(keys[q], seed, H[q], F[q]);
+            H[q] &= mask;
+        }
         std::vector<uint32_t> tab(4 + (size_t)nb * 4, 0u);
         uint32_t *bk = tab.data() + 4;
-        uint32_t max_probe = 0;
-        std::vector<std::pair<uint32_t, uint32_t>> where(keys.size());   // (bucket, slot) per key
+        std::vector<int32_t> who((size_t)nb * 2, -1);   // key per entry
+        auto put = [&](uint32_t b, unsigned e, int32_t q) {
+            bk[4 * (size_t)b + 2 * e] = F[q];
+            bk[4 * (size_t)b + 2 * e + 1] = (uint32_t)keys[q].id;
+            who[2 * (size_t)b + e] = q;
+        };
+        // cuckoo placement: a key takes a free entry of its two buckets, else evicts one (a pseudo-random
+        // walk) and the evicted key moves to its other bucket
         bool bad = false;
-        for (size_t q = 0; q < keys.size() && !bad; q++) {
-            uint32_t h, fp;
-            khash(keys[q], seed, h, fp);
-            uint32_t b = h & (nb - 1), p = 1;
-            for (;; b = (b + 1) & (nb - 1), p++) {
-                uint32_t *e = bk + 4 * (size_t)b;
-                if (e[0] == fp || e[2] == fp) { bad = true; break; }   // an earlier key would answer for this one
-                if (!e[0]) { e[0] = fp; e[1] = (uint32_t)keys[q].id; where[q] = {b, 0}; break; }
-                if (!e[2]) { e[2] = fp; e[3] = (uint32_t)keys[q].id; where[q] = {b, 1}; break; }
+        uint32_t rng = seed | 1u;
+        for (size_t q0 = 0; q0 < keys.size() && !bad; q0++) {
+            int32_t cur = (int32_t)q0;
+            uint32_t b = H[q0];
+            bool placed = false;
+            for (int kick = 0; kick < 2000 && !placed; kick++) {
+                const uint32_t b2 = dpt::tokhash_alt(b, F[cur], mask);
+                const uint32_t cand[4][2] = {{b, 0}, {b, 1}, {b2, 0}, {b2, 1}};
+                for (const auto &c : cand)
+                    if (!placed && who[2 * (size_t)c[0] + c[1]] < 0) { put(c[0], c[1], cur); placed = true; }
+                if (placed) break;
+                rng = rng * 1664525u + 1013904223u;
+                const uint32_t vb = (rng >> 16) & 1u ? b2 : b;
+                const unsigned ve = (rng >> 17) & 1u;
+                const int32_t victim = who[2 * (size_t)vb + ve];
+                put(vb, ve, cur);
+                cur = victim;
+                b = dpt::tokhash_alt(vb, F[cur], mask);   // the victim's other bucket
             }
-            max_probe = p > max_probe ? p : max_probe;
+            bad = !placed;
         }
         if (bad) continue;
-        // every key's lookup (the first entry of its fingerprint from its home bucket) is its own entry
+        // every key's lookup (the first entry of its fingerprint in bucket h, then in its partner) is its own
         for (size_t q = 0; q < keys.size() && !bad; q++) {
-            uint32_t h, fp;
-            khash(keys[q], seed, h, fp);
-            uint32_t b = h & (nb - 1);
-            for (uint32_t p = 0; p < max_probe; p++, b = (b + 1) & (nb - 1)) {
-                const uint32_t *e = bk + 4 * (size_t)b;
-                if (e[0] == fp) { bad = !(where[q].first == b && where[q].second == 0); break; }
-                if (e[2] == fp) { bad = !(where[q].first == b && where[q].second == 1); break; }
+            const uint32_t b1 = H[q], b2 = dpt::tokhash_alt(b1, F[q], mask);
+            const uint32_t cand[4][2] = {{b1, 0}, {b1, 1}, {b2, 0}, {b2, 1}};
+            bool found = false;
+            for (const auto &c : cand) {
+                if (found || bk[4 * (size_t)c[0] + 2 * c[1]] != F[q]) continue;
+                found = true;
+                bad = who[2 * (size_t)c[0] + c[1]] != (int32_t)q;
             }
+            bad = bad || !found;
         }
         if (bad) continue;
-        tab[0] = nb - 1;
-        tab[1] = max_probe;
+        tab[0] = mask;
+        tab[1] = 2;   // a lookup visits two buckets
         tab[2] = seed;
         return tab;
     }

@@ -100,16 +100,20 @@ __host__ __device__ inline unsigned child_bit(unsigned b) { return (b ^ (b >> 5)
 
 // Token hash table (C2's one-lookup ids for tokens of 3..16 expanded bytes; dpt_vocab_create builds
 // it after the A0 table in the pair16 allocation).  Key: the token's bytes as four little-endian
-// dwords, zero past its length, plus the length; bucket = h & mask, buckets of two {fp, id} entries
-// probed linearly; fp != 0 (0 marks a free entry).  The builder checks that every token's lookup
-// finds its own entry within `max_probe` buckets (else it re-seeds): a span the DP selected is a
-// vocabulary token by construction (phase A matched it), so the lookup needs no key compare.
+// dwords, zero past its length, plus the length.  Buckets of two {fp, id} entries (fp != 0; 0 marks a
+// free entry), two choices per key (cuckoo placement, round 5): bucket h & mask or its partner
+// tokhash_alt(h & mask, fp), both loaded at once -- a lookup never walks a probe chain (with linear
+// probing 5.7 % of cfg4's hashed tokens were not in their home bucket, and almost every 64-token round
+// ran the serial probe loop for some lane).  The builder checks that the first entry carrying a key's
+// fp among its two buckets (in the kernel's order) is its own (else it re-seeds): a span the DP
+// selected is a vocabulary token by construction (phase A matched it), so the lookup needs no key
+// compare.
 constexpr unsigned TOKHASH_MAX_BYTES = 16;        // the 16-lane kernels' keys (four dwords)
 constexpr unsigned TOKHASH_MAX_BYTES_LONG = 64;   // the table's tokens; the 64-lane kernels hash keys this long
 constexpr size_t TOKHASH_OFFSET = PAIR16_N * sizeof(int16_t) + 65536 * 8;   // bytes into the pair16 allocation
 struct TokHashHeader {
     uint32_t mask;        // buckets - 1 (a power of two)
-    uint32_t max_probe;   // buckets a lookup may visit (0: no table -- the walkers resolve every token)
+    uint32_t max_probe;   // buckets a lookup visits: 2 (its two choices); 0: no table -- the walkers resolve every token
     uint32_t seed;
     uint32_t nl_id1;      // 1 + the id of "<0x0A>" (0: none): raw mode's one-atom '\n' tokens take it without a lookup
 };
@@ -122,9 +126,7 @@ struct TokHashHeader {
 // byte-level vocabularies' keys whose differences sit in the top bytes of two dwords do not cancel (a
 // linear sum of w_k * K[k] mod 2^32 failed every seed on the 250,680-token BLOOM vocabulary).  (h, fp)
 // carry the whole 64-bit state: a fingerprint derived from h alone (round 2) left 32 bits per key and
-// ~7 full collisions among the BLOOM keys.  Measured with the host builder's insertion on the synthetic
-// 32k vocabulary: 88.7 % of keys in their home bucket, max_probe 14 (the previous hash 88.0 %, 11);
-// BLOOM: the first seed builds, max_probe 16.
+// ~7 full collisions among the BLOOM keys.
 constexpr uint32_t TOKHASH_K[17] = {
     0xFB13EED5u, 0xE031651Bu, 0xD57B9AE9u, 0xF49344BFu, 0xB7A058D5u, 0xB4BC663Du, 0xE3606AA1u, 0x829E9285u, 0x9D183F11u,
     0xF3C85069u, 0xAEAD8A81u, 0xC9C1030Bu, 0xC71547B7u, 0xF78B48A3u, 0xB5FE207Fu, 0xEA0A7265u, 0xC71BEEC7u};
@@ -143,6 +145,8 @@ __host__ __device__ inline void tokhash_end(TokHashState s, uint32_t &h, uint32_
     h = (uint32_t)t ^ (uint32_t)(t >> 32);
     fp = (uint32_t)(t >> 32) | 1u;
 }
+// the partner of bucket b for a key of fingerprint fp (an involution: from either bucket, the other)
+__host__ __device__ inline uint32_t tokhash_alt(uint32_t b, uint32_t fp, uint32_t mask) { return (b ^ (fp >> 8)) & mask; }
 // four-dword keys (tokens of at most 16 bytes)
 __host__ __device__ inline void tokhash(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t len, uint32_t seed,
                                         uint32_t &h, uint32_t &fp) {

@@ -778,6 +778,10 @@ constexpr bool NEAR_CUT64 = false;
 #define DPT_A0_SWAR 1
 #endif
 constexpr bool A0_SWAR = DPT_A0_SWAR != 0;
+#ifndef DPT_HASH_BOTH   // A/B knob: C2's hash lookups load both buckets at once (0: the partner only on a miss)
+#define DPT_HASH_BOTH 0
+#endif
+constexpr bool HASH_BOTH = DPT_HASH_BOTH != 0;
 #ifndef DPT_HP_U        // A/B knob: C2 hash-pass token rounds of 64 per iteration (loads before stores)
 #define DPT_HP_U 2
 #endif
@@ -2489,25 +2493,35 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                         }
                         tt[u] = t; hh2[u] = h & hh.mask; fpv[u] = fp; oqv[u] = q.ob + k; hs[u] = hashed; inr[u] = in;
                     }
-                    // every round's first probe, then the rare further probes, then the stores
                     int32_t idv[HP_U];
+                    if constexpr (HASH_BOTH) {
+                        // every round's two buckets (the key's two choices) at once, then the stores
 #pragma unroll
-                    for (int u = 0; u < HP_U; u++) {
-                        const auto e = __builtin_amdgcn_raw_buffer_load_b128(hr, hh2[u] * 16u, 0, 0);
-                        idv[u] = e[0] == fpv[u] ? (int32_t)e[1] : (e[2] == fpv[u] ? (int32_t)e[3] : INT32_MIN);
-                    }
+                        for (int u = 0; u < HP_U; u++) {
+                            const auto e = __builtin_amdgcn_raw_buffer_load_b128(hr, hh2[u] * 16u, 0, 0);
+                            const auto f = __builtin_amdgcn_raw_buffer_load_b128(hr, tokhash_alt(hh2[u], fpv[u], hh.mask) * 16u, 0, 0);
+                            idv[u] = e[0] == fpv[u] ? (int32_t)e[1] : e[2] == fpv[u] ? (int32_t)e[3] :
+                                     f[0] == fpv[u] ? (int32_t)f[1] : f[2] == fpv[u] ? (int32_t)f[3] : -1;
+                        }
+                    } else {
+                        // every round's home bucket, then the partner buckets of the keys not found there
+                        // (one more load round for the wave, never a chain), then the stores
 #pragma unroll
-                    for (int u = 0; u < HP_U; u++) {
-                        if (hs[u] && idv[u] == INT32_MIN) {
-                            int32_t v = -1;
-                            unsigned b = hh2[u];
-                            for (unsigned pr = 1; pr < hh.max_probe; pr++) {
-                                b = (b + 1u) & hh.mask;
-                                const auto e = __builtin_amdgcn_raw_buffer_load_b128(hr, b * 16u, 0, 0);
-                                if (e[0] == fpv[u]) { v = (int32_t)e[1]; break; }
-                                if (e[2] == fpv[u]) { v = (int32_t)e[3]; break; }
+                        for (int u = 0; u < HP_U; u++) {
+                            const auto e = __builtin_amdgcn_raw_buffer_load_b128(hr, hh2[u] * 16u, 0, 0);
+                            idv[u] = e[0] == fpv[u] ? (int32_t)e[1] : (e[2] == fpv[u] ? (int32_t)e[3] : INT32_MIN);
+                        }
+                        bool miss = false;
+#pragma unroll
+                        for (int u = 0; u < HP_U; u++) miss |= hs[u] && idv[u] == INT32_MIN;
+                        if (ballot(miss)) {
+#pragma unroll
+                            for (int u = 0; u < HP_U; u++) {
+                                if (hs[u] && idv[u] == INT32_MIN) {
+                                    const auto f = __builtin_amdgcn_raw_buffer_load_b128(hr, tokhash_alt(hh2[u], fpv[u], hh.mask) * 16u, 0, 0);
+                                    idv[u] = f[0] == fpv[u] ? (int32_t)f[1] : (f[2] == fpv[u] ? (int32_t)f[3] : -1);
+                                }
                             }
-                            idv[u] = v;
                         }
                     }
 #pragma unroll
