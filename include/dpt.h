@@ -77,8 +77,9 @@ typedef struct {
     uint32_t max_bytes;    /* longest token, UTF-8 bytes */
     uint32_t max_cp;       /* longest token, code points */
     uint64_t device_bytes; /* device memory held by the vocab */
-    uint32_t hash_max_probe;   /* C2's token hash table (ABI 2): buckets a lookup may visit; 0 = no table
-                                  (every selected token is then re-walked in the trie) */
+    uint32_t hash_max_probe;   /* C2's token hash table (ABI 2): buckets a lookup may visit (2: a key's
+                                  two choices, round 5); 0 = no table (every selected token is then
+                                  re-walked in the trie) */
     uint32_t hash_buckets;     /* its buckets of two entries (0 = no table) */
 } dpt_vocab_stats;
 
