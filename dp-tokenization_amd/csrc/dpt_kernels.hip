@@ -453,9 +453,6 @@ __device__ __forceinline__ uint64_t atom_from_info(const uint8_t *bytes, uint32_
     return seq;
 }
 
-#ifndef DPT_KEY_NONL    // timing diagnostic (wrong ids on text with newlines): 1 = no newline scan in C2's keys
-#define DPT_KEY_NONL 0
-#endif
 // C2's hash key of the token of `nbytes` window bytes from p0 (dpt_internal.h tokhash): its expanded
 // bytes -- raw mode: the string's first atom is '\u2581' + its bytes, a leading ' ' is '\u2581' -- as
 // four little-endian dwords, zero past the expanded length E.  False (the walkers take the token) when
@@ -481,15 +478,13 @@ __device__ __forceinline__ bool token_key(const uint8_t *bytes, unsigned p0, uns
     if (raw) {
         uint32_t nl = 0;
         const uint32_t x[4] = {r0, r1, r2, r3};
-        if (DPT_KEY_NONL == 0) {
 #pragma unroll
-            for (unsigned k = 0; k < 4; k++) {
-                // bytes outside [fi, nbytes) read as 0xFF (never '\n'); haszero over x ^ '\n'
-                uint32_t v = x[k] | ~keep(nbytes, k);
-                if (k == 0) v |= fi ? 0xFFu : 0u;
-                v ^= 0x0A0A0A0Au;
-                nl |= (v - 0x01010101u) & ~v & 0x80808080u;
-            }
+        for (unsigned k = 0; k < 4; k++) {
+            // bytes outside [fi, nbytes) read as 0xFF (never '\n'); haszero over x ^ '\n'
+            uint32_t v = x[k] | ~keep(nbytes, k);
+            if (k == 0) v |= fi ? 0xFFu : 0u;
+            v ^= 0x0A0A0A0Au;
+            nl |= (v - 0x01010101u) & ~v & 0x80808080u;
         }
         if (nl) return false;
         if (fi | sp) {
@@ -778,6 +773,9 @@ constexpr bool NEAR_CUT64 = false;
 #define DPT_A0_SWAR 1
 #endif
 constexpr bool A0_SWAR = DPT_A0_SWAR != 0;
+#ifndef DPT_BULK_U      // A/B knob: C2's bulk pass, tokens per lane per round (their lookups before their stores)
+#define DPT_BULK_U 4
+#endif
 #ifndef DPT_HASH_BOTH   // A/B knob: C2's hash lookups load both buckets at once (0: the partner only on a miss)
 #define DPT_HASH_BOTH 0
 #endif
@@ -2551,9 +2549,10 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                 // counts loads and stores together, in issue order), so a store between two rounds of
                 // lookups put a store's full latency on every round.  (Every round's lookups before any
                 // store held the ids in registers and spilled: cfg2 -4.1 %, r03.)
-                auto bulk_round = [&](unsigned t0, int32_t (&ix)[4], unsigned (&kind)[4], uint64_t (&oq)[4]) {
+                constexpr int BU = DPT_BULK_U;   // tokens per lane per round
+                auto bulk_round = [&](unsigned t0, int32_t (&ix)[BU], unsigned (&kind)[BU], uint64_t (&oq)[BU]) {
 #pragma unroll
-                    for (int u = 0; u < 4; u++) {
+                    for (int u = 0; u < BU; u++) {
                         const unsigned t = t0 + 64u * (unsigned)u + lane;
                         const bool in = t < total;
                         unsigned g = 0;
@@ -2587,25 +2586,25 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                         r += (unsigned)__builtin_popcountll(m);
                     }
                 };
-                for (unsigned t0 = 0; t0 < total; t0 += 64u * 4u) {
-                    int32_t ix[4];
-                    unsigned kind[4];   // 0: not here, 1 / 2: a token of that many bytes
-                    uint64_t oq[4];
+                for (unsigned t0 = 0; t0 < total; t0 += 64u * (unsigned)BU) {
+                    int32_t ix[BU];
+                    unsigned kind[BU];   // 0: not here, 1 / 2: a token of that many bytes
+                    uint64_t oq[BU];
                     bulk_round(t0, ix, kind, oq);
                     if constexpr (SW == 1) {
-                        int16_t pv[4];
+                        int16_t pv[BU];
 #pragma unroll
-                        for (int u = 0; u < 4; u++) pv[u] = tv.pair16[ix[u]];
+                        for (int u = 0; u < BU; u++) pv[u] = tv.pair16[ix[u]];
 #pragma unroll
-                        for (int u = 0; u < 4; u++)
+                        for (int u = 0; u < BU; u++)
                             if (kind[u]) a.staging16[oq[u]] = pv[u];
                         continue;
                     }
-                    int4 ent[4];
+                    int4 ent[BU];
 #pragma unroll
-                    for (int u = 0; u < 4; u++) ent[u] = trie_slotA(tv, ix[u]);
+                    for (int u = 0; u < BU; u++) ent[u] = trie_slotA(tv, ix[u]);
 #pragma unroll
-                    for (int u = 0; u < 4; u++) {
+                    for (int u = 0; u < BU; u++) {
                         if (kind[u]) {
                             // the walker's rule: the id of the node reached when every step's check held
                             const bool ok = kind[u] == 1u ? ent[u].y == 0 : (ent[u].y & 0x3FFFFFFF) != 0;
