@@ -13,6 +13,9 @@ for lib in "$@"; do
   tag=$(basename $(dirname $lib))
   DPT_LIB=$PWD/$lib timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $out/$tag/trace -o run --output-format csv -- python3 tools/prof_driver.py $N 4 $GEN > $out/$tag.trace.log 2>&1 || { tail -5 $out/$tag.trace.log; exit 1; }
   DPT_LIB=$PWD/$lib timeout -k 10 120 rocprofv3 --kernel-trace --pmc $CTRS -d $out/$tag/p1 -o run --output-format csv -- python3 tools/prof_driver.py $N 2 $GEN > $out/$tag.pmc.log 2>&1 || { tail -5 $out/$tag.pmc.log; exit 1; }
+  if [ "${PHASE_FETCH:-0}" = 1 ]; then   # HBM read bytes per stop build: where the reads beyond the input come from
+    DPT_LIB=$PWD/$lib timeout -k 10 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $out/$tag/p2 -o run --output-format csv -- python3 tools/prof_driver.py $N 2 $GEN > $out/$tag.fetch.log 2>&1 || { tail -5 $out/$tag.fetch.log; exit 1; }
+  fi
   echo "== $tag"
   python3 tools/pmc_summary.py $out/$tag | grep -A12 "kernel<256"
 done

@@ -36,12 +36,16 @@ for line in open(sys.argv[1]):
     if "tokenize_kernel<2048" in line or "finish" in line:
         kern = False
         continue
-    m = re.match(r"\s+(SQ_\w+)\s+(\S+)", line)
+    m = re.match(r"\s+(SQ_\w+|FETCH_SIZE)\s+(\S+)", line)
     if m and kern:
         cur[m.group(1)] = float(m.group(2))
-keys = ["SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_ACTIVE_INST_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_WAIT_ANY", "SQ_WAVE_CYCLES"]
-print("%-24s %7s %7s | %8s %8s %9s %9s %6s %8s" % ("phase (build)", "ms", "+ms", "+VALU G", "+LDS G", "+LDSact G",
-                                                     "+LDScnf G", "ratio", "+wait G"))
+keys = ["SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_ACTIVE_INST_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_WAIT_ANY", "SQ_WAVE_CYCLES",
+        "FETCH_SIZE"]
+# FETCH_SIZE (PHASE_FETCH=1 runs) is in KiB; x 1.994, the factor tools/pmc_traffic.py calibrates on the
+# prep-only build (whose reads are exactly the input bytes + offsets)
+FETCH_FACTOR = 1.994
+print("%-24s %7s %7s | %8s %8s %9s %9s %6s %8s %9s" % ("phase (build)", "ms", "+ms", "+VALU G", "+LDS G", "+LDSact G",
+                                                          "+LDScnf G", "ratio", "+wait G", "+read MB"))
 prev = {k: 0.0 for k in keys}
 prev_ms = 0.0
 for b in order:
@@ -51,9 +55,10 @@ for b in order:
     ms = r.get("ns", 0.0) / 1e6
     d = {k: r.get(k, 0.0) - prev[k] for k in keys}
     act, cnf = d["SQ_ACTIVE_INST_LDS"], d["SQ_LDS_BANK_CONFLICT"]
-    print("%-24s %7.3f %7.3f | %8.3f %8.3f %9.3f %9.3f %6.2f %8.3f" % (
+    rd = ("%9.1f" % (d["FETCH_SIZE"] * 1024 * FETCH_FACTOR / 1e6)) if "FETCH_SIZE" in r else "        -"
+    print("%-24s %7.3f %7.3f | %8.3f %8.3f %9.3f %9.3f %6.2f %8.3f %s" % (
         names.get(b, b), ms, ms - prev_ms, d["SQ_INSTS_VALU"] / 1e9, d["SQ_INSTS_LDS"] / 1e9, act / 1e9, cnf / 1e9,
-        cnf / act if act > 0 else 0.0, d["SQ_WAIT_ANY"] / 1e9))
+        cnf / act if act > 0 else 0.0, d["SQ_WAIT_ANY"] / 1e9, rd))
     prev = {k: r.get(k, 0.0) for k in keys}
     prev_ms = ms
 full = rows.get("dptok")
