@@ -49,10 +49,12 @@ def parse():
                     help="GPUs (ranks) of the job; default: WORLD_SIZE under torchrun, else 1")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=["cfg1", "cfg2", "cfg4", "cfg5", "bloom"], default="cfg2",
+    ap.add_argument("--workload", choices=["cfg1", "cfg2", "cfg4", "cfg5", "bloom", "cfg2p", "cfg4p"], default="cfg2",
                     help="cfg2 (the metric's config): 256-byte random ASCII; cfg1: BASELINE configs[0], 1k x 64-byte "
                          "random ASCII with the toy 1k vocabulary (the reference's CPU plumbing case); "
-                         "cfg4: S2ORC-shaped; cfg5: Arabic-shaped; "
+                         "cfg4: S2ORC-shaped; cfg5: Arabic-shaped; cfg2p / cfg4p: the same corpora in llama mode "
+                         "(pretokenize_option='llama', the factory's default: BOS word + SentencePiece-shaped words, "
+                         "pre-split on the host (dptok.synth.llama_words), DPT_MODE_PRESPLIT on the GPU); "
                          "bloom: row f3 at BLOOM scale (250,680-entry byte-level BPE, atoms mode, <= 256-byte strings)")
     ap.add_argument("--strings", type=int, default=None,
                     help="strings of the global corpus (strong) or per GPU (weak); default 1M (cfg4: 200k)")
@@ -117,6 +119,9 @@ def _port_init(kind: str = "llama"):
         from bloom_fixture import big_vocab
         _PORT["t2i"] = big_vocab()
         _PORT["f"] = ref_port.dp_tokenize_word_atoms
+    elif kind == "presplit":   # words of code points (llama mode: merge_tokens' strings, tokenizer_utils.py:70-71)
+        _PORT["t2i"] = synth.llama_shaped_vocab()
+        _PORT["f"] = ref_port.dp_tokenize_word_atoms
     else:
         _PORT["t2i"] = synth.toy_vocab() if kind == "toy" else synth.llama_shaped_vocab()
         _PORT["f"] = ref_port.dp_tokenize_raw
@@ -130,7 +135,11 @@ def _port_one(item):
     signal.alarm(10)
     try:
         x = item[0]
-        if isinstance(x, tuple):   # bloom: (bytes, cut bytes) -> words of atoms, in the worker
+        if isinstance(x, tuple) and x[0] == "presplit":   # (tag, bytes, cut bytes) -> words of code points
+            b, c = x[1], x[2]
+            starts = [k for k in range(len(b)) if c[k] and (b[k] & 0xC0) != 0x80] + [len(b)]
+            x = [list(b[starts[j]:starts[j + 1]].decode("utf-8")) for j in range(len(starts) - 1)]
+        elif isinstance(x, tuple):   # bloom: (bytes, cut bytes) -> words of atoms, in the worker
             b, c = x
             x = words_of_atoms(np.frombuffer(b, np.uint8), np.array([0, len(b)], np.uint64), np.frombuffer(c, np.uint8))[0]
         _PORT["f"](x, _PORT["t2i"])
@@ -288,12 +297,31 @@ def resolve_world(args, env=os.environ) -> int:
 
 def spawn_ranks(args, argv) -> int:
     """--gpus N > 1 from a plain `python bench.py`: one rank per GPU through torch.distributed.run, as a
-    child process (this process has not touched the GPU); its exit code is ours."""
+    child process (this process has not touched the GPU); its exit code is ours.  A SIGTERM / SIGINT to
+    this process is passed on to torchrun as SIGTERM (which stops its ranks), and we wait for it to exit,
+    so no rank is left holding a GPU.  (The port is picked just before the launch; torchrun binds it
+    first thing, so the window for another process to take it is the launch itself.)"""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
            "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + list(argv)
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     log("launching %d ranks: %s" % (args.gpus, " ".join(cmd)))
-    return subprocess.call(cmd, env=env)
+    child = subprocess.Popen(cmd, env=env)
+    stop = []
+
+    def forward(signum, frame):
+        stop.append(signum)
+        if child.poll() is None:
+            child.send_signal(signal.SIGTERM)
+    old = {sg: signal.signal(sg, forward) for sg in (signal.SIGTERM, signal.SIGINT)}
+    try:
+        rc = child.wait()
+    finally:
+        for sg, h in old.items():
+            signal.signal(sg, h)
+    if stop:
+        log("stopped by signal %d; torchrun exited with %d" % (stop[0], rc))
+        return 128 + stop[0]
+    return rc
 
 
 def main():
@@ -312,6 +340,8 @@ def main():
     from dptok import Encoder, Vocab, synth
     from dptok import dist as ddist
     bloom = args.workload == "bloom"
+    presplit = args.workload in ("cfg2p", "cfg4p")
+    base_wl = args.workload[:-1] if presplit else args.workload
     if bloom:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         from bloom_fixture import big_vocab
@@ -325,7 +355,7 @@ def main():
     gen_procs = args.gen_procs or max(1, min(16, cores))
     if args.cpu_sample is None:
         args.cpu_sample = 262144 if bloom else 2048
-    default_n = {"cfg1": 1000, "cfg4": 200_000, "bloom": 500_000}.get(args.workload, 1_000_000)
+    default_n = {"cfg1": 1000, "cfg4": 200_000, "bloom": 500_000}.get(base_wl, 1_000_000)
     N = args.strings or default_n
     lo, hi = rank_strings(N, rank, world, scaling)
     M = hi - lo
@@ -342,11 +372,11 @@ def main():
         wl = f"cfg1: {N} x {Lb}-byte random ASCII strings {per}, raw pre-tokenization, toy 1k vocabulary"
         data = ("synthetic random printable ASCII (Philox keyed by seed+global index; tests/golden/cfg1_toy1k holds the "
                 "reference's outputs for seed 1); synthetic toy 1000-entry vocab")
-    elif args.workload == "cfg2":
+    elif base_wl == "cfg2":
         text, offs = synth.random_ascii_corpus(M, Lb, seed=args.seed, start=lo)
         wl = f"cfg2: {N // 1000}k x {Lb}-byte random ASCII strings {per}, raw pre-tokenization"
         data = "synthetic random printable ASCII (Philox keyed by seed+global index); synthetic Llama-shaped 32k vocab"
-    elif args.workload == "cfg4":
+    elif base_wl == "cfg4":
         text, offs = synth.generate_parallel("s2orc", M, start=lo, procs=gen_procs, seed=4)
         wl = f"cfg4: {N // 1000}k S2ORC-shaped abstracts {per} (~1200 B, N(1200,400) clipped to [64,4096]), raw"
         data = "synthetic S2ORC-shaped pseudo-English (dptok.synth.s2orc_like_corpus); synthetic Llama-shaped 32k vocab"
@@ -354,6 +384,16 @@ def main():
         text, offs = synth.generate_parallel("arabic", M, start=lo, procs=gen_procs, length=Lb, seed=5)
         wl = f"cfg5: {N // 1000}k x ~{Lb}-byte Arabic-shaped strings {per} (2-byte code points), raw"
         data = "synthetic Arabic-shaped UTF-8 (dptok.synth.arabic_corpus); synthetic Llama-shaped 32k vocab + Arabic letters"
+    raw_text_bytes = int(offs[-1])
+    if presplit:
+        # llama mode (reference tokenizer_utils.py:24-31, :64-65): the host's SentencePiece + merge_tokens words,
+        # here the shape a Llama-2 model gives this text (BOS word, '▁' for spaces and the dummy prefix, the
+        # byte-fallback piece for '\n'), as UTF-8 + a word-start mask; the timed step is the GPU part
+        text, offs, cut = synth.llama_words(text, offs)
+        wl = args.workload + wl[len(base_wl):]
+        wl = wl.replace("raw pre-tokenization", "llama mode").replace("), raw", "), llama mode") + \
+            " (pre-split words: <s>, then SentencePiece-shaped words; DPT_MODE_PRESPLIT)"
+        data += "; words pre-split on the host by dptok.synth.llama_words (SentencePiece's shape for this text)"
     Lb = int(offs[-1]) // max(M, 1)
     log(f"corpus ready: {M} strings, {int(offs[-1])} bytes")
     cpu = None
@@ -364,11 +404,14 @@ def main():
         if bloom:
             tb, cb = text.tobytes(), cut.tobytes()
             inputs = [(tb[int(sub[i]):int(sub[i + 1])], cb[int(sub[i]):int(sub[i + 1])]) for i in range(args.cpu_sample)]
+        elif presplit:
+            tb, cb = text.tobytes(), cut.tobytes()
+            inputs = [("presplit", tb[int(sub[i]):int(sub[i + 1])], cb[int(sub[i]):int(sub[i + 1])]) for i in range(args.cpu_sample)]
         else:
             inputs = synth.unpack(text[: int(offs[args.cpu_sample])], sub)
         items = list(zip(inputs, np.diff(sub).astype(int).tolist()))
         v, nd, nto, cdt = cpu_baseline(items, args.cpu_budget, cores,
-                                       "bloom" if bloom else ("toy" if args.workload == "cfg1" else "llama"))
+                                       "bloom" if bloom else "presplit" if presplit else ("toy" if args.workload == "cfg1" else "llama"))
         cpu = {"value": v, "unit": "bytes/s", "cores": cores, "host_cpus_visible": cpus_visible, "kind": "port",
                "sample": f"{nd} of the first {args.cpu_sample} {args.workload} strings in {cdt:.1f}s "
                          f"(enumerate-then-select, oracle/ref_port.py, {cores} processes = the box's CPU share "
@@ -412,6 +455,7 @@ def main():
     pending = [None, None]
     n_step = [0]
     enc.reserve(n_bytes, M)
+    kmode = "atoms" if bloom else "presplit" if presplit else "raw"
     stream = torch.cuda.current_stream(dev).cuda_stream
 
     def step():
@@ -426,7 +470,7 @@ def main():
         enc.set_histogram(h.data_ptr(), N_BINS, overwrite=True)
         enc.encode_device(d_text.data_ptr(), n_bytes, d_off.data_ptr(), M, d_ids.data_ptr(), max(n_bytes, 1),
                           d_idoff.data_ptr(), d_status.data_ptr(), stream=stream,
-                          cut_ptr=d_cut.data_ptr() if bloom else 0, mode="atoms" if bloom else "raw")
+                          cut_ptr=d_cut.data_ptr() if d_cut is not None else 0, mode=kmode)
         if coll:   # the single collective: RCCL over xGMI with nccl, gloo in rehearsals
             if red_dev.type == "cpu":
                 hc = h.cpu()
@@ -482,7 +526,7 @@ def main():
     def step_padded():
         enc.encode_device_padded(d_text.data_ptr(), n_bytes, d_off.data_ptr(), M, d_pids.data_ptr(), max(n_bytes, 1),
                                  d_cnt.data_ptr(), d_pst.data_ptr(), stream=stream,
-                                 cut_ptr=d_cut.data_ptr() if bloom else 0, mode="atoms" if bloom else "raw")
+                                 cut_ptr=d_cut.data_ptr() if d_cut is not None else 0, mode=kmode)
 
     for _ in range(args.warmup):
         step_padded()
@@ -511,6 +555,7 @@ def main():
     n_tok_all = int(hist[N_BINS])          # after the all-reduce: all ranks' ids
     ok_strings = int(hist[N_BINS + 2])
     bytes_all = all_sum(float(n_bytes))
+    raw_all = all_sum(float(raw_text_bytes))
     strings_all = int(all_sum(float(M)))
 
     # roofline of the dominant kernel (tokenize), SURVEY.md §8d bytes per launch (ids at 4 bytes)
@@ -530,7 +575,7 @@ def main():
     off_h = d_idoff.cpu().numpy().view(np.uint64)
     st_h = d_status.cpu().numpy()
     ov = oracle.OracleVocab(t2i)
-    omode = oracle.ATOMS if bloom else oracle.RAW
+    omode = oracle.ATOMS if bloom else oracle.PRESPLIT if presplit else oracle.RAW
     rids, roff, rst, _ = ov.encode_csr(text, offs[: S + 1], mode=omode, cut_mask=cut, nthreads=per_rank_threads)
     same = exact_matches(ids_h, off_h, st_h, rids, roff, rst, S)
     same_all, checked_all = all_sum(float(same)), all_sum(float(S))
@@ -566,6 +611,7 @@ def main():
                        "parallelism": f"dp{world} ({scaling} scaling: corpus shards, 1 all-reduce of the histogram per step)"},
             "per_gpu_bytes_per_s": value / world,
             "tokens_per_byte": n_tok_all / max(bytes_all, 1.0),
+            **({"raw_text_bytes_per_s": raw_all * args.steps / dt, "raw_text_bytes": int(raw_all)} if presplit else {}),
             "ok_strings": ok_strings,
             # the reduced histogram itself (tests/test_gpu_sharded.py compares ranks x shards runs)
             "histogram": {"n_bins": N_BINS, "sha256": hashlib.sha256(hist.astype("<i8").tobytes()).hexdigest(),
@@ -576,8 +622,9 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic_for(M, Lb) if (args.workload == "cfg2" and world == 1) else None,
-                         "kernel": ("tokenize_kernel<256,64,false,true>" if bloom else
-                                    "tokenize_kernel<256,16,false,false,%d>" % (1 if id_bytes == 2 else 2)),
+                         "kernel": ("tokenize_kernel<256,64,false,true,0,false>" if bloom else
+                                    "tokenize_kernel<256,16,false,false,%d,%s>" % (1 if id_bytes == 2 else 2,
+                                                                                 "false" if presplit else "true")),
                          "alg_bytes_per_launch": alg_bytes,
                          "alg_bytes_formula": "N_in + 4*N_tok + 8(N+1) + 8(N+1) + 4N (SURVEY.md 8d)",
                          "alg_bytes_staged_width": alg_staged, "staged_id_bytes": id_bytes,

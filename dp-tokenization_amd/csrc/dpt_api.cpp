@@ -70,6 +70,9 @@ struct dpt_ctx {
     bool profile = false;
     std::vector<hipEvent_t> events;   // groups of 4 per call
     uint64_t launches = 0;
+    // test-only (dpt_ctx_debug_counter_bias): every call starts the unbounded pass's arena counter and the
+    // far-pair counter at this value, the arena and far pointers passed down shifted by it
+    uint64_t counter_bias = 0;
 };
 
 namespace {
@@ -154,12 +157,13 @@ int ensure_workspace(dpt_ctx *c, const dpt_vocab *v, uint64_t n_bytes, uint64_t 
         c->arena_cap = cap / ARENA_PER_BYTE;
     }
     if (n_str > c->cap_str || !c->counts) {
-        uint64_t cap = c->cap_str, cap2 = 2 * c->cap_str;
+        uint64_t cap = c->cap_str, cap2 = 3 * c->cap_str;
         e = grow(&c->counts, &cap, n_str);
         if (e != hipSuccess) return hip_fail(e, "hipMalloc(counts)");
-        e = grow(&c->retry_list, &cap2, 2 * n_str);   // the 2048-byte pass's list, then the unbounded pass's
+        // the first pass's retry list, the unbounded pass's list, the 2048-byte pass's list after the 512-byte pass
+        e = grow(&c->retry_list, &cap2, 3 * n_str);
         if (e != hipSuccess) return hip_fail(e, "hipMalloc(retry_list)");
-        cap2 /= 2;
+        cap2 /= 3;
         c->cap_str = cap < cap2 ? cap : cap2;
     }
     const uint64_t nbat = (n_str + dpt::FIN_BATCH - 1) / dpt::FIN_BATCH;
@@ -514,7 +518,7 @@ int dpt_ctx_reserve_vocab(dpt_ctx *c, const dpt_vocab *v, uint64_t n_bytes, uint
 int dpt_ctx_workspace_bytes(const dpt_ctx *c, uint64_t *device_path, uint64_t *host_path) {
     if (!c) return fail(DPT_E_ARG, "null ctx");
     if (device_path)
-        *device_path = c->cap16 * 2 + c->cap32 * 4 + c->arena_cap * ARENA_PER_BYTE + c->cap_str * (8 + 2 * 4) +
+        *device_path = c->cap16 * 2 + c->cap32 * 4 + c->arena_cap * ARENA_PER_BYTE + c->cap_str * (8 + 3 * 4) +
                        flag_words(c->cap_batches) * 8 + (c->wsl_scratch ? dpt::wsl_scratch_bytes(c->max_blocks) : 0) +
                        (c->pend ? dpt::pend_scratch_bytes(c->max_blocks) : 0) +
                        (c->retry_count ? dpt::CTR_ALLOC_BYTES : 0);
@@ -530,6 +534,14 @@ int dpt_ctx_long_need(dpt_ctx *c, uint64_t *need, uint64_t *cap) {
     DeviceGuard g(c->device);
     hipError_t e = hipMemcpy(need, reinterpret_cast<uint8_t *>(c->retry_count) + 40, sizeof(uint64_t), hipMemcpyDeviceToHost);
     if (e != hipSuccess) return hip_fail(e, "D2H arena counter");
+    *need = *need >= c->counter_bias ? *need - c->counter_bias : 0;   // (0 after an empty call)
+    return DPT_OK;
+}
+
+int dpt_ctx_debug_counter_bias(dpt_ctx *c, uint64_t bias) {
+    if (!c) return fail(DPT_E_ARG, "null ctx");
+    if (bias >= (1ull << 62)) return fail(DPT_E_ARG, "counter bias too large");
+    c->counter_bias = bias;
     return DPT_OK;
 }
 
@@ -594,6 +606,23 @@ static int encode_impl(dpt_ctx *c, const dpt_vocab *v, int mode_flags, const uin
     p.max_blocks = c->max_blocks;
     p.arena = c->arena;
     p.arena_cap = c->arena_cap;
+    p.counter_bias = c->counter_bias;
+    if (c->counter_bias && n_str) {
+        // test-only: the arena and far-pair counters start this call at the bias (the previous call's reset
+        // left them 0), so the kernels' offsets have a low word >= 2^31 without a 40-GiB arena; the far
+        // list is passed down shifted by as many pairs
+        const uint64_t b = c->counter_bias;
+        uint32_t *ctr = c->retry_count;
+        for (unsigned w : {8u, 12u}) {   // (uint64 counters 4 and 6: the arena's claimed bytes, the far pairs)
+            hipError_t e0 = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ctr + w), (int)(uint32_t)b, 1, st);
+            if (e0 == hipSuccess) e0 = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ctr + w + 1), (int)(uint32_t)(b >> 32), 1, st);
+            if (e0 != hipSuccess) return hip_fail(e0, "counter bias");
+        }
+        if (p.far) {
+            p.far = reinterpret_cast<uint64_t *>(reinterpret_cast<uintptr_t>(p.far) - 16 * b);
+            p.far_cap = far_cap + b;
+        }
+    }
     p.variant = kernel_variant(v->stats.max_cp);
     // int16 staging when every id fits in 0..32767 (half the staging traffic)
     p.staging16 = v->ids16 ? c->staging16 : nullptr;
@@ -790,6 +819,7 @@ static int encode_host_impl(dpt_ctx *c, const dpt_vocab *v, int mode, const uint
         if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_fail(e, "sync");
         uint64_t used = 0;
         if (n_str) memcpy(&used, c->p_out + o_ctr + 40, sizeof(used));   // the call's claimed bytes (finish_kernel)
+        if (n_str) used -= c->counter_bias;   // (test-only dpt_ctx_debug_counter_bias)
         if (used > n_bytes) return fail(DPT_E_HIP, "unbounded pass counter out of range");   // never expected
         if (used <= c->arena_cap) break;
         // the unbounded pass's arena was too small for the strings routed to it (those strings got
@@ -808,6 +838,7 @@ static int encode_host_impl(dpt_ctx *c, const dpt_vocab *v, int mode, const uint
     uint64_t nf = 0;
     if (want_far) {
         if (n_str) memcpy(&nf, c->p_out + o_ctr + 56, sizeof(nf));   // the call's far edge pairs (finish_kernel)
+        if (n_str) nf -= c->counter_bias;
         if (n_far) *n_far = nf;
         if (nf > far_cap) return fail(DPT_E_CAP, "far edge list overflow (*n_far holds the pairs needed)");
     }

@@ -51,6 +51,7 @@ struct EncodeLaunch {
     bool hist_overwrite;     // DPT_HIST_OVERWRITE: the call's histogram replaces hist (zeroed on the device first)
     uint8_t *arena;          // the unbounded pass's scratch: 20 bytes per input byte of the strings it takes
     uint64_t arena_cap;      // input bytes the arena holds
+    uint64_t counter_bias;   // test-only (dpt_ctx_debug_counter_bias): the arena and far-pair counters start at it
     // vocabulary
     const int2 *slots;
     const int32_t *slot_ids;
@@ -102,9 +103,11 @@ __host__ __device__ inline unsigned child_bit(unsigned b) { return (b ^ (b >> 5)
 // it after the A0 table in the pair16 allocation).  Key: the token's bytes as four little-endian
 // dwords, zero past its length, plus the length.  Buckets of two {fp, id} entries (fp != 0; 0 marks a
 // free entry), two choices per key (cuckoo placement, round 5): bucket h & mask or its partner
-// tokhash_alt(h & mask, fp), both loaded at once -- a lookup never walks a probe chain (with linear
-// probing 5.7 % of cfg4's hashed tokens were not in their home bucket, and almost every 64-token round
-// ran the serial probe loop for some lane).  The builder checks that the first entry carrying a key's
+// tokhash_alt(h & mask, fp).  The kernels load a key's home bucket first and its partner only when the
+// key is not in its home bucket (one more load round for the wave, never a chain; DPT_HASH_BOTH=1 in
+// dpt_kernels.hip loads both at once -- measured slower on cfg2 / cfg5, round 5 r05aj) -- a lookup never
+// walks a probe chain (with linear probing 5.7 % of cfg4's hashed tokens were not in their home bucket,
+// and almost every 64-token round ran the serial probe loop for some lane).  The builder checks that the first entry carrying a key's
 // fp among its two buckets (in the kernel's order) is its own (else it re-seeds): a span the DP
 // selected is a vocabulary token by construction (phase A matched it), so the lookup needs no key
 // compare.
@@ -172,6 +175,7 @@ struct LongLaunch {
     int16_t *staging16;      // as EncodeLaunch: the final ids go here instead when non-null
     uint8_t *arena;          // scratch: uint4 rec[arena_cap] then int32 stg[arena_cap], per string at its
     uint64_t arena_cap;      //   claimed offset (input bytes; 20 bytes of scratch per input byte)
+    uint64_t arena_bias;     // test-only: the arena counter starts at it (the kernel's offsets >= bias)
     unsigned long long *arena_used;   // claimed input bytes (all long strings; > arena_cap: overflow)
     uint64_t *counts;
     int32_t *status;

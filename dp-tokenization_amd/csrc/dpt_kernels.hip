@@ -281,7 +281,8 @@ struct SlotState {
     uint32_t abase;
     uint16_t wlen, n_atoms, n_words;
     uint8_t active, status, inval, capb;   // capb: some atom of the window is not a token by itself (the cap can bind)
-    uint8_t pad[2];
+    uint8_t cpw;   // a '\u2581'-compressed PRESPLIT window (prep_window): raw mode's ASCII paths, no first-atom rule
+    uint8_t pad;
 };
 static_assert(sizeof(SlotState) == 48, "slot state layout");
 
@@ -386,6 +387,18 @@ __device__ unsigned long long g_stamps[10];
 #define STAMP_DECL
 #define STAMP(k)
 #define STAMP_FLUSH
+#endif
+#ifdef DPT_WSTAMPS
+// diagnostic build only (its own library, no phase stamps): the first pass's per-wave timeline (tools/wave_timeline.py): per wave (blockIdx), [0] its first
+// instruction, [1 + k] the end of its k-th slot round (| the round's busy slots << 56), [WST_N - 1] its exit
+// (| its rounds << 48); s_memrealtime (100 MHz, one clock for the whole chip)
+constexpr unsigned WST_MAXW = 8192, WST_N = 128;
+__device__ unsigned long long g_wst[WST_MAXW * WST_N];
+#define WST_REC(k, v) do { if (!BIG && lane == 0 && bid < WST_MAXW && (unsigned)(k) < WST_N) g_wst[(size_t)bid * WST_N + (k)] = (v); } while (0)
+#define WST_NOW() ((unsigned long long)__builtin_amdgcn_s_memrealtime())
+#else
+#define WST_REC(k, v)
+#define WST_NOW() 0ull
 #endif
 
 // Phase A's per-atom descriptor: byte offset | byte length << PB | "a word or the window ends
@@ -640,12 +653,17 @@ __device__ bool window_bounds(const WinRegs<CH> &W, uint64_t slen, uint64_t pos,
 // Atomise window bytes [pos, pos+wlen) into L: the bytes themselves, atom byte offsets,
 // code-point prefixes (+ word-start bits) and the word list.  One packed DPP scan per 256
 // bytes.  Returns false if an atom is longer than MAX_ATOM_BYTES (4 bytes in RAW mode).
+// cpw_o: 1 when the window was stored '\u2581'-compressed (PRESPLIT, 16-lane first pass; below).
 template <int CH, int G, bool WIDE>
 __device__ bool prep_window(GroupLDS<CH, G> &L, uint8_t *gw, const WinRegs<CH> &W, uint64_t pos,
-                            unsigned wlen, int mode, unsigned lane, unsigned &n_atoms_o, unsigned &n_words_o) {
+                            unsigned wlen, int mode, unsigned lane, unsigned &n_atoms_o, unsigned &n_words_o,
+                            unsigned &cpw_o) {
     const bool raw = mode == 0;
     unsigned n_atoms = 0, cp_tot = 0, n_words = 0;
     bool hi_byte = false;   // some byte >= 0x80: atoms may be longer than one byte
+    bool ast0[4] = {false, false, false, false};   // (256-byte windows: the lane's atom starts and atom indices)
+    unsigned aiu0[4] = {0, 0, 0, 0};
+    cpw_o = 0;
 #pragma unroll
     for (int c = 0; c < CH / 256; c++) {
         const unsigned c0 = c * 256u;
@@ -706,6 +724,9 @@ __device__ bool prep_window(GroupLDS<CH, G> &L, uint8_t *gw, const WinRegs<CH> &
                 cp += cpl[u];
             }
         }
+        if (c == 0)
+#pragma unroll
+            for (int u = 0; u < 4; u++) { ast0[u] = ast[u]; aiu0[u] = aiu[u]; }
         // (the 256-byte pass's word list lives in global scratch and is needed only by row-mode
         // windows: C0 rebuilds it there -- a store here would hold phase A's first loads back)
         if constexpr (!GroupLDS<CH, G>::WSLG) {
@@ -728,6 +749,53 @@ __device__ bool prep_window(GroupLDS<CH, G> &L, uint8_t *gw, const WinRegs<CH> &
     n_atoms_o = n_atoms;
     n_words_o = n_words;
     wave_sync();
+    // PRESPLIT windows of llama mode's words (reference tokenizer_utils.py:24-31: SentencePiece pieces merged
+    // by merge_tokens, every word after the BOS one starting with '\u2581' = E2 96 81): when the window's only
+    // non-ASCII bytes are such '\u2581's, each exactly at a word start, every word start after byte 0 is one,
+    // and no literal ' ' or '\n' is in it, the window is a raw-mode window in disguise -- '\u2581' then a
+    // word, as raw mode's ' ' is.  It is stored compressed: atom j's byte at bytes[j] ('\u2581' as ' '),
+    // aoff[j] = j; the rest of the first pass runs raw mode's ASCII paths on it (A0, the ASCII walker,
+    // C2's bulk and hash passes with the ' ' -> '\u2581' expansion) without raw mode's first-atom rule
+    // (SlotState::cpw).  Other PRESPLIT windows keep the generic path.
+    if constexpr (G == 16 && CH == 256 && !WIDE) {
+        if (mode == 1 && n_atoms > 0) {
+            const uint32_t *b32 = reinterpret_cast<const uint32_t *>(L.bytes);
+            const uint32_t w0 = b32[lane], w1 = b32[lane + 1u];   // (past the window: masked by wlen below)
+            const uint32_t n1w = __builtin_amdgcn_alignbyte(w1, w0, 1u), n2w = __builtin_amdgcn_alignbyte(w1, w0, 2u);
+            const uint32_t cmw = W.c[0];
+            unsigned bad = 0, cnt = 0;   // cnt: bytes >= 0x80 | '\u2581's << 16
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const unsigned k = 4u * lane + (unsigned)u;
+                const unsigned in = (unsigned)(k < wlen);
+                const unsigned b = (w0 >> (8 * u)) & 0xFFu, n1 = (n1w >> (8 * u)) & 0xFFu, n2 = (n2w >> (8 * u)) & 0xFFu;
+                const unsigned c = (cmw >> (8 * u)) & 0xFFu;
+                const unsigned bar = in & (unsigned)(k + 2u < wlen) & (unsigned)(b == 0xE2u) & (unsigned)(n1 == 0x96u) &
+                                     (unsigned)(n2 == 0x81u);
+                const unsigned ws = in & (unsigned)(k > 0u) & (unsigned)(c != 0u) & (unsigned)((b & 0xC0u) != 0x80u);
+                bad |= in & ((unsigned)(b == 0x20u) | (unsigned)(b == 0x0Au));
+                bad |= ws & (bar ^ 1u);
+                bad |= bar & (unsigned)(k > 0u) & (unsigned)(c == 0u);
+                cnt += (in & (b >> 7)) | (bar << 16);
+            }
+            const unsigned tot = __builtin_amdgcn_readlane(wave_incl_scan_add(cnt), 63);
+            if (!ballot(bad != 0u) && (tot & 0xFFFFu) == 3u * (tot >> 16)) {
+                wave_sync();   // (every lane has read the bytes it tested)
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    if (ast0[u]) {
+                        const unsigned b = (W.t[0] >> (8 * u)) & 0xFFu;
+                        L.bytes[aiu0[u]] = (uint8_t)(b == 0xE2u ? 0x20u : b);
+                        L.aoff[aiu0[u]] = (typename GroupLDS<CH, G>::Idx)aiu0[u];
+                    }
+                }
+                if (lane == 0) L.aoff[n_atoms] = (typename GroupLDS<CH, G>::Idx)n_atoms;
+                wave_sync();
+                cpw_o = 1;
+                return true;   // (atoms of one byte each)
+            }
+        }
+    }
     // per-atom walk descriptor for phase A (parked in fin[], which phase B overwrites):
     //   byte offset | byte length << 12 | "a word or the window ends after it" << 16 | "first atom of the string" << 17
     const unsigned lim = WIDE ? MAX_ATOM_BYTES : 4u;   // RAW / PRESPLIT: code points (and '▁' + one fits 8 bytes)
@@ -837,8 +905,8 @@ __device__ __forceinline__ TrieView tv_of(ConstKernArgs *kp) {
 // Counter block (EncodeLaunch::retry_count, CTR_ALLOC_BYTES; zeroed once at allocation, then reset for
 // the next call by the batch scan or the finish pass -- or, in a one-string host-path call, by the lone
 // wave of the first pass): uint32 [0] retry count, [1] 2048-byte blocks done (fallback_kernel), [2]
-// 2048-byte pass work, [3] long count, [4] long work, [5] unused, [6] fallback_kernel's
-// block ticket; uint64 [4] (byte
+// 2048-byte pass work, [3] long count, [4] long work, [5] the 512-byte pass's work (mid_kernel), [6]
+// fallback_kernel's block ticket, [7] the 2048-byte pass's list count when the 512-byte pass ran; uint64 [4] (byte
 // 32) the unbounded pass's claimed bytes, [5] (byte 40) the last call's claimed bytes
 // (dpt_ctx_long_need), [6] (byte 48) far edge pairs found, [7] (byte 56) the last call's far edge pairs
 // (dpt_dp_host_far); from byte PART_CTR_OFFSET the first pass's partition counters and their used-up
@@ -857,7 +925,7 @@ __device__ __forceinline__ void reset_counters(uint32_t *ctr, uint64_t *snap = n
     c64[CTR_FAR64] = 0;
     if (snap)
         for (unsigned q = 0; q < 8; q++) snap[q] = c64[q];
-    ctr[0] = 0; ctr[1] = 0; ctr[2] = 0; ctr[3] = 0; ctr[4] = 0; ctr[5] = 0; ctr[6] = 0;
+    ctr[0] = 0; ctr[1] = 0; ctr[2] = 0; ctr[3] = 0; ctr[4] = 0; ctr[5] = 0; ctr[6] = 0; ctr[7] = 0;
     uint32_t *pc = ctr + PART_CTR_OFFSET / 4;
     for (unsigned q = 0; q <= NPART; q++) pc[q * PART_STRIDE] = 0;   // the partition counters and the mask
 }
@@ -917,8 +985,15 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
     unsigned n_pend = 0;   // 16-lane first pass: residual tokens waiting in the wave's pending row
     // one claim of up to req strings (uniform): partition-local [nb, ne) of partition cp, possibly
     // empty once every partition is used up
+#ifdef DPT_WSTAMPS
+    unsigned wst_claims = 0;
+#define WST_CLAIM() (wst_claims++)
+#else
+#define WST_CLAIM()
+#endif
     auto claim = [&](unsigned req, uint64_t &nb, uint64_t &ne, unsigned &cp) {
         for (;;) {
+            WST_CLAIM();
             uint32_t *ctr = BIG ? a.work_next : a.part_ctr + part * PART_STRIDE;
             const uint64_t hi = BIG ? n_work : part_size((unsigned)n_work, npart, part);
             unsigned b = 0;
@@ -964,13 +1039,15 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
     // per expanded byte from one call site -- starting at the node after '\u2581' when the token
     // starts with it; the id of the node reached when every step's check held, else -1.  Entry:
     // staging element (.x, .y bits 0..15), byte length (.y bits 16..23, <= 8), first atom of the
-    // string (.y bit 24), the bytes (.z, .w).
+    // string (.y bit 24), raw mode's expansions (.y bit 25: raw mode, or a '\u2581'-compressed PRESPLIT
+    // window), the bytes (.z, .w).
     auto walk_pending = [&](unsigned P) {
         wave_sync();   // the entries other lanes stored
         if (lane < P) {
             const uint4 e = a.pend[(uint64_t)bid * 64u + lane];
             const uint64_t out = (uint64_t)e.x | ((uint64_t)(e.y & 0xFFFFu) << 32);
             const unsigned len = (e.y >> 16) & 0xFFu;
+            const bool raw = RAW || ((e.y >> 25) & 1u);   // (shadows the mode's: this token's bytes)
             const bool fi = raw && ((e.y >> 24) & 1u);
             const uint64_t by = (uint64_t)e.z | ((uint64_t)e.w << 32);
             const unsigned b0 = (unsigned)(by & 0xFFu);
@@ -1006,6 +1083,8 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
     };
 
     STAMP_DECL
+    WST_REC(0, WST_NOW());
+    [[maybe_unused]] unsigned wst_it = 0;
 
     if (lane < (unsigned)NG) SSr(lane).active = 0;
     wave_sync();
@@ -1073,12 +1152,12 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                 SlotState &S = SSr(g);
                 const uint64_t slen = uni64(S.slen), pos = uni64(S.pos);
                 unsigned status = uni(S.status);
-                unsigned wlen = 0, na = 0, nw = 0;
+                unsigned wlen = 0, na = 0, nw = 0, cpw = 0;
                 bool ok = status != 2;
                 if (ok) ok = window_bounds<CH>(W[g], slen, pos, mode, lane, wlen);
-                if (ok) ok = prep_window<CH, G, WIDE>(L, wsl_of(g), W[g], pos, wlen, mode, lane, na, nw);
+                if (ok) ok = prep_window<CH, G, WIDE>(L, wsl_of(g), W[g], pos, wlen, mode, lane, na, nw, cpw);
                 if (ok) {
-                    if (lane == 0) { S.wlen = wlen; S.n_atoms = na; S.n_words = nw; S.wtok = 0; S.inval = 0; S.capb = 0; }
+                    if (lane == 0) { S.wlen = wlen; S.n_atoms = na; S.n_words = nw; S.wtok = 0; S.inval = 0; S.capb = 0; S.cpw = (uint8_t)cpw; }
                     prepared |= 1u << g;
                     busy++;
                     continue;
@@ -1089,8 +1168,9 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                 if (lane == 0) {
                     const uint64_t s = S.s;
                     if (status == 3) {
-                        uint32_t *cnt = BIG ? a.long_count : a.retry_count;
-                        uint32_t *lst = BIG ? a.long_list : a.retry_list;
+                        // (the 512-byte pass, mid_kernel: its retry_* fields are the 2048-byte pass's list)
+                        uint32_t *cnt = (BIG && CH > 512) ? a.long_count : a.retry_count;
+                        uint32_t *lst = (BIG && CH > 512) ? a.long_list : a.retry_list;
                         lst[atomicAdd(cnt, 1u)] = (uint32_t)s;
                     }
                     a.status[s] = (int32_t)status;
@@ -1120,7 +1200,11 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
             unsigned a0mask = 0;
             uint32_t mark = 0;
             if constexpr (G == 16 && !BIG) {
-                if (raw) {
+                if (!raw) {   // PRESPLIT: the '\u2581'-compressed windows (prep_window)
+#pragma unroll
+                    for (int g = 0; g < NG; g++)
+                        if (uni(SSr(g).n_atoms) > 0 && uni(SSr(g).cpw)) a0mask |= 1u << g;
+                } else {
 #pragma unroll
                     for (int g = 0; g < NG; g++) {
                         const unsigned wl = uni(SSr(g).n_atoms) > 0 ? uni(SSr(g).wlen) : 0u;
@@ -1137,7 +1221,7 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
             for (int g = 0; g < NG; g++) nstart[g] = uni(SSr(g).n_atoms);
             unsigned fwmask = 0;   // slots whose window starts the string (raw: '▁' + first atom)
 #pragma unroll
-            for (int g = 0; g < NG; g++) fwmask |= (uni(SSr(g).pos) == 0 ? 1u : 0u) << g;
+            for (int g = 0; g < NG; g++) fwmask |= (raw && uni(SSr(g).pos) == 0 ? 1u : 0u) << g;
             // One walk per lane.  Walk state: start atom j, the LDS byte offset of its slot's group,
             // atoms matched so far (len), the trie node, the expanded bytes left of the current atom
             // (seq, cnt) and its descriptor (info).  Finished walks take the next start (ballot +
@@ -1195,8 +1279,9 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
 #pragma unroll
                     for (int g = 0; g < NG; g++) {
                         if (!((a0mask >> g) & 1u)) continue;
-                        const unsigned wl = uni(SSr(g).wlen);
-                        const bool first = uni(SSr(g).pos) == 0;
+                        // (window bytes in LDS = atoms: raw ASCII windows and '\u2581'-compressed ones alike)
+                        const unsigned wl = uni(SSr(g).n_atoms);
+                        const bool first = raw && uni(SSr(g).pos) == 0;
                         const unsigned gbase = (unsigned)g * GSTR;
                         const uint32_t *b32 = reinterpret_cast<const uint32_t *>(grp(g).bytes);
                         const unsigned k0 = 4u * lane;
@@ -1427,7 +1512,7 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                         const GL &L = *reinterpret_cast<const GL *>(smem + fl);
                         const unsigned jj = L.fin[uu - base].v;
                         fj = jj;
-                        fwl = SSr(gs).wlen;
+                        fwl = SSr(gs).n_atoms;   // (= the LDS bytes: one per atom)
                         const unsigned b0 = L.bytes[jj];
                         isr = 0; one = 0; pc = 0;
                         if (((fwmask >> gs) & 1u) && jj == 0) {   // '\u2581' + b0: one atom
@@ -2183,7 +2268,11 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                     if (!raw && L.scf[j]) {
                         // a word that is one token (phase A's whole-word shortcut): only that edge, whose key
                         // (cost 1) is final at the word end; its inner positions are never read (C0/C1 read
-                        // word ends, C1 walks from them; no cut lies inside the word)
+                        // word ends, C1 walks from them; no cut lies inside the word).  Sound only because
+                        // (1) every window ends at a word start or the string's end (window_bounds), so the
+                        // BF_STOP the byte-stream walker stopped on is the word's real end, not a window cut
+                        // through it, and (2) that walker never steps past a BF_STOP; a change to either
+                        // must revisit this (tests/test_gpu_parity.py::test_bloom_words_across_windows)
                         const unsigned dd = 63u - (unsigned)__builtin_clzll(sm);   // the longest token from j
                         uint2 f = fin2[j + 1u + dd];
                         upd(f, dd);
@@ -2392,14 +2481,16 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
             unsigned pre[NG + 1], na_g[NG];
             uint64_t obase[NG];       // staging element of the window's first token, per slot
             const bool n16 = SW == 1 || (SW == 0 && a.staging16 != nullptr);   // int16 staging (uniform)
-            unsigned firstmask = 0;   // groups whose window starts the string (raw '▁' + first atom)
+            // per slot, bit 0: the window starts the string (raw '▁' + first atom); bit 1: a '\u2581'-compressed
+            // PRESPLIT window (its ' ' bytes expand to '\u2581' as raw mode's do)
+            unsigned firstmask = 0;
             pre[0] = 0;
 #pragma unroll
             for (int g = 0; g < NG; g++) {
                 const bool gv = !len_only && uni(SSr(g).inval) == 0 && uni(SSr(g).status) == 0 && uni(SSr(g).n_atoms) > 0;
                 pre[g + 1] = pre[g] + (gv ? uni(SSr(g).wtok) : 0u);
                 na_g[g] = uni(SSr(g).n_atoms);
-                firstmask |= (uni64(SSr(g).pos) == 0 ? 1u : 0u) << g;
+                firstmask |= ((raw && uni64(SSr(g).pos) == 0 ? 1u : 0u) | (uni(SSr(g).cpw) ? 2u : 0u)) << (2 * g);
                 const uint64_t e0 = uni64(SSr(g).sb) + uni(SSr(g).ntok);
                 obase[g] = e0;
             }
@@ -2418,7 +2509,7 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
 #pragma unroll
                 for (int g = 0; g < NG; g++) {
                     C2Slot &q = *reinterpret_cast<C2Slot *>(&grp(g).fin[0]);
-                    q.base = pre[g]; q.ntk = pre[g + 1] - pre[g]; q.na = na_g[g]; q.fw = (firstmask >> g) & 1u; q.ob = obase[g];
+                    q.base = pre[g]; q.ntk = pre[g + 1] - pre[g]; q.na = na_g[g]; q.fw = (firstmask >> (2 * g)) & 3u; q.ob = obase[g];
                 }
             }
             wave_sync();
@@ -2478,13 +2569,13 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                         const unsigned j1 = k + 1 < q.ntk ? nx : q.na;
                         const unsigned p0 = L.aoff[jj];
                         const unsigned nbytes = (typename GL::Idx)(L.aoff[j1] - p0);
-                        const unsigned fa = (raw ? 1u : 0u) & q.fw & (unsigned)(jj == 0);
+                        const unsigned fa = q.fw & 1u & (unsigned)(jj == 0);   // (bit 0: raw mode only)
                         uint32_t h = 0, fp = 0;
                         bool hashed;
                         if constexpr (G == 16) {
                             uint32_t w[4];
                             unsigned E = 0;
-                            hashed = in && token_key<CH>(L.bytes, p0, nbytes, raw, fa, w, E);
+                            hashed = in && token_key<CH>(L.bytes, p0, nbytes, raw || (q.fw >> 1) != 0u, fa, w, E);
                             if (hashed) tokhash(w[0], w[1], w[2], w[3], E, hh.seed, h, fp);
                         } else {   // 64-lane rows (BLOOM-scale vocabularies): keys of up to 64 bytes
                             hashed = in && token_hash_long<CH>(L.bytes, p0, nbytes, raw, fa, hh.seed, h, fp);
@@ -2569,9 +2660,10 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                         const uint32_t *w = reinterpret_cast<const uint32_t *>(L.bytes) + (p0 >> 2);
                         const unsigned two = __builtin_amdgcn_alignbyte(w[1], w[0], p0 & 3u);
                         const unsigned b0 = two & 0xFFu, b1 = (two >> 8) & 0xFFu;
-                        // raw mode expands ' ' (a word start), '\n' and the string's first atom
-                        const unsigned expd = (raw ? 1u : 0u) &
-                                              ((unsigned)(b0 == ' ') | (unsigned)(b0 == '\n') | (q.fw & (unsigned)(jj == 0)) |
+                        // raw mode (and '\u2581'-compressed PRESPLIT windows, q.fw bit 1) expands ' ' (a word start),
+                        // '\n' and the string's first atom
+                        const unsigned expd = ((raw ? 1u : 0u) | (q.fw >> 1)) &
+                                              ((unsigned)(b0 == ' ') | (unsigned)(b0 == '\n') | (q.fw & 1u & (unsigned)(jj == 0)) |
                                                ((unsigned)(nbytes == 2u) & ((unsigned)(b1 == ' ') | (unsigned)(b1 == '\n'))));
                         const unsigned bulk = (unsigned)in & (unsigned)(nbytes - 1u <= 1u) & (expd ^ 1u);
                         if constexpr (SW == 1)   // int16 ids: the 128-KB pair table (L1-resident for ASCII)
@@ -2640,11 +2732,13 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                         const unsigned j1 = k + 1 < q.ntk ? nx : q.na;
                         const unsigned p0 = L.aoff[jj];
                         const unsigned len = (uint8_t)(L.aoff[j1] - p0);
-                        const unsigned fi = (raw ? 1u : 0u) & q.fw & (unsigned)(jj == 0);
+                        const unsigned fi = q.fw & 1u & (unsigned)(jj == 0);
+                        const unsigned rl = (raw ? 1u : 0u) | (q.fw >> 1);   // raw mode's expansions
                         lng = len > 8u;
                         const uint64_t by = load_bytes(L.bytes, p0, lng ? 8u : len);
                         const uint64_t out = q.ob + k;
-                        ent = make_uint4((uint32_t)out, ((uint32_t)(out >> 32) & 0xFFFFu) | (len << 16) | (fi << 24), (uint32_t)by, (uint32_t)(by >> 32));
+                        ent = make_uint4((uint32_t)out, ((uint32_t)(out >> 32) & 0xFFFFu) | (len << 16) | (fi << 24) | (rl << 25),
+                                         (uint32_t)by, (uint32_t)(by >> 32));
                     }
                     if (!ballot(lng)) {
                         if (n_pend + r > (unsigned)PEND_CAP) {
@@ -2673,6 +2767,7 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                 unsigned jj, j1, cnt, lbase;
                 uint64_t seq;
                 uint64_t out;
+                bool rl;   // raw mode's expansions (raw mode, or a '\u2581'-compressed PRESPLIT window)
             };
             auto tstart = [&](unsigned t) -> Tok {
                 Tok T;
@@ -2686,7 +2781,8 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                 T.jj = (unsigned)L.rec[k].smask;
                 const unsigned nx = (unsigned)L.rec[k + 1].smask;   // k + 1 <= ntk < NA
                 T.j1 = k + 1 < q.ntk ? nx : q.na;
-                T.seq = atom_from_info<CH, WIDE>(L.bytes, AInfo<CH>::pack(L.aoff[T.jj], L.atom_len(T.jj), 0, (raw ? 1u : 0u) & q.fw & (unsigned)(T.jj == 0)), raw, T.cnt);
+                T.rl = raw || (q.fw >> 1) != 0u;
+                T.seq = atom_from_info<CH, WIDE>(L.bytes, AInfo<CH>::pack(L.aoff[T.jj], L.atom_len(T.jj), 0, q.fw & 1u & (unsigned)(T.jj == 0)), T.rl, T.cnt);
                 T.out = q.ob + k;
                 return T;
             };
@@ -2700,7 +2796,7 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
 #pragma unroll
             for (int w = 0; w < NW; w++) {
                 active[w] = wbeg + lane + 64u * w < wend;
-                C[w].jj = C[w].j1 = C[w].cnt = C[w].lbase = 0; C[w].seq = 0; C[w].out = 0;
+                C[w].jj = C[w].j1 = C[w].cnt = C[w].lbase = 0; C[w].seq = 0; C[w].out = 0; C[w].rl = raw;
                 if (active[w]) C[w] = tstart(tok_at(wbeg + lane + 64u * w));
                 node[w] = 0; nb[w] = tv.root_base; ok[w] = true;
             }
@@ -2729,7 +2825,7 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                     if (aend & (dn ^ 1u)) {
                         C[w].jj++;
                         const GL &L = *reinterpret_cast<const GL *>(smem + C[w].lbase);
-                        C[w].seq = atom_from_info<CH, WIDE>(L.bytes, AInfo<CH>::pack(L.aoff[C[w].jj], L.atom_len(C[w].jj), 0, 0), raw, C[w].cnt);
+                        C[w].seq = atom_from_info<CH, WIDE>(L.bytes, AInfo<CH>::pack(L.aoff[C[w].jj], L.atom_len(C[w].jj), 0, 0), C[w].rl, C[w].cnt);
                     }
                 }
                 // ---- the trie steps; finished walks write their id and take the next token
@@ -2785,6 +2881,8 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
         wave_sync();
         STAMP(4);
         STAMP(8);
+        WST_REC(1 + min(wst_it, WST_N - 4), WST_NOW() | ((unsigned long long)busy << 56));
+        wst_it++;
     }
     if constexpr (G == 16 && !BIG)
         if (n_pend) {
@@ -2797,6 +2895,10 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
     }
     STAMP(9);
     STAMP_FLUSH;
+    WST_REC(WST_N - 1, WST_NOW() | ((unsigned long long)wst_it << 48));
+#ifdef DPT_WSTAMPS
+    WST_REC(WST_N - 2, wst_claims);
+#endif
 #undef a
 #undef tv
 }
@@ -3148,6 +3250,7 @@ __global__ void __launch_bounds__(HIST_THREADS) hist_kernel(const uint64_t *__re
 // ------------------------------------------------------------------ the fallback passes in one launch
 
 constexpr int SMALL_CH = 256;   // the first pass's window
+constexpr int MID_CH = 512;     // the 512-byte pass's (PRESPLIT / ATOMS calls of 16-lane vocabularies)
 constexpr int BIG_CH = 2048;    // the 2048-byte pass's
 
 // The 2048-byte pass and the unbounded pass as ONE launch (they used to be two, ~5 us each on every call
@@ -3205,6 +3308,18 @@ __global__ void __launch_bounds__(64) fallback_kernel(FallbackArgs fa) {
 static_assert(block_lds_bytes<SMALL_CH, 16>() <= 64 * 1024, "small LDS");
 static_assert(block_lds_bytes<SMALL_CH, 64>() <= 64 * 1024, "small LDS");
 static_assert(block_lds_bytes<BIG_CH, 64>() <= 160 * 1024, "big LDS");
+static_assert(block_lds_bytes<MID_CH, 16>() <= 64 * 1024, "mid LDS");
+
+// The 512-byte pass (PRESPLIT / ATOMS calls, 16-lane vocabularies): the first pass's retry list -- strings
+// with a word of 257..512 bytes, which marker bytes make common there (cfg2p: a 256-character word plus
+// its '\u2581' is 257 code points) -- four strings per wave in 16-lane rows like the first
+// pass (the generic walker, C2's hash pass and walkers: no A0 / bulk pass), ~7 waves per CU (LDS); its own
+// failures go on to the 2048-byte pass.  A persistent grid over the list: with no retries every wave reads
+// a zero count and exits.
+template <int SW, bool WIDE>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) mid_kernel(KernArgs ka) {
+    tokenize_body<MID_CH, 16, true, WIDE, SW, false>(blockIdx.x);
+}
 
 constexpr int MAX_DEVICES = 64;
 // Resident waves per CU for an instantiation (LDS / VGPR limited); DPT_WAVES_PER_CU overrides.
@@ -3305,13 +3420,15 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     if (p.n_str > 0) {
         {
             const unsigned n_cu = p.max_blocks / 64;
+            // A/B knob (diagnostic): raw mode through the generic 16-lane kernel (r06i: cfg2 +9 %, cfg4 +7 %)
+            static const bool generic_raw = getenv("DPT_GENERIC_RAW") != nullptr;
             if (p.variant == KERNEL_ROWS16) {
                 // the hot kernel gets the staged id width as a template constant
                 const uint64_t nu = (p.n_str + 3) / 4;
                 if (wide) {
                     if (st16) launch_tok<SMALL_CH, 16, false, true, 1>(a, tv, nu, n_cu, stream, e0);
                     else launch_tok<SMALL_CH, 16, false, true, 2>(a, tv, nu, n_cu, stream, e0);
-                } else if (raw) {
+                } else if (raw && !generic_raw) {
                     if (st16) launch_tok<SMALL_CH, 16, false, false, 1, true>(a, tv, nu, n_cu, stream, e0);
                     else launch_tok<SMALL_CH, 16, false, false, 2, true>(a, tv, nu, n_cu, stream, e0);
                 } else {
@@ -3333,6 +3450,31 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
         EncodeArgs b = a;
         b.work_list = p.retry_list; b.work_count = p.retry_count;
         b.work_next = p.retry_count + 2;
+        static const bool mid_on = getenv("DPT_NO_MID") == nullptr;   // (A/B: the 512-byte pass off)
+        if (!raw && p.variant == KERNEL_ROWS16 && mid_on) {
+            // the 512-byte pass over the retry list; the strings it cannot hold go on to the 2048-byte pass
+            EncodeArgs m = a;
+            m.work_list = p.retry_list; m.work_count = p.retry_count; m.work_next = p.retry_count + 5;
+            m.retry_list = p.retry_list + 2 * p.n_str; m.retry_count = p.retry_count + 7;
+            m.hist_zero = nullptr; m.n_hist = 0;
+            static unsigned mid_per_cu[MAX_DEVICES] = {};
+            int dev = 0;
+            if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAX_DEVICES) dev = 0;
+            if (!mid_per_cu[dev]) {
+                int nb = 0;
+                if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, st16 ? (wide ? mid_kernel<1, true> : mid_kernel<1, false>)
+                                                                            : (wide ? mid_kernel<2, true> : mid_kernel<2, false>),
+                                                                 64, block_lds_bytes<MID_CH, 16>()) != hipSuccess || nb <= 0)
+                    nb = 4;
+                mid_per_cu[dev] = (unsigned)nb;
+            }
+            uint64_t mb = (uint64_t)(p.max_blocks / 64) * mid_per_cu[dev];
+            mb = mb < p.n_str ? mb : p.n_str;
+            constexpr int mlds = block_lds_bytes<MID_CH, 16>();
+            auto mk = st16 ? (wide ? mid_kernel<1, true> : mid_kernel<1, false>) : (wide ? mid_kernel<2, true> : mid_kernel<2, false>);
+            hipLaunchKernelGGL(mk, dim3((unsigned)(mb ? mb : 1)), dim3(64), mlds, stream, KernArgs{m, tv});
+            b.work_list = m.retry_list; b.work_count = m.retry_count;
+        }
         if (!p.padded && fin_fold(p.n_str) && p.hist && p.hist_overwrite && p.hist_bins >= 2 &&
             p.hist_bins <= FIN_MAX_BINS) {
             b.hist_zero = reinterpret_cast<unsigned long long *>(p.hist);   // (the finish pass adds to it)
@@ -3343,6 +3485,14 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
         constexpr unsigned FALLBACK_DIV = 4;
         // (n_units caps the grid: one block per FALLBACK_DIV CUs; the retry list is rare and short)
         uint64_t fb_units = (uint64_t)(p.max_blocks / 64) / FALLBACK_DIV;
+        // PRESPLIT / ATOMS text carries its word markers as bytes ('\u2581' is 3 of them), so a word the
+        // 256-byte window cannot hold is not rare there (cfg2p: the 6.8 % of 256-character strings without a
+        // space are one 257-code-point word after the dummy prefix): a full grid of 2048-byte blocks (three
+        // per CU: LDS) takes them, instead of one block per four CUs (DPT_FB_BIG_PER_CU overrides)
+        {
+            static const int per_cu = getenv("DPT_FB_BIG_PER_CU") ? atoi(getenv("DPT_FB_BIG_PER_CU")) : 3;
+            if (!raw && per_cu > 0) fb_units = (uint64_t)(p.max_blocks / 64) * (uint64_t)per_cu;
+        }
         fb_units = fb_units < p.n_str ? fb_units : p.n_str;
         // (skipped when the host showed no string needs them -- small host-path calls: two dispatches
         // of a per-string dp_tokenize call -- unless they time the call or zero its histogram)
@@ -3352,7 +3502,7 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
         LongLaunch l;
         l.mode = p.mode; l.text = p.text; l.str_off = p.str_off; l.cut_mask = p.cut_mask;
         l.staging = p.staging; l.staging16 = p.staging16; l.counts = p.counts; l.bsum = p.padded ? nullptr : p.flags; l.status = p.status; l.capped = p.capped;
-        l.arena = p.arena; l.arena_cap = p.arena_cap;
+        l.arena = p.arena; l.arena_cap = p.arena_cap; l.arena_bias = p.counter_bias;
         l.arena_used = reinterpret_cast<unsigned long long *>(p.retry_count + 8);
         l.edges = p.edges; l.far = p.far; l.far_cap = p.far_cap;
         l.far_count = reinterpret_cast<unsigned long long *>(p.retry_count) + CTR_FAR64;
@@ -3472,6 +3622,19 @@ extern "C" int dpt_debug_stamps(unsigned long long *out, int reset) {
     }
     return 0;
 }
+#endif
+#ifdef DPT_WSTAMPS
+// the first pass's per-wave timeline (WST_REC): WST_MAXW x WST_N u64 into out; reset zeroes it
+extern "C" int dpt_debug_wstamps(unsigned long long *out, int reset) {
+    const size_t nbytes = sizeof(unsigned long long) * WST_MAXW * WST_N;
+    if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wst), nbytes) != hipSuccess) return -1;
+    if (reset) {
+        void *p = nullptr;
+        if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_wst)) != hipSuccess || hipMemset(p, 0, nbytes) != hipSuccess) return -1;
+    }
+    return 0;
+}
+extern "C" int dpt_debug_wstamps_dims(unsigned *maxw, unsigned *n) { *maxw = WST_MAXW; *n = WST_N; return 0; }
 #endif
 
 }  // namespace dpt

@@ -562,9 +562,11 @@ inline Args long_args(const LongLaunch &p) {
     Args a;
     a.text = p.text; a.str_off = p.str_off; a.cut_mask = p.cut_mask;
     a.staging = p.staging; a.staging16 = p.staging16; a.counts = p.counts; a.bsum = p.bsum; a.status = p.status; a.capped = p.capped;
-    a.rec = reinterpret_cast<uint4 *>(p.arena);
-    a.stg = reinterpret_cast<int32_t *>(p.arena + 16 * p.arena_cap);
-    a.arena_cap = p.arena_cap;
+    // (a test-only arena_bias B: the counter starts at B, so offset ao addresses element ao - B; the
+    // pointers are shifted by B elements, the capacity raised by B -- dpt_ctx_debug_counter_bias)
+    a.rec = reinterpret_cast<uint4 *>(reinterpret_cast<uintptr_t>(p.arena) - 16 * p.arena_bias);
+    a.stg = reinterpret_cast<int32_t *>(reinterpret_cast<uintptr_t>(p.arena + 16 * p.arena_cap) - 4 * p.arena_bias);
+    a.arena_cap = p.arena_cap + p.arena_bias;
     a.arena_used = p.arena_used;
     a.edges = p.edges; a.far = p.far; a.far_cap = p.far_cap; a.far_count = p.far_count; a.list = p.list; a.list_count = p.list_count; a.work_next = p.work_next;
     a.slots = p.slots; a.slots4 = p.slots4; a.n_slots = p.n_slots; a.root_base = p.root_base;

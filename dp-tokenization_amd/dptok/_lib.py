@@ -74,9 +74,10 @@ def lib():
     L.dpt_ctx_set_histogram_ex.argtypes = [P, P, ctypes.c_uint32, I32]
     L.dpt_ctx_profile.argtypes = [P, I32]
     L.dpt_ctx_profile_read.argtypes = [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(U64)]
+    L.dpt_ctx_debug_counter_bias.argtypes = [P, U64]
     for name in ("dpt_vocab_create", "dpt_vocab_destroy", "dpt_vocab_stats_get", "dpt_ctx_create", "dpt_ctx_destroy",
                  "dpt_ctx_reserve", "dpt_ctx_reserve_vocab", "dpt_ctx_workspace_bytes", "dpt_ctx_long_need", "dpt_encode", "dpt_encode_padded", "dpt_encode_host", "dpt_dp_host", "dpt_dp_host_far", "dpt_token_histogram",
-                 "dpt_ctx_set_histogram", "dpt_ctx_set_histogram_ex", "dpt_ctx_profile", "dpt_ctx_profile_read"):
+                 "dpt_ctx_set_histogram", "dpt_ctx_set_histogram_ex", "dpt_ctx_profile", "dpt_ctx_profile_read", "dpt_ctx_debug_counter_bias"):
         getattr(L, name).restype = I32
     _lib = L
     return L
@@ -93,4 +94,4 @@ EXPORTED = ["dpt_last_error", "dpt_abi_version", "dpt_vocab_create", "dpt_vocab_
             "dpt_ctx_long_need",
             "dpt_encode", "dpt_encode_padded", "dpt_encode_host",
             "dpt_dp_host", "dpt_dp_host_far", "dpt_token_histogram", "dpt_ctx_set_histogram", "dpt_ctx_set_histogram_ex",
-            "dpt_ctx_profile", "dpt_ctx_profile_read"]
+            "dpt_ctx_profile", "dpt_ctx_profile_read", "dpt_ctx_debug_counter_bias"]

@@ -434,6 +434,11 @@ class Encoder:
                                              ctypes.c_void_p(hist_ptr), n_bins, ctypes.c_void_p(stream or None)),
               "dpt_token_histogram")
 
+    def debug_counter_bias(self, bias: int) -> None:
+        """TEST-ONLY (dpt_ctx_debug_counter_bias): later calls start the unbounded pass's arena and far-pair
+        counters at ``bias`` (results unchanged; its kernels' offsets become >= bias)."""
+        check(_lib.lib().dpt_ctx_debug_counter_bias(self.handle, bias), "dpt_ctx_debug_counter_bias")
+
     def profile(self, on: bool = True) -> None:
         check(_lib.lib().dpt_ctx_profile(self.handle, 1 if on else 0), "dpt_ctx_profile")
 

@@ -195,6 +195,47 @@ def unpack(text: np.ndarray, offs: np.ndarray) -> List[str]:
     return [raw[o[i]:o[i + 1]].decode("utf-8", "surrogatepass") for i in range(len(o) - 1)]
 
 
+LLAMA_PREFIX = "<s>▁".encode("utf-8")   # the BOS piece, then SentencePiece's dummy-prefix '▁'
+_SPACE_PIECE = "▁".encode("utf-8")
+_NL_PIECE = b"<0x0A>"
+
+
+def llama_words(text: np.ndarray, offs: np.ndarray) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """Raw strings -> the pre-split form llama mode hands the DP (reference tokenizer_utils.py:24-31, :7-22):
+    per string the BOS word ``"<s>"``, then the text with every ``' '`` as ``'▁'`` opening a word (SentencePiece's
+    normaliser, plus its dummy prefix before the first character) and ``'\\n'`` as its byte-fallback piece
+    ``"<0x0A>"`` -- the words ``merge_tokens`` builds from the pieces of a Llama-2 SentencePiece model whose
+    pieces never cross a '▁', written out as UTF-8 with a word-start mask (DPT_MODE_PRESPLIT).  Vectorised:
+    -> (text, offs, cut) with cut[k] = 1 where a word starts."""
+    offs = np.asarray(offs, dtype=np.uint64)
+    text = np.asarray(text, dtype=np.uint8)[int(offs[0]):int(offs[-1])]
+    offs = offs - offs[0]
+    n = len(offs) - 1
+    sp = text == 0x20
+    nl = text == 0x0A
+    width = 1 + 2 * sp.astype(np.int64) + 5 * nl.astype(np.int64)
+    P = len(LLAMA_PREFIX)
+    sid = np.repeat(np.arange(n, dtype=np.int64), np.diff(offs).astype(np.int64))   # string of each byte
+    pos = np.cumsum(width) - width + P * (sid + 1)                                   # output position of each byte
+    tot = np.zeros(n + 1, dtype=np.int64)
+    tot[1:] = np.cumsum(np.bincount(sid, weights=width, minlength=n).astype(np.int64) + P)
+    out = np.empty(int(tot[-1]), dtype=np.uint8)
+    cut = np.zeros(int(tot[-1]), dtype=np.uint8)
+    plain = ~(sp | nl)
+    out[pos[plain]] = text[plain]
+    for k in range(3):
+        out[pos[sp] + k] = _SPACE_PIECE[k]
+    for k in range(6):
+        out[pos[nl] + k] = _NL_PIECE[k]
+    base = tot[:-1]
+    for k in range(P):
+        out[base + k] = LLAMA_PREFIX[k]
+    cut[base] = 1                    # "<s>"
+    cut[base + 3] = 1                # the dummy prefix '▁' opens the first word
+    cut[pos[sp]] = 1                 # every other '▁'
+    return out, tot.astype(np.uint64), cut
+
+
 def _gen_chunk(args):
     kind, n, start, kw = args
     return {"s2orc": s2orc_like_corpus, "arabic": arabic_corpus}[kind](n, start=start, **kw)

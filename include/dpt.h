@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define DPT_ABI_VERSION 4
+#define DPT_ABI_VERSION 5
 
 /* return codes */
 #define DPT_OK 0
@@ -217,6 +217,14 @@ int dpt_ctx_profile(dpt_ctx *c, int enable);
 /* Sums over calls since the last read (synchronises on the recorded events):
  * ms[0] tokenize passes; ms[1], ms[2] = -1 (not timed); *launches = calls timed. */
 int dpt_ctx_profile_read(dpt_ctx *c, double *ms, uint64_t *launches);
+
+/* TEST-ONLY.  Every later call on c starts the unbounded pass's arena counter and the far-pair counter
+ * at `bias` instead of 0, with the arena and far-list pointers the kernels get shifted back by as many
+ * elements: results are unchanged, but the kernels' arena offsets and far-pair indices are >= bias.
+ * With a bias whose low word is >= 2^31 this exercises the 64-bit uniform reassembly of those values
+ * (two readfirstlane halves; an int low half sign-extends) without a 40-GiB arena
+ * (tests/test_gpu_parity.py::test_long_pass_offsets_past_2g).  bias < 2^62; 0 turns it off. */
+int dpt_ctx_debug_counter_bias(dpt_ctx *c, uint64_t bias);
 
 #ifdef __cplusplus
 }

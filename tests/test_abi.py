@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     for name in _declared():
         assert hasattr(L, name), name
     assert set(_declared()) == set(_lib.EXPORTED)
-    assert L.dpt_abi_version() == 4
+    assert L.dpt_abi_version() == 5
     for gone in ("dpt_ctx_pipeline", "dpt_ctx_join", "dpt_ctx_copy_stats", "dpt_self_copy_available"):   # ABI 4 dropped them
         assert not hasattr(L, gone), gone
 

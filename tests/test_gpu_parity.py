@@ -625,6 +625,88 @@ def test_dp_host_without_far_list_reports_status_3():
     assert far.tolist() == [[len(t) + 2 - 1, len(t) - 1]]
 
 
+def _long_word_texts():
+    """test_long_words_big_window's inputs: words of 255..20000 bytes (the 2048-byte and unbounded passes)."""
+    rng = np.random.default_rng(5)
+    texts = []
+    for L in (255, 256, 257, 300, 700, 1500, 2047, 2048, 2049, 3000, 5000, 20000):
+        w = "".join(chr(c) for c in rng.integers(0x21, 0x7F, size=L))
+        texts += [w, "ab cd " + w + " ef", w + " " + w[: L // 2], ("\n" + w[:L // 3] + " x\n").join([w[:100], w[100:]])]
+    return texts
+
+
+@pytest.mark.parametrize("bias", [0x80000000 + 12345, (3 << 32) | 0xFFFFF000])
+def test_long_pass_offsets_past_2g(bias, vocabs, oracles):
+    """Round 5's fault (gpurun_out/r05v/ab_ascii_1000000.log): a 64-bit uniform value put together from two
+    readfirstlane halves sign-extends an int low half >= 2^31.  Besides the finish copy's store resource
+    (test_device_path_output_at_high_addresses) the fix covered the unbounded pass's arena offset and its
+    far-pair base (dpt_long.hip).  dpt_ctx_debug_counter_bias starts both counters at `bias` (low word >= 2^31;
+    the second also carries into the high word), so those offsets pass 2^31 without a 40-GiB arena: the
+    long-word inputs (test_long_words_big_window, test_tokens_longer_than_64_code_points) through the host
+    and device paths against the oracle, and the far-pair lists against an unbiased engine's."""
+    torch = pytest.importorskip("torch")
+    from dptok import Encoder, Vocab, synth
+    from dptok.engine import atoms_to_csr
+    from oracle import oracle
+    # (1) the arena offset: the unbounded pass takes the words over 2048 bytes
+    enc = Encoder(Vocab(vocabs["llama32k"], 0))
+    enc.debug_counter_bias(bias)
+    text, offs = _csr(_long_word_texts())
+    ref = oracles["llama32k"].encode_csr(text, offs)
+    got = enc.encode_csr(text, offs)
+    _cmp_csr(got, ref)
+    assert np.array_equal(got[3], ref[3])
+    assert enc.long_need()[0] > 0          # (the pass ran, and the bias is subtracted from what it reports)
+    n = len(offs) - 1
+    dt = torch.from_numpy(text).cuda()
+    do = torch.from_numpy(offs.view(np.int64)).cuda()
+    ids = torch.empty(len(text), dtype=torch.int32, device="cuda")
+    io = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    st = torch.empty(n, dtype=torch.int32, device="cuda")
+    enc.encode_device(dt.data_ptr(), len(text), do.data_ptr(), n, ids.data_ptr(), len(text), io.data_ptr(), st.data_ptr(),
+                      stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    off_h = io.cpu().numpy().view(np.uint64)
+    assert np.array_equal(off_h, ref[1]) and np.array_equal(st.cpu().numpy(), ref[2])
+    assert np.array_equal(ids[: int(off_h[-1])].cpu().numpy(), ref[0])
+    need, cap = enc.long_need()
+    assert 0 < need <= cap
+    # (2) a vocabulary with tokens of 65..300 code points: words over 64 atoms take the unbounded pass
+    t2i = dict(synth.llama_shaped_vocab())
+    rng = np.random.default_rng(4)
+    long_toks = ["".join(chr(c) for c in rng.integers(0x61, 0x64, size=L)) for L in (65, 70, 80, 150, 300) for _ in range(10)]
+    for t in long_toks:
+        t2i.setdefault(t, len(t2i))
+    v = Vocab(t2i, 0)
+    encl = Encoder(v)
+    encl.debug_counter_bias(bias)
+    long_ = ["x" + "".join(chr(c) for c in rng.integers(0x61, 0x64, size=rng.integers(65, 400))) for _ in range(200)]
+    for k in range(100):
+        a, b = long_toks[k % len(long_toks)], long_toks[(7 * k + 3) % len(long_toks)]
+        long_.append("x" + a + "ab" + b[: (k * 13) % len(b)] + " " + b)
+    text, offs = _csr(long_)
+    got = encl.encode_csr(text, offs)
+    ref = oracle.OracleVocab(t2i).encode_csr(text, offs)
+    _cmp_csr(got, ref)
+    assert np.array_equal(got[3], ref[3])
+    # (3) the far-pair base: optimal predecessors more than 64 atoms back, listed by dpt_dp_host_far
+    longs = ["".join(chr(c) for c in rng.integers(0x61, 0x64, size=L)) for L in (65, 66, 70, 80, 100, 150, 300)]
+    u, w = longs[2], longs[3]
+    fv = {"a", "b", "c", "x", "ab", "bc", "ca"} | set(longs) | {u + w[:3], w[3:], u[:-2], u[-2:] + w}
+    words = [u + w, "x" + u + w, u + w + "ab", longs[0] + longs[1], longs[6] + "abc" + longs[5]]
+    words += [longs[k % 7] + "abc"[: k % 4] + longs[(3 * k + 1) % 7][: 60 + k] for k in range(25)]
+    ft2i = {t: i for i, t in enumerate(sorted(fv))}
+    plain, biased = Encoder(Vocab(ft2i, 0)), Encoder(Vocab(ft2i, 0))
+    biased.debug_counter_bias(bias)
+    ftext, foffs, fcut = atoms_to_csr([list(wd) for wd in words])
+    r0 = plain.dp(ftext, foffs, cut_mask=fcut, edges=True, far=True)
+    r1 = biased.dp(ftext, foffs, cut_mask=fcut, edges=True, far=True)
+    for x, y in zip(r0[:3], r1[:3]):
+        assert np.array_equal(x, y)
+    assert len(r0[3]) >= 5
+    assert sorted(map(tuple, r0[3].tolist())) == sorted(map(tuple, r1[3].tolist()))
+
+
 @pytest.mark.parametrize("n", [4095, 8192, 65535, 65536, 100003])
 def test_work_partitions_vs_oracle(n, engines, oracles):
     """First-pass work distribution (tokenize_kernel: min(16, n / 4096) partition counters, claims of
@@ -684,3 +766,46 @@ def test_encode_padded_matches_csr(vocabs, engines):
             a, b = int(offs[i]), int(off_h[i])
             c = int(cnt_h[i])
             assert np.array_equal(pids_h[a:a + c], ids_h[b:b + c]), (rep, i)
+
+
+def test_bloom_words_across_windows():
+    """The 64-lane kernel's whole-word shortcut (a word that is ONE token is taken as such) relies on every
+    256-byte window ending at a word start (window_bounds) and on the byte-stream walker never stepping past
+    a word's end.  Strings of 240..900 bytes (2..4 windows) of BLOOM-scale words: tokens, tokens + 1..2
+    letters (the prefix up to any cut is a token, the word is not), tokens less their last letter, short
+    tokens -- every string against the oracle."""
+    from bloom_fixture import big_vocab
+    from dptok import Encoder, Vocab, synth
+    from oracle import oracle
+    t2i = big_vocab()
+    longs, shorts = synth.bloom_word_pool(t2i)
+    rng = np.random.default_rng(21)
+    sp = synth.BYTE_SPACE
+    parts, cuts = [], []
+    for _ in range(3000):
+        target, n, buf, cut = int(rng.integers(240, 900)), 0, bytearray(), bytearray()
+        while n < target:
+            r = rng.random()
+            w = longs[int(rng.integers(len(longs)))]
+            if 0.3 <= r < 0.6:
+                w = w + "".join(rng.choice(list("xqz"), size=int(rng.integers(1, 3))))
+            elif 0.6 <= r < 0.8:
+                w = w[:-1]
+            elif r >= 0.8:
+                w = shorts[int(rng.integers(len(shorts)))]
+            atoms = ([sp] if buf else []) + list(w)
+            for k, a in enumerate(atoms):
+                e = a.encode("utf-8")
+                buf += e
+                cut += bytes([3 if k == 0 else 2]) + b"\x00" * (len(e) - 1)
+            n += len(w) + 2
+        parts.append(bytes(buf))
+        cuts.append(bytes(cut))
+    offs = np.zeros(len(parts) + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([len(p) for p in parts], dtype=np.uint64)
+    text = np.frombuffer(b"".join(parts), dtype=np.uint8).copy()
+    cut = np.frombuffer(b"".join(cuts), dtype=np.uint8).copy()
+    got = Encoder(Vocab(t2i, 0)).encode_csr(text, offs, mode="atoms", cut_mask=cut)
+    ref = oracle.OracleVocab(t2i).encode_csr(text, offs, mode=oracle.ATOMS, cut_mask=cut)
+    _cmp_csr(got, ref)
+    assert (got[2] == 0).sum() > 2500

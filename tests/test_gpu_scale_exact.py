@@ -51,3 +51,21 @@ def test_bloom_prefix_exact():
     t2i = big_vocab()
     text, offs, cut = synth.bloom_like_parallel(200_000, t2i, start=0, procs=1, length=256)
     _check(Encoder(Vocab(t2i, 0)), oracle.OracleVocab(t2i), text, offs, "atoms", oracle.ATOMS, cut)
+
+
+def test_presplit_llama_mode_prefix_exact():
+    """llama mode (pretokenize_option='llama', the factory's default, reference tokenizer_utils.py:52, :64-65) at
+    bench scale: the first 262,144 cfg2 strings and 20,000 cfg4 abstracts of `bench.py --workload cfg2p|cfg4p`
+    (BOS word + SentencePiece-shaped words, dptok.synth.llama_words), DPT_MODE_PRESPLIT, against the oracle's
+    PRESPLIT mode -- every string."""
+    from dptok import Encoder, Vocab, synth
+    from oracle import oracle
+    t2i = synth.llama_shaped_vocab()
+    enc, ov = Encoder(Vocab(t2i, 0)), oracle.OracleVocab(t2i)
+    text, offs = synth.random_ascii_corpus(262_144, 256, seed=1)
+    t2, o2, cut = synth.llama_words(text, offs)
+    n, nb = _check(enc, ov, t2, o2, "presplit", oracle.PRESPLIT, cut)
+    assert n == 262_144 and nb > 262_144 * 262
+    text, offs = synth.generate_parallel("s2orc", 20_000, start=0, procs=1, seed=4)
+    t2, o2, cut = synth.llama_words(text, offs)
+    _check(enc, ov, t2, o2, "presplit", oracle.PRESPLIT, cut)
