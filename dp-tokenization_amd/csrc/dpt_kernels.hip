@@ -118,6 +118,30 @@ __device__ __forceinline__ unsigned wave_shift_in(unsigned x, unsigned in) {
     return (unsigned)__builtin_amdgcn_update_dpp((int)in, (int)x, 0x138, 0xF, 0xF, false);
 }
 
+// Lane-group shifts for lane-mode B: lane l of a group of LW lanes receives x of lane l + K (gshl) / l - K (gshr),
+// `fill` past the group's edge.  LW = 16: one DPP row op (row_shl / row_shr:K); LW = 64 (one string across the
+// wave, the one-string kernel): ds_bpermute.
+template <int LW, unsigned K>
+__device__ __forceinline__ unsigned gshl(unsigned x, unsigned fill) {
+    if constexpr (LW == 16) {
+        return (unsigned)__builtin_amdgcn_update_dpp((int)fill, (int)x, 0x100 | K, 0xF, 0xF, false);
+    } else {
+        const unsigned l = lane_id();
+        const unsigned v = (unsigned)__builtin_amdgcn_ds_bpermute((int)(((l + K) & 63u) << 2), (int)x);
+        return l + K < 64u ? v : fill;
+    }
+}
+template <int LW, unsigned K>
+__device__ __forceinline__ unsigned gshr(unsigned x, unsigned fill) {
+    if constexpr (LW == 16) {
+        return (unsigned)__builtin_amdgcn_update_dpp((int)fill, (int)x, 0x110 | K, 0xF, 0xF, false);
+    } else {
+        const unsigned l = lane_id();
+        const unsigned v = (unsigned)__builtin_amdgcn_ds_bpermute((int)(((l - K) & 63u) << 2), (int)x);
+        return l >= K ? v : fill;
+    }
+}
+
 // 64-bit inclusive add-scan over the wave (ds_bpermute shifts)
 __device__ __forceinline__ uint64_t wave_incl_scan_add64(uint64_t v, unsigned lane) {
 #pragma unroll
@@ -936,7 +960,7 @@ __device__ __forceinline__ void reset_counters(uint32_t *ctr, uint64_t *snap = n
 // The body of tokenize_kernel (and of fallback_kernel's 2048-byte blocks); bid: the block's index
 // among the blocks running it.  The kernel arguments start with a KernArgs (read through the kernarg
 // segment pointer, KREFRESH).
-template <int CH, int G, bool BIG, bool WIDE, int SW = 0, bool RAW = false>
+template <int CH, int G, bool BIG, bool WIDE, int SW = 0, bool RAW = false, bool SOLO = false>
 __device__ __forceinline__ void tokenize_body(const unsigned bid) {
     ConstKernArgs *kp = (ConstKernArgs *)__builtin_amdgcn_kernarg_segment_ptr();
 #define a (kp->ea)
@@ -1941,6 +1965,15 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
             // every j in E(i) then ties on max(G[j], cp(span))).  de and E(i) are local.
             auto forward_lanes = [&]() {
               if constexpr (G == 16) {
+                // LW lanes share a window: a 16-lane row per slot, or (the one-string kernel, SOLO) the whole
+                // wave on slot 0 -- chunks of <= 5 boundaries instead of 17, so the dependent LDS steps of the
+                // recurrence and of the C1 walks are a quarter as many (the per-call floor)
+                constexpr int LW = SOLO ? 64 : 16;
+                constexpr unsigned CMAX = ((unsigned)(CH + LW - 1) / (unsigned)LW) | 1u;   // boundaries per lane, at most
+                const unsigned mg = SOLO ? 0u : lane / 16u;
+                const unsigned d = SOLO ? lane : lane % 16u;
+                GL &L = grp(mg);
+                const unsigned na = SSr(mg).n_atoms;
                 uint32_t *rec32 = reinterpret_cast<uint32_t *>(L.rec);
                 constexpr unsigned FRESH = 31u;   // key16 of a fresh start: cost 0, reachable, G 0
                 // key16 = cost << 6 | invalid << 5 | 31 - G (the Wfin<16> form)
@@ -1954,14 +1987,14 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                 // boundaries per lane (na <= 256), odd: lanes stepping through their chunks together
                 // then hit distinct LDS banks (ds_read_b32: 32 banks per 32-lane group; a stride of
                 // 16 dwords put 8 lanes on a bank)
-                const unsigned C = ((na + 15u) >> 4) | 1u;   // <= 17
+                const unsigned C = ((na + (unsigned)LW - 1u) / (unsigned)LW) | 1u;   // <= CMAX
                 const unsigned c0 = min(d * C, na), c1 = min(c0 + C, na);
                 // one backward pass over the chunk's ends (c0, c1]: the local suffix min of lo
                 // decides the cuts as far as this chunk's ends go; the later chunks' ends (min S)
                 // then only cap them: p is a cut iff both mins are >= p, i.e. p <= S
                 unsigned mloc = 0xFFFFu, lcut = 0;
 #pragma unroll 4
-                for (int k = 16; k >= 0; k--) {
+                for (int k = (int)CMAX - 1; k >= 0; k--) {
                     const unsigned i = c0 + 1u + (unsigned)k;
                     if (i <= c1) {
                         const unsigned hb = 31u - (unsigned)__builtin_clz((~rec32[i] >> 16) | 1u);   // bit 0 is set in a capless window
@@ -1969,36 +2002,48 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                         if (mloc >= i - 1u) lcut |= 1u << k;   // boundary p = i-1 = c0+k < c1
                     }
                 }
-                // min lo over the later lanes of the row (row_shl: lane l reads lane l+k)
+                // min lo over the later lanes of the group (shift left: lane l reads lane l+k)
                 unsigned sm = mloc;
-                sm = min(sm, (unsigned)__builtin_amdgcn_update_dpp((int)0xFFFFu, (int)sm, 0x101, 0xF, 0xF, false));
-                sm = min(sm, (unsigned)__builtin_amdgcn_update_dpp((int)0xFFFFu, (int)sm, 0x102, 0xF, 0xF, false));
-                sm = min(sm, (unsigned)__builtin_amdgcn_update_dpp((int)0xFFFFu, (int)sm, 0x104, 0xF, 0xF, false));
-                sm = min(sm, (unsigned)__builtin_amdgcn_update_dpp((int)0xFFFFu, (int)sm, 0x108, 0xF, 0xF, false));
-                const unsigned S = (unsigned)__builtin_amdgcn_update_dpp((int)0xFFFFu, (int)sm, 0x101, 0xF, 0xF, false);
+                sm = min(sm, gshl<LW, 1>(sm, 0xFFFFu));
+                sm = min(sm, gshl<LW, 2>(sm, 0xFFFFu));
+                sm = min(sm, gshl<LW, 4>(sm, 0xFFFFu));
+                sm = min(sm, gshl<LW, 8>(sm, 0xFFFFu));
+                if constexpr (LW == 64) {
+                    sm = min(sm, gshl<LW, 16>(sm, 0xFFFFu));
+                    sm = min(sm, gshl<LW, 32>(sm, 0xFFFFu));
+                }
+                const unsigned S = gshl<LW, 1>(sm, 0xFFFFu);
                 // boundaries c0 + k <= S
-                const unsigned cut = S < c0 ? 0u : (S - c0 >= 16u ? lcut : lcut & ((2u << (S - c0)) - 1u));
+                const unsigned cut = S < c0 ? 0u : (S - c0 >= CMAX - 1u ? lcut : lcut & ((2u << (S - c0)) - 1u));
                 // rs = the first cut at or after c0 (in this lane's chunk or a later one; na is a cut)
                 unsigned rs = cut ? c0 + ffbl(cut) : na;
-                rs = min(rs, (unsigned)__builtin_amdgcn_update_dpp((int)na, (int)rs, 0x101, 0xF, 0xF, false));
-                rs = min(rs, (unsigned)__builtin_amdgcn_update_dpp((int)na, (int)rs, 0x102, 0xF, 0xF, false));
-                rs = min(rs, (unsigned)__builtin_amdgcn_update_dpp((int)na, (int)rs, 0x104, 0xF, 0xF, false));
-                rs = min(rs, (unsigned)__builtin_amdgcn_update_dpp((int)na, (int)rs, 0x108, 0xF, 0xF, false));
+                rs = min(rs, gshl<LW, 1>(rs, na));
+                rs = min(rs, gshl<LW, 2>(rs, na));
+                rs = min(rs, gshl<LW, 4>(rs, na));
+                rs = min(rs, gshl<LW, 8>(rs, na));
+                if constexpr (LW == 64) {
+                    rs = min(rs, gshl<LW, 16>(rs, na));
+                    rs = min(rs, gshl<LW, 32>(rs, na));
+                }
                 if constexpr (NEAR_CUT) {
                     // the NEAREST cut to c0 instead of the first one after it: snapping up made the longest
                     // chunk of a wave ~2x the mean on cfg4's long words (a 256-atom window: 36.7 ends
                     // against C = 17), and the wave steps as long as its longest chunk; nearest-cut
                     // rounding is monotone in c0, so the chunks still tile (0, na]
                     const unsigned lastc = cut ? c0 + (31u - (unsigned)__builtin_clz(cut)) : 0u;   // (0 is a cut)
-                    unsigned pm = lastc;   // max over the lanes <= d of the row, then shifted: lanes < d
-                    pm = max(pm, (unsigned)__builtin_amdgcn_update_dpp(0, (int)pm, 0x111, 0xF, 0xF, false));   // row_shr:1
-                    pm = max(pm, (unsigned)__builtin_amdgcn_update_dpp(0, (int)pm, 0x112, 0xF, 0xF, false));   // row_shr:2
-                    pm = max(pm, (unsigned)__builtin_amdgcn_update_dpp(0, (int)pm, 0x114, 0xF, 0xF, false));   // row_shr:4
-                    pm = max(pm, (unsigned)__builtin_amdgcn_update_dpp(0, (int)pm, 0x118, 0xF, 0xF, false));   // row_shr:8
-                    const unsigned prevc = (unsigned)__builtin_amdgcn_update_dpp(0, (int)pm, 0x111, 0xF, 0xF, false);
+                    unsigned pm = lastc;   // max over the lanes <= d of the group, then shifted: lanes < d
+                    pm = max(pm, gshr<LW, 1>(pm, 0u));
+                    pm = max(pm, gshr<LW, 2>(pm, 0u));
+                    pm = max(pm, gshr<LW, 4>(pm, 0u));
+                    pm = max(pm, gshr<LW, 8>(pm, 0u));
+                    if constexpr (LW == 64) {
+                        pm = max(pm, gshr<LW, 16>(pm, 0u));
+                        pm = max(pm, gshr<LW, 32>(pm, 0u));
+                    }
+                    const unsigned prevc = gshr<LW, 1>(pm, 0u);
                     rs = (c0 - prevc < rs - c0) ? prevc : rs;
                 }
-                const unsigned re = (unsigned)__builtin_amdgcn_update_dpp((int)na, (int)rs, 0x101, 0xF, 0xF, false);
+                const unsigned re = gshl<LW, 1>(rs, na);
                 if (DPT_STOP == 25) return;   // diagnostic: cut points only
 
                 // ---- the recurrence over ends (rs, re], one position per iteration
@@ -2059,11 +2104,15 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                     const unsigned comb = (y & 0xFFC0u) + (x & 0xFFC0u) + min(y & 31u, x & 31u);
                     x = (x >> 16) ? x : ((y & 0x10000u) | comb);
                 };
-                compose((unsigned)__builtin_amdgcn_update_dpp((int)FRESH, (int)x, 0x111, 0xF, 0xF, false));   // row_shr:1
-                compose((unsigned)__builtin_amdgcn_update_dpp((int)FRESH, (int)x, 0x112, 0xF, 0xF, false));   // row_shr:2
-                compose((unsigned)__builtin_amdgcn_update_dpp((int)FRESH, (int)x, 0x114, 0xF, 0xF, false));   // row_shr:4
-                compose((unsigned)__builtin_amdgcn_update_dpp((int)FRESH, (int)x, 0x118, 0xF, 0xF, false));   // row_shr:8
-                const unsigned in = (unsigned)__builtin_amdgcn_update_dpp((int)FRESH, (int)x, 0x111, 0xF, 0xF, false) & 0xFFFFu;
+                compose(gshr<LW, 1>(x, FRESH));
+                compose(gshr<LW, 2>(x, FRESH));
+                compose(gshr<LW, 4>(x, FRESH));
+                compose(gshr<LW, 8>(x, FRESH));
+                if constexpr (LW == 64) {
+                    compose(gshr<LW, 16>(x, FRESH));
+                    compose(gshr<LW, 32>(x, FRESH));
+                }
+                const unsigned in = gshr<LW, 1>(x, FRESH) & 0xFFFFu;
                 const unsigned gin = 31u - (in & 31u);   // G at rs
                 if (gin) {
                     const unsigned lim = pe ? pe : re;
@@ -2096,22 +2145,30 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                 // and that chunk re-walks P1 in de mode.
                 // token base: exclusive prefix sum of T over the row; the window's count to wtok
                 unsigned tb = T;
-                tb += (unsigned)__builtin_amdgcn_update_dpp(0, (int)tb, 0x111, 0xF, 0xF, false);
-                tb += (unsigned)__builtin_amdgcn_update_dpp(0, (int)tb, 0x112, 0xF, 0xF, false);
-                tb += (unsigned)__builtin_amdgcn_update_dpp(0, (int)tb, 0x114, 0xF, 0xF, false);
-                tb += (unsigned)__builtin_amdgcn_update_dpp(0, (int)tb, 0x118, 0xF, 0xF, false);
-                if (d == 15) SSr(mg).wtok = tb;
+                tb += gshr<LW, 1>(tb, 0u);
+                tb += gshr<LW, 2>(tb, 0u);
+                tb += gshr<LW, 4>(tb, 0u);
+                tb += gshr<LW, 8>(tb, 0u);
+                if constexpr (LW == 64) {
+                    tb += gshr<LW, 16>(tb, 0u);
+                    tb += gshr<LW, 32>(tb, 0u);
+                }
+                if (d == (unsigned)LW - 1u) SSr(mg).wtok = tb;
                 tb -= T;
                 // P1's L*: from rec[re] when its word ends at re, else from the right (the first
                 // word end of the next chunk that has one)
                 unsigned lsr = pe ? (0x10000u | (((unsigned)L.rec[pe].cpos >> 11) & 15u)) : 0u;
                 auto copy_r = [&](unsigned y) { lsr = (lsr >> 16) ? lsr : y; };
-                copy_r((unsigned)__builtin_amdgcn_update_dpp(0, (int)lsr, 0x101, 0xF, 0xF, false));   // row_shl:1
-                copy_r((unsigned)__builtin_amdgcn_update_dpp(0, (int)lsr, 0x102, 0xF, 0xF, false));   // row_shl:2
-                copy_r((unsigned)__builtin_amdgcn_update_dpp(0, (int)lsr, 0x104, 0xF, 0xF, false));   // row_shl:4
-                copy_r((unsigned)__builtin_amdgcn_update_dpp(0, (int)lsr, 0x108, 0xF, 0xF, false));   // row_shl:8
+                copy_r(gshl<LW, 1>(lsr, 0u));
+                copy_r(gshl<LW, 2>(lsr, 0u));
+                copy_r(gshl<LW, 4>(lsr, 0u));
+                copy_r(gshl<LW, 8>(lsr, 0u));
+                if constexpr (LW == 64) {
+                    copy_r(gshl<LW, 16>(lsr, 0u));
+                    copy_r(gshl<LW, 32>(lsr, 0u));
+                }
                 // (DPP reads outside any branch: a lane masked off in EXEC reads as 0)
-                const unsigned lsn = (unsigned)__builtin_amdgcn_update_dpp(0, (int)lsr, 0x101, 0xF, 0xF, false);
+                const unsigned lsn = gshl<LW, 1>(lsr, 0u);
                 const unsigned ls1 = re_ws ? gre : (lsn & 15u) + 1u;
                 const bool walk = !len_only && SSr(mg).status == 0;   // per row (not uniform)
                 const bool left_of_q = gre < ls1;
@@ -2151,11 +2208,15 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                 // whose last piece is P1 also passes on what came in; none crosses a word start
                 unsigned fl = ((T > 0 && afin >= lsm) ? 1u : 0u) | ((!p1in || re_ws) ? 2u : 0u);
                 auto flag_r = [&](unsigned y) { fl = (fl & 2u) ? fl : (fl | (y & 3u)); };
-                flag_r((unsigned)__builtin_amdgcn_update_dpp(0, (int)fl, 0x101, 0xF, 0xF, false));   // row_shl:1
-                flag_r((unsigned)__builtin_amdgcn_update_dpp(0, (int)fl, 0x102, 0xF, 0xF, false));   // row_shl:2
-                flag_r((unsigned)__builtin_amdgcn_update_dpp(0, (int)fl, 0x104, 0xF, 0xF, false));   // row_shl:4
-                flag_r((unsigned)__builtin_amdgcn_update_dpp(0, (int)fl, 0x108, 0xF, 0xF, false));   // row_shl:8
-                const unsigned fln = (unsigned)__builtin_amdgcn_update_dpp(0, (int)fl, 0x101, 0xF, 0xF, false);
+                flag_r(gshl<LW, 1>(fl, 0u));
+                flag_r(gshl<LW, 2>(fl, 0u));
+                flag_r(gshl<LW, 4>(fl, 0u));
+                flag_r(gshl<LW, 8>(fl, 0u));
+                if constexpr (LW == 64) {
+                    flag_r(gshl<LW, 16>(fl, 0u));
+                    flag_r(gshl<LW, 32>(fl, 0u));
+                }
+                const unsigned fln = gshl<LW, 1>(fl, 0u);
                 const bool fin_in = !re_ws && (fln & 1u) != 0;
                 // q's chunk with a chance L* token to the right: P1 again in de mode (A = L*);
                 // P1 starts below L* only from rs with gin < L* or from a word start inside
@@ -2903,10 +2964,11 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
 #undef tv
 }
 
-template <int CH, int G, bool BIG, bool WIDE, int SW = 0, bool RAW = false>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((CH == 256 && G == 16) ? WPE16 : ((CH == 256 && G == 64) ? WPE64 : 1))))
+template <int CH, int G, bool BIG, bool WIDE, int SW = 0, bool RAW = false, bool SOLO = false>
+// (the one-string kernel, SOLO, is one wave: no occupancy to keep, so no VGPR cap and no spills)
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SOLO ? 1 : ((CH == 256 && G == 16) ? WPE16 : ((CH == 256 && G == 64) ? WPE64 : 1)))))
 tokenize_kernel(KernArgs ka) {
-    tokenize_body<CH, G, BIG, WIDE, SW, RAW>(blockIdx.x);
+    tokenize_body<CH, G, BIG, WIDE, SW, RAW, SOLO>(blockIdx.x);
 }
 
 // ------------------------------------------------------------------ compaction
@@ -3323,14 +3385,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) mi
 
 constexpr int MAX_DEVICES = 64;
 // Resident waves per CU for an instantiation (LDS / VGPR limited); DPT_WAVES_PER_CU overrides.
-template <int CH, int G, bool BIG, bool WIDE, int SW = 0, bool RAW = false>
+template <int CH, int G, bool BIG, bool WIDE, int SW = 0, bool RAW = false, bool SOLO = false>
 static unsigned resident_per_cu() {
     static unsigned cached[MAX_DEVICES] = {};   // per device: a process may drive several
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAX_DEVICES) dev = 0;
     if (cached[dev]) return cached[dev];
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, tokenize_kernel<CH, G, BIG, WIDE, SW, RAW>, 64, block_lds_bytes<CH, G>()) != hipSuccess || nb <= 0)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, tokenize_kernel<CH, G, BIG, WIDE, SW, RAW, SOLO>, 64, block_lds_bytes<CH, G>()) != hipSuccess || nb <= 0)
         nb = 8;
     if (const char *e = getenv("DPT_WAVES_PER_CU")) {
         const int v = atoi(e);
@@ -3341,11 +3403,11 @@ static unsigned resident_per_cu() {
 }
 
 // Persistent grid: every resident wave pulls strings from the work counter until it runs dry.
-template <int CH, int G, bool BIG, bool WIDE, int SW = 0, bool RAW = false>
+template <int CH, int G, bool BIG, bool WIDE, int SW = 0, bool RAW = false, bool SOLO = false>
 static void launch_tok(const EncodeArgs &a, const TrieView &tv, uint64_t n_units, unsigned n_cu, hipStream_t stream,
                        hipEvent_t ev_start = nullptr) {
     constexpr int lds = block_lds_bytes<CH, G>();
-    uint64_t wpc = resident_per_cu<CH, G, BIG, WIDE, SW, RAW>();
+    uint64_t wpc = resident_per_cu<CH, G, BIG, WIDE, SW, RAW, SOLO>();
     static const bool small_rule = getenv("DPT_NO_SMALL_WPC") == nullptr;   // (A/B: the rule below off)
     if (G == 16 && !BIG && small_rule) {
         // small calls: no more resident waves than give every slot ~7 strings (rounds of 4 strings per
@@ -3369,10 +3431,10 @@ static void launch_tok(const EncodeArgs &a, const TrieView &tv, uint64_t n_units
     if (blocks > (uint64_t)n_cu * 64u) blocks = (uint64_t)n_cu * 64u;   // the scratch is sized for 64 per CU
     if (blocks > n_units) blocks = n_units ? n_units : 1;
     if (ev_start)   // the start timestamp rides on the dispatch (a separate hipEventRecord left a ~6 us bubble)
-        hipExtLaunchKernelGGL((tokenize_kernel<CH, G, BIG, WIDE, SW, RAW>), dim3((unsigned)blocks), dim3(64), lds, stream,
+        hipExtLaunchKernelGGL((tokenize_kernel<CH, G, BIG, WIDE, SW, RAW, SOLO>), dim3((unsigned)blocks), dim3(64), lds, stream,
                               ev_start, nullptr, 0, KernArgs{a, tv});
     else
-        hipLaunchKernelGGL((tokenize_kernel<CH, G, BIG, WIDE, SW, RAW>), dim3((unsigned)blocks), dim3(64), lds, stream, KernArgs{a, tv});
+        hipLaunchKernelGGL((tokenize_kernel<CH, G, BIG, WIDE, SW, RAW, SOLO>), dim3((unsigned)blocks), dim3(64), lds, stream, KernArgs{a, tv});
 }
 
 hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t ev[2]) {
@@ -3425,7 +3487,12 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
             if (p.variant == KERNEL_ROWS16) {
                 // the hot kernel gets the staged id width as a template constant
                 const uint64_t nu = (p.n_str + 3) / 4;
-                if (wide) {
+                static const bool solo_wave = getenv("DPT_NO_SOLO_WAVE") == nullptr;   // (A/B: solo calls on 16-lane rows)
+                if (solo && !wide && solo_wave) {
+                    // the one-string kernel: lane-mode B and its C1 walks over the whole wave (forward_lanes, SOLO)
+                    if (raw) launch_tok<SMALL_CH, 16, false, false, 2, true, true>(a, tv, 1, n_cu, stream, e0);
+                    else launch_tok<SMALL_CH, 16, false, false, 2, false, true>(a, tv, 1, n_cu, stream, e0);
+                } else if (wide) {
                     if (st16) launch_tok<SMALL_CH, 16, false, true, 1>(a, tv, nu, n_cu, stream, e0);
                     else launch_tok<SMALL_CH, 16, false, true, 2>(a, tv, nu, n_cu, stream, e0);
                 } else if (raw && !generic_raw) {

@@ -291,6 +291,33 @@ class Encoder:
                                          max(n_bytes, 1), _ptr(id_off), _ptr(status), _ptr(capped)), "dpt_encode_host")
         return ids[: int(id_off[-1])], id_off, status[:n], capped[:n]
 
+    def encode_one(self, s: str) -> Tuple[List[int], int]:
+        """One raw-mode string -> (ids, status): the drop-in's per-string call (reference main_analyze_s2orc.py:74-78)
+        with as little host work as a ctypes call allows -- the UTF-8 bytes passed as they are, the offsets,
+        outputs and their pointers kept from the previous call (dpt_encode_host runs it as one zero-copy launch)."""
+        b = s.encode("utf-8", "surrogatepass")
+        n = len(b)
+        one = self.__dict__.get("_one")
+        if one is None or one[0] < n + 1:
+            cap = max(4096, 2 * n + 2)
+            ids = np.empty(cap, dtype=np.int32)
+            off = np.zeros(4, dtype=np.uint64)   # [0:2] the string's offsets (in), [2:4] id_off (out)
+            st = np.empty(2, dtype=np.int32)
+            L = _lib.lib()
+            fn = ctypes.cast(L.dpt_encode_host, ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                                                 ctypes.c_char_p, ctypes.c_uint64, ctypes.c_void_p,
+                                                                 ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                                                 ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                                                 ctypes.c_void_p))
+            one = self._one = (cap, ids, off, st, fn, off.ctypes.data, ids.ctypes.data, st.ctypes.data,
+                               st.ctypes.data + 4, off.ctypes.data + 16)
+        cap, ids, off, st, fn, p_off, p_ids, p_st, p_cap, p_idoff = one
+        off[1] = n
+        rc = fn(self.handle, self.vocab.handle, DPT_MODE_RAW, b, n, p_off, None, 1, p_ids, max(n, 1), p_idoff, p_st, p_cap)
+        if rc != _lib.DPT_OK:
+            check(rc, "dpt_encode_host")
+        return ids[:int(off[3])].tolist(), int(st[0])
+
     def encode_strs(self, texts: Sequence[str]) -> List[Tuple[List[int], int]]:
         text, offs = pack_strings(texts)
         ids, id_off, st, _ = self.encode_csr(text, offs)

@@ -177,8 +177,14 @@ def dp_tokenize_llama(llama_tokenizer, pretokenize_option="llama"):
         def encode_many(texts):
             raise NameError("name 'pretokenize_func' is not defined")
 
-    def dp_tokenize(input_str) -> List[int]:
-        return encode_many([input_str])[0]
+    if pretokenize_option == "raw":
+        def dp_tokenize(input_str) -> List[int]:
+            ids, st = engine.encode_one(input_str)   # (the per-string call: one zero-copy launch)
+            raise_for_status(st, input_str)
+            return ids
+    else:
+        def dp_tokenize(input_str) -> List[int]:
+            return encode_many([input_str])[0]
 
     def decode_dp_tokenization(encoding: List[int]):
         # reference tokenizer_utils.py:82-84: drop the 4-character "<s> " prefix

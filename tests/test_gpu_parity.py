@@ -809,3 +809,32 @@ def test_bloom_words_across_windows():
     ref = oracle.OracleVocab(t2i).encode_csr(text, offs, mode=oracle.ATOMS, cut_mask=cut)
     _cmp_csr(got, ref)
     assert (got[2] == 0).sum() > 2500
+
+
+def test_one_string_calls_vs_oracle(engines, oracles):
+    """The drop-in's per-string call (reference main_analyze_s2orc.py:74-78: one dp_tokenize(str) per row) runs the
+    one-string kernel -- lane-mode B and its C1 walks across the whole wave (SOLO) -- when the host's scan rules out
+    the long-word passes: raw-mode strings of every corpus shape and llama-mode (PRESPLIT) ones, one call each,
+    against the oracle (multi-window abstracts, Arabic, the golden edge cases, tie-heavy toy strings)."""
+    from dptok import synth
+    from oracle import oracle
+    texts = synth.unpack(*synth.random_ascii_corpus(120, 256, seed=31))
+    texts += synth.unpack(*synth.s2orc_like_corpus(40, seed=32))
+    texts += synth.unpack(*synth.arabic_corpus(60, seed=33))
+    texts += [c["text"] for c in load_golden("edge_llama32k.json.gz")["cases"] if not c.get("skipped")]
+    for name in ("llama32k", "toy1k"):
+        enc, ov = engines[name], oracles[name]
+        for t in texts:
+            got = enc.encode_strs([t])[0]
+            rids, roff, rst, _ = ov.encode_csr(*_csr([t]))
+            assert got == (rids[int(roff[0]):int(roff[1])].tolist(), int(rst[0])), (name, t[:60])
+    # llama mode: one pre-split string per call (the '▁'-compressed windows included)
+    text, offs = synth.random_ascii_corpus(60, 256, seed=34)
+    t2, o2, cut = synth.llama_words(text, offs)
+    enc, ov = engines["llama32k"], oracles["llama32k"]
+    for i in range(60):
+        a, b = int(o2[i]), int(o2[i + 1])
+        one = np.array([0, b - a], dtype=np.uint64)
+        got = enc.encode_csr(t2[a:b], one, mode="presplit", cut_mask=cut[a:b])
+        ref = ov.encode_csr(t2[a:b], one, mode=oracle.PRESPLIT, cut_mask=cut[a:b])
+        _cmp_csr(got, ref)
