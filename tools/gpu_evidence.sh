@@ -22,7 +22,7 @@ bash tools/pmc.sh $tag > $out/pmc.log 2>&1 || { tail -20 $out/pmc.log; exit 1; }
 cp gpurun_out/pmc_$tag/summary.txt $out/pmc_summary.txt 2>/dev/null
 fi
 [ $part = 1 ] && exit 0
-for wl in cfg1 cfg4 cfg5 bloom; do
+for wl in cfg1 cfg4 cfg5 bloom cfg2p cfg4p; do
   timeout -k 10 400 python -u bench.py --workload $wl --steps 10 --warmup 3 > $out/bench_$wl.log 2>&1 || { tail -20 $out/bench_$wl.log; exit 1; }
   tail -1 $out/bench_$wl.log > $out/bench_$wl.json
 done
@@ -35,6 +35,10 @@ for r in 1 2 3; do   # (three runs in one lease: the drop-in's spread across run
   tail -1 $out/host_$r.log > $out/host_path_$r.json
 done
 timeout -k 10 300 python tools/percall.py 3000 > $out/percall.json 2>/dev/null || { echo percall failed; exit 1; }
+# llama mode (PRESPLIT, cfg4p): kernel trace + PMC summary of its first pass
+bash tools/pmc.sh ${tag}_cfg4p 200000 s2orcp > $out/pmc_cfg4p.log 2>&1 || { tail -20 $out/pmc_cfg4p.log; exit 1; }
+cp gpurun_out/pmc_${tag}_cfg4p/summary.txt $out/pmc_cfg4p_summary.txt 2>/dev/null
+find gpurun_out/pmc_${tag}_cfg4p/trace -name "*kernel_stats.csv" | head -1 | xargs -I{} cp {} $out/cfg4p_kernel_stats.csv
 for f in $(ls $out/bench.json $out/bench_*.json $out/strong_*.json 2>/dev/null); do
   python3 -c "import json; d=json.loads(open('$f').read()); print('$f', '%.2f GB/s' % (d['value']/1e9), 'ms/step %.4f' % d['ms_per_step'], 'exact', d['exact_match']['rate'], d['exact_match']['sample'], 'tok ms %.4f' % d['stage_ms_per_step']['tokenize'], 'frac %.4f' % d['roofline']['frac'], 'traffic', d['roofline'].get('traffic'))"
 done

@@ -62,7 +62,10 @@ def main():
     # after prep (-DDPT_STOP=1, `make variant V=stop1`) reads exactly the text (aligned dword buffer loads,
     # n x 256 B) and the offsets (8 (n+1) B) from HBM -- the trie tables stay in L2 -- so known bytes /
     # its raw FETCH_SIZE is the factor for the full kernel's fetches (the guide's x2 is for 16-B streams)
-    stop1 = os.path.join(ROOT, "dp-tokenization_amd", "csrc", "build", "var_stop1", "libdpt.so")
+    # (ablibs/ travels to the GPU box; csrc/build/ is in .gpurunignore)
+    stop1 = os.path.join(ROOT, "ablibs", "libdpt_stop1.so")
+    if not os.path.exists(stop1):
+        stop1 = os.path.join(ROOT, "dp-tokenization_amd", "csrc", "build", "var_stop1", "libdpt.so")
     known = n * 256 + 8 * (n + 1)
     factor, cal = 2.0, None
     if os.path.exists(stop1):

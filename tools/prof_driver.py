@@ -16,6 +16,10 @@ if gen == "bloom":
     t2i = big_vocab()
 else:
     t2i = synth.llama_shaped_vocab()
+presplit = gen.endswith("p")   # ascii / s2orc in llama mode (bench --workload cfg2p / cfg4p): dptok.synth.llama_words
+if presplit:
+    gen = gen[:-1]
+    cache = "/tmp/dpt_corpus_%s_%d.npz" % (gen, n)
 if gen != "ascii" and os.path.exists(cache):
     z = np.load(cache)
     text, offs = z["text"], z["offs"]
@@ -34,6 +38,8 @@ else:
     np.savez(cache, text=text, offs=offs)
 if len(sys.argv) > 4 and sys.argv[4] == "gen-only":   # run without a profiler first: the forks happen here
     sys.exit(0)
+if presplit:
+    text, offs, cut = synth.llama_words(text, offs)
 import torch  # noqa: E402
 from dptok import Encoder, Vocab  # noqa: E402
 enc = Encoder(Vocab(t2i, 0))
@@ -46,6 +52,7 @@ s = torch.cuda.current_stream().cuda_stream
 dc = torch.from_numpy(cut).to(dev) if cut is not None else None
 for _ in range(reps):
     enc.encode_device(dt.data_ptr(), nb, do.data_ptr(), n, ids.data_ptr(), nb, io.data_ptr(), st.data_ptr(), stream=s,
-                      cut_ptr=dc.data_ptr() if dc is not None else 0, mode="atoms" if dc is not None else "raw")
+                      cut_ptr=dc.data_ptr() if dc is not None else 0,
+                      mode="presplit" if presplit else ("atoms" if dc is not None else "raw"))
 torch.cuda.synchronize()
 print("tokens", int(io[-1].item()), "bytes", nb)
