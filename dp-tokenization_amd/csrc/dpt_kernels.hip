@@ -1992,14 +1992,17 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                 // one backward pass over the chunk's ends (c0, c1]: the local suffix min of lo
                 // decides the cuts as far as this chunk's ends go; the later chunks' ends (min S)
                 // then only cap them: p is a cut iff both mins are >= p, i.e. p <= S
-                unsigned mloc = 0xFFFFu, lcut = 0;
+                // (the 512-byte pass's chunks have up to 33 boundaries: a 64-bit cut mask there)
+                using CutM = std::conditional_t<(CMAX > 32u), uint64_t, uint32_t>;
+                unsigned mloc = 0xFFFFu;
+                CutM lcut = 0;
 #pragma unroll 4
                 for (int k = (int)CMAX - 1; k >= 0; k--) {
                     const unsigned i = c0 + 1u + (unsigned)k;
                     if (i <= c1) {
                         const unsigned hb = 31u - (unsigned)__builtin_clz((~rec32[i] >> 16) | 1u);   // bit 0 is set in a capless window
                         mloc = min(mloc, i - 1u - hb);
-                        if (mloc >= i - 1u) lcut |= 1u << k;   // boundary p = i-1 = c0+k < c1
+                        if (mloc >= i - 1u) lcut |= (CutM)1 << k;   // boundary p = i-1 = c0+k < c1
                     }
                 }
                 // min lo over the later lanes of the group (shift left: lane l reads lane l+k)
@@ -2014,9 +2017,11 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                 }
                 const unsigned S = gshl<LW, 1>(sm, 0xFFFFu);
                 // boundaries c0 + k <= S
-                const unsigned cut = S < c0 ? 0u : (S - c0 >= CMAX - 1u ? lcut : lcut & ((2u << (S - c0)) - 1u));
+                const CutM cut = S < c0 ? (CutM)0 : (S - c0 >= CMAX - 1u ? lcut : lcut & (((CutM)2 << (S - c0)) - 1u));
                 // rs = the first cut at or after c0 (in this lane's chunk or a later one; na is a cut)
-                unsigned rs = cut ? c0 + ffbl(cut) : na;
+                unsigned rs = na;
+                if constexpr (CMAX > 32u) rs = cut ? c0 + (unsigned)__builtin_ctzll(cut) : na;
+                else rs = cut ? c0 + ffbl(cut) : na;
                 rs = min(rs, gshl<LW, 1>(rs, na));
                 rs = min(rs, gshl<LW, 2>(rs, na));
                 rs = min(rs, gshl<LW, 4>(rs, na));
@@ -2030,7 +2035,9 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                     // chunk of a wave ~2x the mean on cfg4's long words (a 256-atom window: 36.7 ends
                     // against C = 17), and the wave steps as long as its longest chunk; nearest-cut
                     // rounding is monotone in c0, so the chunks still tile (0, na]
-                    const unsigned lastc = cut ? c0 + (31u - (unsigned)__builtin_clz(cut)) : 0u;   // (0 is a cut)
+                    unsigned lastc = 0;   // (0 is a cut)
+                    if constexpr (CMAX > 32u) lastc = cut ? c0 + (63u - (unsigned)__builtin_clzll(cut)) : 0u;
+                    else lastc = cut ? c0 + (31u - (unsigned)__builtin_clz((unsigned)cut)) : 0u;
                     unsigned pm = lastc;   // max over the lanes <= d of the group, then shifted: lanes < d
                     pm = max(pm, gshr<LW, 1>(pm, 0u));
                     pm = max(pm, gshr<LW, 2>(pm, 0u));

@@ -838,3 +838,46 @@ def test_one_string_calls_vs_oracle(engines, oracles):
         got = enc.encode_csr(t2[a:b], one, mode="presplit", cut_mask=cut[a:b])
         ref = ov.encode_csr(t2[a:b], one, mode=oracle.PRESPLIT, cut_mask=cut[a:b])
         _cmp_csr(got, ref)
+
+
+def test_mid_pass_words_257_to_512_bytes(engines, oracles):
+    """The 512-byte pass (mid_kernel: PRESPLIT / ATOMS calls of 16-lane vocabularies) takes the strings whose word
+    does not fit the first pass's 256-byte window: words of 200..530 bytes (its lane-mode B has chunks of up to 33
+    boundaries), mixed with short ones, with and without '▁' markers, in PRESPLIT and ATOMS mode -- against the
+    oracle; words over 512 bytes go on to the 2048-byte pass."""
+    from dptok.engine import pack_word_atoms
+    from oracle import oracle
+    rng = np.random.default_rng(41)
+    alpha = [chr(c) for c in range(0x21, 0x7F)]
+    strings = []
+    for k in range(600):
+        words = []
+        for _ in range(int(rng.integers(1, 4))):
+            L = int(rng.integers(200, 531)) if rng.random() < 0.6 else int(rng.integers(1, 40))
+            w = "".join(rng.choice(alpha, size=L))
+            words.append(("▁" + w) if (words and k % 2) else w)
+        strings.append(words)
+    enc, ov = engines["llama32k"], oracles["llama32k"]
+    # PRESPLIT: words as UTF-8 text + a word-start mask
+    parts, cuts = [], []
+    for words in strings:
+        b = bytearray(); c = bytearray()
+        for w in words:
+            e = w.encode("utf-8")
+            c += b"\x01" + b"\x00" * (len(e) - 1)
+            b += e
+        parts.append(bytes(b)); cuts.append(bytes(c))
+    offs = np.zeros(len(parts) + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([len(p) for p in parts], dtype=np.uint64)
+    text = np.frombuffer(b"".join(parts), dtype=np.uint8).copy()
+    cut = np.frombuffer(b"".join(cuts), dtype=np.uint8).copy()
+    got = enc.encode_csr(text, offs, mode="presplit", cut_mask=cut)
+    ref = ov.encode_csr(text, offs, mode=oracle.PRESPLIT, cut_mask=cut)
+    _cmp_csr(got, ref)
+    assert np.array_equal(got[3], ref[3])
+    assert (got[2] == 0).sum() > 500
+    # ATOMS: the same words, every code point an atom
+    t2, o2, c2 = pack_word_atoms([[list(w) for w in words] for words in strings])
+    got = enc.encode_csr(t2, o2, mode="atoms", cut_mask=c2)
+    ref = ov.encode_csr(t2, o2, mode=oracle.ATOMS, cut_mask=c2)
+    _cmp_csr(got, ref)
