@@ -320,7 +320,7 @@ constexpr int group_lds_bytes() { return (int)((sizeof(GroupLDS<CH, G>) + 15) & 
 // 2-way bank conflicts; interleaved, the same bytes are conflict-free.
 template <int CH, int G>
 constexpr int group_stride() { return group_lds_bytes<CH, G>() + (int)sizeof(SlotState); }
-static_assert(group_stride<256, 16>() == 1856, "16-lane group stride: 22 waves per CU, slots 16 dwords mod 32 apart");
+static_assert(group_stride<256, 16>() == 1856, "16-lane group stride: 21 resident waves per CU (512-B LDS granule), slots 16 dwords mod 32 apart");
 template <int CH, int G>
 constexpr int block_lds_bytes() { return (64 / G) * group_stride<CH, G>(); }
 
@@ -901,6 +901,12 @@ constexpr unsigned A_REFILL64 = 32;   // the same for the 64-lane kernels (8 / 1
 // Waves per SIMD by VGPRs (<= 80 VGPRs each).  The 256-byte 16-lane rows: LDS (22 waves per CU) then
 // binds (96 VGPRs / 5 waves: no scratch spills, cfg2 -1.9 %, r03e).  The 256-byte 64-lane kernel: BLOOM
 // 17.4 -> 19.8 GB/s against no cap (95 VGPRs, 20 waves; 7 or 8 waves spill more: r03aa, r03ac).
+#ifndef DPT_WPC_LO      // small calls: the persistent grid's fewest resident waves per CU (launch_tok)
+#define DPT_WPC_LO 20
+#endif
+#ifndef DPT_WPC_GRAN    // LDS allocation granule (bytes) that caps the resident waves per CU (resident_per_cu)
+#define DPT_WPC_GRAN 512
+#endif
 #ifndef DPT_WPE16
 #define DPT_WPE16 6
 #endif
@@ -3401,6 +3407,13 @@ static unsigned resident_per_cu() {
     int nb = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, tokenize_kernel<CH, G, BIG, WIDE, SW, RAW, SOLO>, 64, block_lds_bytes<CH, G>()) != hipSuccess || nb <= 0)
         nb = 8;
+    {   // the residency by LDS at its 512-byte allocation granule: the occupancy API counts 22 blocks of
+        // 7 424 B per CU, the timeline shows 21 resident and the 22nd starting only when another exits
+        // (profiles/r06_ab.log r06b; 21 against 22 at 175k / 250k: +0.9 %, r06o)
+        constexpr int g = DPT_WPC_GRAN;
+        const int fit = (160 * 1024) / ((block_lds_bytes<CH, G>() + g - 1) / g * g);
+        if (fit < nb) nb = fit;
+    }
     if (const char *e = getenv("DPT_WAVES_PER_CU")) {
         const int v = atoi(e);
         if (v > 0) nb = v;
@@ -3421,11 +3434,13 @@ static void launch_tok(const EncodeArgs &a, const TrieView &tv, uint64_t n_units
         // wave; a wave's last round is the tail): 125k strings run 3 % faster at 18 waves per CU than
         // at the occupancy limit of 22, 250k and more are fastest at 22 (profiles/r02_ab_issue_model.log)
         const uint64_t want = (n_units + 7ull * n_cu - 1) / (7ull * n_cu);   // n_units = strings / 4
-        const uint64_t lo = wpc < 16u ? wpc : 16u;
+        const uint64_t lo = wpc < DPT_WPC_LO ? wpc : DPT_WPC_LO;
         if (want < wpc) {
             // of the wave counts from lo up, the one with the fewest slot-rounds w * ceil(rounds) -- the
-            // work plus the idle part of the last round -- the smallest on ties (100k strings: 16 waves
-            // per CU ran 6.1 rounds, a last round 10 % full; 125k keeps 18)
+            // work plus the idle part of the last round -- the smallest on ties (100k strings: 20 waves
+            // per CU, 4.9 rounds).  lo = 20: a CU's string throughput grows up to 20-21 waves (r06c:
+            // 0.411 / 0.424 / 0.431 / 0.434 string-rounds per us at 18..21), which a shorter last
+            // round at 16-18 waves does not pay back (125k: 18 -> 21 waves, +1.9 %, r06o)
             uint64_t best = lo, bc = ~0ull;
             for (uint64_t w = lo; w <= wpc; w++) {
                 const uint64_t c = w * ((n_units + w * n_cu - 1) / (w * n_cu));
