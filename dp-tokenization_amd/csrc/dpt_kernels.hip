@@ -966,7 +966,7 @@ __device__ __forceinline__ void reset_counters(uint32_t *ctr, uint64_t *snap = n
 // The body of tokenize_kernel (and of fallback_kernel's 2048-byte blocks); bid: the block's index
 // among the blocks running it.  The kernel arguments start with a KernArgs (read through the kernarg
 // segment pointer, KREFRESH).
-template <int CH, int G, bool BIG, bool WIDE, int SW = 0, bool RAW = false, bool SOLO = false>
+template <int CH, int G, bool BIG, bool WIDE, int SW = 0, bool RAW = false, bool SOLO = false, bool PS = false>
 __device__ __forceinline__ void tokenize_body(const unsigned bid) {
     ConstKernArgs *kp = (ConstKernArgs *)__builtin_amdgcn_kernarg_segment_ptr();
 #define a (kp->ea)
@@ -994,7 +994,8 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
     const uint64_t base_off = a.str_off[0];
     // (the other instantiations keep the mode a run-time value: folding raw = false into the atoms-mode
     // 16-lane kernel crashes ROCm 7.2's greedy register allocator)
-    const int mode = RAW ? 0 : (a.mode & DPT_MODE_MASK);
+    // RAW / PS: raw / PRESPLIT mode as a compile-time constant (the other instantiations read it)
+    const int mode = RAW ? 0 : (PS ? 1 : (a.mode & DPT_MODE_MASK));
     const bool raw = mode == 0;
     const bool uncapped = (a.mode & DPT_FLAG_UNCAPPED) != 0;   // f2: inspect_tokenizer's inf-initialised DP
     const bool len_only = (a.mode & (DPT_FLAG_UNCAPPED | DPT_FLAG_LEN_ONLY)) != 0;
@@ -2977,11 +2978,11 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
 #undef tv
 }
 
-template <int CH, int G, bool BIG, bool WIDE, int SW = 0, bool RAW = false, bool SOLO = false>
+template <int CH, int G, bool BIG, bool WIDE, int SW = 0, bool RAW = false, bool SOLO = false, bool PS = false>
 // (the one-string kernel, SOLO, is one wave: no occupancy to keep, so no VGPR cap and no spills)
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SOLO ? 1 : ((CH == 256 && G == 16) ? WPE16 : ((CH == 256 && G == 64) ? WPE64 : 1)))))
 tokenize_kernel(KernArgs ka) {
-    tokenize_body<CH, G, BIG, WIDE, SW, RAW, SOLO>(blockIdx.x);
+    tokenize_body<CH, G, BIG, WIDE, SW, RAW, SOLO, PS>(blockIdx.x);
 }
 
 // ------------------------------------------------------------------ compaction
@@ -3398,14 +3399,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) mi
 
 constexpr int MAX_DEVICES = 64;
 // Resident waves per CU for an instantiation (LDS / VGPR limited); DPT_WAVES_PER_CU overrides.
-template <int CH, int G, bool BIG, bool WIDE, int SW = 0, bool RAW = false, bool SOLO = false>
+template <int CH, int G, bool BIG, bool WIDE, int SW = 0, bool RAW = false, bool SOLO = false, bool PS = false>
 static unsigned resident_per_cu() {
     static unsigned cached[MAX_DEVICES] = {};   // per device: a process may drive several
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAX_DEVICES) dev = 0;
     if (cached[dev]) return cached[dev];
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, tokenize_kernel<CH, G, BIG, WIDE, SW, RAW, SOLO>, 64, block_lds_bytes<CH, G>()) != hipSuccess || nb <= 0)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, tokenize_kernel<CH, G, BIG, WIDE, SW, RAW, SOLO, PS>, 64, block_lds_bytes<CH, G>()) != hipSuccess || nb <= 0)
         nb = 8;
     {   // the residency by LDS at its 512-byte allocation granule: the occupancy API counts 22 blocks of
         // 7 424 B per CU, the timeline shows 21 resident and the 22nd starting only when another exits
@@ -3423,11 +3424,11 @@ static unsigned resident_per_cu() {
 }
 
 // Persistent grid: every resident wave pulls strings from the work counter until it runs dry.
-template <int CH, int G, bool BIG, bool WIDE, int SW = 0, bool RAW = false, bool SOLO = false>
+template <int CH, int G, bool BIG, bool WIDE, int SW = 0, bool RAW = false, bool SOLO = false, bool PS = false>
 static void launch_tok(const EncodeArgs &a, const TrieView &tv, uint64_t n_units, unsigned n_cu, hipStream_t stream,
                        hipEvent_t ev_start = nullptr) {
     constexpr int lds = block_lds_bytes<CH, G>();
-    uint64_t wpc = resident_per_cu<CH, G, BIG, WIDE, SW, RAW, SOLO>();
+    uint64_t wpc = resident_per_cu<CH, G, BIG, WIDE, SW, RAW, SOLO, PS>();
     static const bool small_rule = getenv("DPT_NO_SMALL_WPC") == nullptr;   // (A/B: the rule below off)
     if (G == 16 && !BIG && small_rule) {
         // small calls: no more resident waves than give every slot ~7 strings (rounds of 4 strings per
@@ -3453,10 +3454,10 @@ static void launch_tok(const EncodeArgs &a, const TrieView &tv, uint64_t n_units
     if (blocks > (uint64_t)n_cu * 64u) blocks = (uint64_t)n_cu * 64u;   // the scratch is sized for 64 per CU
     if (blocks > n_units) blocks = n_units ? n_units : 1;
     if (ev_start)   // the start timestamp rides on the dispatch (a separate hipEventRecord left a ~6 us bubble)
-        hipExtLaunchKernelGGL((tokenize_kernel<CH, G, BIG, WIDE, SW, RAW, SOLO>), dim3((unsigned)blocks), dim3(64), lds, stream,
+        hipExtLaunchKernelGGL((tokenize_kernel<CH, G, BIG, WIDE, SW, RAW, SOLO, PS>), dim3((unsigned)blocks), dim3(64), lds, stream,
                               ev_start, nullptr, 0, KernArgs{a, tv});
     else
-        hipLaunchKernelGGL((tokenize_kernel<CH, G, BIG, WIDE, SW, RAW, SOLO>), dim3((unsigned)blocks), dim3(64), lds, stream, KernArgs{a, tv});
+        hipLaunchKernelGGL((tokenize_kernel<CH, G, BIG, WIDE, SW, RAW, SOLO, PS>), dim3((unsigned)blocks), dim3(64), lds, stream, KernArgs{a, tv});
 }
 
 hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t ev[2]) {
@@ -3506,6 +3507,8 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
             const unsigned n_cu = p.max_blocks / 64;
             // A/B knob (diagnostic): raw mode through the generic 16-lane kernel (r06i: cfg2 +9 %, cfg4 +7 %)
             static const bool generic_raw = getenv("DPT_GENERIC_RAW") != nullptr;
+            static const bool generic_ps = getenv("DPT_GENERIC_PS") != nullptr;   // (A/B: PRESPLIT on the generic kernel)
+            const bool presplit = (p.mode & DPT_MODE_MASK) == DPT_MODE_PRESPLIT;
             if (p.variant == KERNEL_ROWS16) {
                 // the hot kernel gets the staged id width as a template constant
                 const uint64_t nu = (p.n_str + 3) / 4;
@@ -3520,6 +3523,9 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
                 } else if (raw && !generic_raw) {
                     if (st16) launch_tok<SMALL_CH, 16, false, false, 1, true>(a, tv, nu, n_cu, stream, e0);
                     else launch_tok<SMALL_CH, 16, false, false, 2, true>(a, tv, nu, n_cu, stream, e0);
+                } else if (presplit && !generic_ps) {
+                    if (st16) launch_tok<SMALL_CH, 16, false, false, 1, false, false, true>(a, tv, nu, n_cu, stream, e0);
+                    else launch_tok<SMALL_CH, 16, false, false, 2, false, false, true>(a, tv, nu, n_cu, stream, e0);
                 } else {
                     if (st16) launch_tok<SMALL_CH, 16, false, false, 1>(a, tv, nu, n_cu, stream, e0);
                     else launch_tok<SMALL_CH, 16, false, false, 2>(a, tv, nu, n_cu, stream, e0);

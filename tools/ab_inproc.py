@@ -2,7 +2,7 @@
 
     python tools/ab_inproc.py <workload> <n_strings> <rounds> lib1.so lib2.so ...
 
-workload: ascii (cfg2), s2orc (cfg4), arabic (cfg5), bloom.  The corpus is generated and uploaded
+workload: ascii (cfg2), s2orc (cfg4), arabic (cfg5), bloom; ascii_p / s2orc_p: llama mode (cfg2p / cfg4p).  The corpus is generated and uploaded
 ONCE; every library gets its own vocab + ctx (ctypes.CDLL: each build's kernels in their own
 namespace, one HIP runtime -- torch's); each round times K encodes of every library back to back
 (HIP events on the stream), so drift of the box hits all of them alike.  Outputs of every library
@@ -30,6 +30,10 @@ def corpus(gen, n):
         text, offs, cut = synth.bloom_like_parallel(n, t2i, procs=16, length=256)
     else:
         t2i = synth.llama_shaped_vocab()
+        if gen.endswith("_p"):   # llama mode (PRESPLIT): the same corpus pre-split as bench.py's cfg2p / cfg4p
+            _, text, offs, _ = corpus(gen[:-2], n)
+            text, offs, cut = synth.llama_words(text, offs)
+            return t2i, text, offs, cut
         if gen == "ascii":
             text, offs = synth.random_ascii_corpus(n, 256, seed=1)
         elif gen == "s2orc":
@@ -51,7 +55,7 @@ def main():
     dt = torch.from_numpy(text).to(dev)
     do = torch.from_numpy(offs.view(np.int64)).to(dev)
     dc = torch.from_numpy(cut).to(dev) if cut is not None else None
-    mode = 2 if cut is not None else 0
+    mode = (1 if gen.endswith("_p") else 2) if cut is not None else 0
     toks = list(t2i.keys())
     encs = [encode_utf8(t) for t in toks]
     boff = np.zeros(len(encs) + 1, dtype=np.uint64)
