@@ -3392,9 +3392,9 @@ static_assert(block_lds_bytes<MID_CH, 16>() <= 64 * 1024, "mid LDS");
 // pass (the generic walker, C2's hash pass and walkers: no A0 / bulk pass), ~7 waves per CU (LDS); its own
 // failures go on to the 2048-byte pass.  A persistent grid over the list: with no retries every wave reads
 // a zero count and exits.
-template <int SW, bool WIDE>
+template <int SW, bool WIDE, bool PS = false>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) mid_kernel(KernArgs ka) {
-    tokenize_body<MID_CH, 16, true, WIDE, SW, false>(blockIdx.x);
+    tokenize_body<MID_CH, 16, true, WIDE, SW, false, false, PS>(blockIdx.x);
 }
 
 constexpr int MAX_DEVICES = 64;
@@ -3502,13 +3502,14 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     }
     // profiling (dpt_ctx_profile): the first pass's dispatch records ev[0], the unbounded pass's ev[1]
     hipEvent_t e0 = ev ? ev[0] : nullptr;
+    // llama mode (PRESPLIT) runs its own instantiations of the 16-lane passes (the PS template flag)
+    static const bool generic_ps = getenv("DPT_GENERIC_PS") != nullptr;   // (A/B: PRESPLIT on the generic kernels)
+    const bool presplit = (p.mode & DPT_MODE_MASK) == DPT_MODE_PRESPLIT;
     if (p.n_str > 0) {
         {
             const unsigned n_cu = p.max_blocks / 64;
             // A/B knob (diagnostic): raw mode through the generic 16-lane kernel (r06i: cfg2 +9 %, cfg4 +7 %)
             static const bool generic_raw = getenv("DPT_GENERIC_RAW") != nullptr;
-            static const bool generic_ps = getenv("DPT_GENERIC_PS") != nullptr;   // (A/B: PRESPLIT on the generic kernel)
-            const bool presplit = (p.mode & DPT_MODE_MASK) == DPT_MODE_PRESPLIT;
             if (p.variant == KERNEL_ROWS16) {
                 // the hot kernel gets the staged id width as a template constant
                 const uint64_t nu = (p.n_str + 3) / 4;
@@ -3566,7 +3567,8 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
             uint64_t mb = (uint64_t)(p.max_blocks / 64) * mid_per_cu[dev];
             mb = mb < p.n_str ? mb : p.n_str;
             constexpr int mlds = block_lds_bytes<MID_CH, 16>();
-            auto mk = st16 ? (wide ? mid_kernel<1, true> : mid_kernel<1, false>) : (wide ? mid_kernel<2, true> : mid_kernel<2, false>);
+            auto mk = st16 ? (wide ? mid_kernel<1, true> : (presplit && !generic_ps) ? mid_kernel<1, false, true> : mid_kernel<1, false>)
+                           : (wide ? mid_kernel<2, true> : (presplit && !generic_ps) ? mid_kernel<2, false, true> : mid_kernel<2, false>);
             hipLaunchKernelGGL(mk, dim3((unsigned)(mb ? mb : 1)), dim3(64), mlds, stream, KernArgs{m, tv});
             b.work_list = m.retry_list; b.work_count = m.retry_count;
         }
