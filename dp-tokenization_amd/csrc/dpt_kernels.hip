@@ -966,7 +966,7 @@ __device__ __forceinline__ void reset_counters(uint32_t *ctr, uint64_t *snap = n
 // The body of tokenize_kernel (and of fallback_kernel's 2048-byte blocks); bid: the block's index
 // among the blocks running it.  The kernel arguments start with a KernArgs (read through the kernarg
 // segment pointer, KREFRESH).
-template <int CH, int G, bool BIG, bool WIDE, int SW = 0, bool RAW = false, bool SOLO = false, bool PS = false>
+template <int CH, int G, bool BIG, bool WIDE, int SW = 0, bool RAW = false, bool SOLO = false, int MC = -1>
 __device__ __forceinline__ void tokenize_body(const unsigned bid) {
     ConstKernArgs *kp = (ConstKernArgs *)__builtin_amdgcn_kernarg_segment_ptr();
 #define a (kp->ea)
@@ -994,8 +994,8 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
     const uint64_t base_off = a.str_off[0];
     // (the other instantiations keep the mode a run-time value: folding raw = false into the atoms-mode
     // 16-lane kernel crashes ROCm 7.2's greedy register allocator)
-    // RAW / PS: raw / PRESPLIT mode as a compile-time constant (the other instantiations read it)
-    const int mode = RAW ? 0 : (PS ? 1 : (a.mode & DPT_MODE_MASK));
+    // RAW / MC >= 0: the mode as a compile-time constant (PRESPLIT, ATOMS; the other instantiations read it)
+    const int mode = RAW ? 0 : (MC >= 0 ? MC : (a.mode & DPT_MODE_MASK));
     const bool raw = mode == 0;
     const bool uncapped = (a.mode & DPT_FLAG_UNCAPPED) != 0;   // f2: inspect_tokenizer's inf-initialised DP
     const bool len_only = (a.mode & (DPT_FLAG_UNCAPPED | DPT_FLAG_LEN_ONLY)) != 0;
@@ -2978,11 +2978,11 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
 #undef tv
 }
 
-template <int CH, int G, bool BIG, bool WIDE, int SW = 0, bool RAW = false, bool SOLO = false, bool PS = false>
+template <int CH, int G, bool BIG, bool WIDE, int SW = 0, bool RAW = false, bool SOLO = false, int MC = -1>
 // (the one-string kernel, SOLO, is one wave: no occupancy to keep, so no VGPR cap and no spills)
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SOLO ? 1 : ((CH == 256 && G == 16) ? WPE16 : ((CH == 256 && G == 64) ? WPE64 : 1)))))
 tokenize_kernel(KernArgs ka) {
-    tokenize_body<CH, G, BIG, WIDE, SW, RAW, SOLO, PS>(blockIdx.x);
+    tokenize_body<CH, G, BIG, WIDE, SW, RAW, SOLO, MC>(blockIdx.x);
 }
 
 // ------------------------------------------------------------------ compaction
@@ -3392,21 +3392,21 @@ static_assert(block_lds_bytes<MID_CH, 16>() <= 64 * 1024, "mid LDS");
 // pass (the generic walker, C2's hash pass and walkers: no A0 / bulk pass), ~7 waves per CU (LDS); its own
 // failures go on to the 2048-byte pass.  A persistent grid over the list: with no retries every wave reads
 // a zero count and exits.
-template <int SW, bool WIDE, bool PS = false>
+template <int SW, bool WIDE, int MC = -1>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) mid_kernel(KernArgs ka) {
-    tokenize_body<MID_CH, 16, true, WIDE, SW, false, false, PS>(blockIdx.x);
+    tokenize_body<MID_CH, 16, true, WIDE, SW, false, false, MC>(blockIdx.x);
 }
 
 constexpr int MAX_DEVICES = 64;
 // Resident waves per CU for an instantiation (LDS / VGPR limited); DPT_WAVES_PER_CU overrides.
-template <int CH, int G, bool BIG, bool WIDE, int SW = 0, bool RAW = false, bool SOLO = false, bool PS = false>
+template <int CH, int G, bool BIG, bool WIDE, int SW = 0, bool RAW = false, bool SOLO = false, int MC = -1>
 static unsigned resident_per_cu() {
     static unsigned cached[MAX_DEVICES] = {};   // per device: a process may drive several
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAX_DEVICES) dev = 0;
     if (cached[dev]) return cached[dev];
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, tokenize_kernel<CH, G, BIG, WIDE, SW, RAW, SOLO, PS>, 64, block_lds_bytes<CH, G>()) != hipSuccess || nb <= 0)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, tokenize_kernel<CH, G, BIG, WIDE, SW, RAW, SOLO, MC>, 64, block_lds_bytes<CH, G>()) != hipSuccess || nb <= 0)
         nb = 8;
     {   // the residency by LDS at its 512-byte allocation granule: the occupancy API counts 22 blocks of
         // 7 424 B per CU, the timeline shows 21 resident and the 22nd starting only when another exits
@@ -3424,11 +3424,11 @@ static unsigned resident_per_cu() {
 }
 
 // Persistent grid: every resident wave pulls strings from the work counter until it runs dry.
-template <int CH, int G, bool BIG, bool WIDE, int SW = 0, bool RAW = false, bool SOLO = false, bool PS = false>
+template <int CH, int G, bool BIG, bool WIDE, int SW = 0, bool RAW = false, bool SOLO = false, int MC = -1>
 static void launch_tok(const EncodeArgs &a, const TrieView &tv, uint64_t n_units, unsigned n_cu, hipStream_t stream,
                        hipEvent_t ev_start = nullptr) {
     constexpr int lds = block_lds_bytes<CH, G>();
-    uint64_t wpc = resident_per_cu<CH, G, BIG, WIDE, SW, RAW, SOLO, PS>();
+    uint64_t wpc = resident_per_cu<CH, G, BIG, WIDE, SW, RAW, SOLO, MC>();
     static const bool small_rule = getenv("DPT_NO_SMALL_WPC") == nullptr;   // (A/B: the rule below off)
     if (G == 16 && !BIG && small_rule) {
         // small calls: no more resident waves than give every slot ~7 strings (rounds of 4 strings per
@@ -3454,10 +3454,10 @@ static void launch_tok(const EncodeArgs &a, const TrieView &tv, uint64_t n_units
     if (blocks > (uint64_t)n_cu * 64u) blocks = (uint64_t)n_cu * 64u;   // the scratch is sized for 64 per CU
     if (blocks > n_units) blocks = n_units ? n_units : 1;
     if (ev_start)   // the start timestamp rides on the dispatch (a separate hipEventRecord left a ~6 us bubble)
-        hipExtLaunchKernelGGL((tokenize_kernel<CH, G, BIG, WIDE, SW, RAW, SOLO, PS>), dim3((unsigned)blocks), dim3(64), lds, stream,
+        hipExtLaunchKernelGGL((tokenize_kernel<CH, G, BIG, WIDE, SW, RAW, SOLO, MC>), dim3((unsigned)blocks), dim3(64), lds, stream,
                               ev_start, nullptr, 0, KernArgs{a, tv});
     else
-        hipLaunchKernelGGL((tokenize_kernel<CH, G, BIG, WIDE, SW, RAW, SOLO, PS>), dim3((unsigned)blocks), dim3(64), lds, stream, KernArgs{a, tv});
+        hipLaunchKernelGGL((tokenize_kernel<CH, G, BIG, WIDE, SW, RAW, SOLO, MC>), dim3((unsigned)blocks), dim3(64), lds, stream, KernArgs{a, tv});
 }
 
 hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t ev[2]) {
@@ -3502,8 +3502,8 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     }
     // profiling (dpt_ctx_profile): the first pass's dispatch records ev[0], the unbounded pass's ev[1]
     hipEvent_t e0 = ev ? ev[0] : nullptr;
-    // llama mode (PRESPLIT) runs its own instantiations of the 16-lane passes (the PS template flag)
-    static const bool generic_ps = getenv("DPT_GENERIC_PS") != nullptr;   // (A/B: PRESPLIT on the generic kernels)
+    // PRESPLIT (llama mode) and ATOMS run instantiations with the mode a compile-time constant (MC)
+    static const bool generic_ps = getenv("DPT_GENERIC_PS") != nullptr;   // (A/B: the runtime-mode kernels)
     const bool presplit = (p.mode & DPT_MODE_MASK) == DPT_MODE_PRESPLIT;
     if (p.n_str > 0) {
         {
@@ -3519,14 +3519,19 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
                     if (raw) launch_tok<SMALL_CH, 16, false, false, 2, true, true>(a, tv, 1, n_cu, stream, e0);
                     else launch_tok<SMALL_CH, 16, false, false, 2, false, true>(a, tv, 1, n_cu, stream, e0);
                 } else if (wide) {
-                    if (st16) launch_tok<SMALL_CH, 16, false, true, 1>(a, tv, nu, n_cu, stream, e0);
-                    else launch_tok<SMALL_CH, 16, false, true, 2>(a, tv, nu, n_cu, stream, e0);
+                    if (generic_ps) {
+                        if (st16) launch_tok<SMALL_CH, 16, false, true, 1>(a, tv, nu, n_cu, stream, e0);
+                        else launch_tok<SMALL_CH, 16, false, true, 2>(a, tv, nu, n_cu, stream, e0);
+                    } else {
+                        if (st16) launch_tok<SMALL_CH, 16, false, true, 1, false, false, DPT_MODE_ATOMS>(a, tv, nu, n_cu, stream, e0);
+                        else launch_tok<SMALL_CH, 16, false, true, 2, false, false, DPT_MODE_ATOMS>(a, tv, nu, n_cu, stream, e0);
+                    }
                 } else if (raw && !generic_raw) {
                     if (st16) launch_tok<SMALL_CH, 16, false, false, 1, true>(a, tv, nu, n_cu, stream, e0);
                     else launch_tok<SMALL_CH, 16, false, false, 2, true>(a, tv, nu, n_cu, stream, e0);
                 } else if (presplit && !generic_ps) {
-                    if (st16) launch_tok<SMALL_CH, 16, false, false, 1, false, false, true>(a, tv, nu, n_cu, stream, e0);
-                    else launch_tok<SMALL_CH, 16, false, false, 2, false, false, true>(a, tv, nu, n_cu, stream, e0);
+                    if (st16) launch_tok<SMALL_CH, 16, false, false, 1, false, false, DPT_MODE_PRESPLIT>(a, tv, nu, n_cu, stream, e0);
+                    else launch_tok<SMALL_CH, 16, false, false, 2, false, false, DPT_MODE_PRESPLIT>(a, tv, nu, n_cu, stream, e0);
                 } else {
                     if (st16) launch_tok<SMALL_CH, 16, false, false, 1>(a, tv, nu, n_cu, stream, e0);
                     else launch_tok<SMALL_CH, 16, false, false, 2>(a, tv, nu, n_cu, stream, e0);
@@ -3535,7 +3540,8 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
 #if DPT_STOP == 3   // (this diagnostic build crashes ROCm 7.2's register allocator on the 64-lane first pass)
                 return hipErrorNotSupported;
 #else
-                if (wide) launch_tok<SMALL_CH, 64, false, true>(a, tv, p.n_str, n_cu, stream, e0);
+                if (wide && !generic_ps) launch_tok<SMALL_CH, 64, false, true, 0, false, false, DPT_MODE_ATOMS>(a, tv, p.n_str, n_cu, stream, e0);
+                else if (wide) launch_tok<SMALL_CH, 64, false, true>(a, tv, p.n_str, n_cu, stream, e0);
                 else if (raw) launch_tok<SMALL_CH, 64, false, false, 0, true>(a, tv, p.n_str, n_cu, stream, e0);
                 else launch_tok<SMALL_CH, 64, false, false>(a, tv, p.n_str, n_cu, stream, e0);
 #endif
@@ -3567,8 +3573,10 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
             uint64_t mb = (uint64_t)(p.max_blocks / 64) * mid_per_cu[dev];
             mb = mb < p.n_str ? mb : p.n_str;
             constexpr int mlds = block_lds_bytes<MID_CH, 16>();
-            auto mk = st16 ? (wide ? mid_kernel<1, true> : (presplit && !generic_ps) ? mid_kernel<1, false, true> : mid_kernel<1, false>)
-                           : (wide ? mid_kernel<2, true> : (presplit && !generic_ps) ? mid_kernel<2, false, true> : mid_kernel<2, false>);
+            // (wide <=> ATOMS mode; the mode-constant instantiations unless DPT_GENERIC_PS)
+            auto mk = generic_ps ? (st16 ? (wide ? mid_kernel<1, true> : mid_kernel<1, false>) : (wide ? mid_kernel<2, true> : mid_kernel<2, false>))
+                    : st16 ? (wide ? mid_kernel<1, true, DPT_MODE_ATOMS> : presplit ? mid_kernel<1, false, DPT_MODE_PRESPLIT> : mid_kernel<1, false>)
+                           : (wide ? mid_kernel<2, true, DPT_MODE_ATOMS> : presplit ? mid_kernel<2, false, DPT_MODE_PRESPLIT> : mid_kernel<2, false>);
             hipLaunchKernelGGL(mk, dim3((unsigned)(mb ? mb : 1)), dim3(64), mlds, stream, KernArgs{m, tv});
             b.work_list = m.retry_list; b.work_count = m.retry_count;
         }
