@@ -997,8 +997,11 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
     // RAW / MC >= 0: the mode as a compile-time constant (PRESPLIT, ATOMS; the other instantiations read it)
     const int mode = RAW ? 0 : (MC >= 0 ? MC : (a.mode & DPT_MODE_MASK));
     const bool raw = mode == 0;
-    const bool uncapped = (a.mode & DPT_FLAG_UNCAPPED) != 0;   // f2: inspect_tokenizer's inf-initialised DP
-    const bool len_only = (a.mode & (DPT_FLAG_UNCAPPED | DPT_FLAG_LEN_ONLY)) != 0;
+    // PLAIN: the mode-constant instantiations serve only calls without edges, the uncapped DP or len_only
+    // (launch_encode sends those to the runtime-mode kernels): their loop versions are compiled out
+    constexpr bool PLAIN = (RAW || MC >= 0) && !SOLO;
+    const bool uncapped = !PLAIN && (a.mode & DPT_FLAG_UNCAPPED) != 0;   // f2: inspect_tokenizer's inf-initialised DP
+    const bool len_only = !PLAIN && (a.mode & (DPT_FLAG_UNCAPPED | DPT_FLAG_LEN_ONLY)) != 0;
     // Strings are handed out by npart device counters (each in its own 256-byte line).  Partition p
     // holds the FIN_BATCH-string chunks p, p + npart, p + 2 npart, ... of the batch, in that order
     // (part_size / part_string): the partitions advance through the batch side by side, so strings
@@ -1660,7 +1663,7 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
                     const unsigned na_ = nstart[0];
                     nstart[0] = 0;   // (the generic walker gets nothing)
                     GL &L = grp(0);
-                    const bool wsc = a.edges == nullptr;
+                    const bool wsc = PLAIN || a.edges == nullptr;
                     const int32_t rb = tv.root_base;
                     const unsigned nsl = tv.n_slots;
                     for (unsigned jj = lane; jj < na_; jj += 64u) L.scf[jj] = 0;
@@ -2415,7 +2418,7 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
             unsigned capb = 0;
 #pragma unroll
             for (int g = 0; g < NG; g++) capb |= uni(SSr(g).capb);
-            if (a.edges) {
+            if (!PLAIN && a.edges) {
                 if (!capb) forward(T_{}, C2_{}); else if (uncapped) forward(T_{}, C1_{}); else forward(T_{}, C0_{});
             } else {
                 if (!capb) {
@@ -3505,6 +3508,9 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
     // PRESPLIT (llama mode) and ATOMS run instantiations with the mode a compile-time constant (MC)
     static const bool generic_ps = getenv("DPT_GENERIC_PS") != nullptr;   // (A/B: the runtime-mode kernels)
     const bool presplit = (p.mode & DPT_MODE_MASK) == DPT_MODE_PRESPLIT;
+    // ... and, like the RAW ones, only for calls without edges, the uncapped DP or len_only (PLAIN)
+    const bool plain = p.edges == nullptr && (p.mode & (DPT_FLAG_UNCAPPED | DPT_FLAG_LEN_ONLY)) == 0;
+    const bool spec = plain && !generic_ps;
     if (p.n_str > 0) {
         {
             const unsigned n_cu = p.max_blocks / 64;
@@ -3519,17 +3525,17 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
                     if (raw) launch_tok<SMALL_CH, 16, false, false, 2, true, true>(a, tv, 1, n_cu, stream, e0);
                     else launch_tok<SMALL_CH, 16, false, false, 2, false, true>(a, tv, 1, n_cu, stream, e0);
                 } else if (wide) {
-                    if (generic_ps) {
+                    if (!spec) {
                         if (st16) launch_tok<SMALL_CH, 16, false, true, 1>(a, tv, nu, n_cu, stream, e0);
                         else launch_tok<SMALL_CH, 16, false, true, 2>(a, tv, nu, n_cu, stream, e0);
                     } else {
                         if (st16) launch_tok<SMALL_CH, 16, false, true, 1, false, false, DPT_MODE_ATOMS>(a, tv, nu, n_cu, stream, e0);
                         else launch_tok<SMALL_CH, 16, false, true, 2, false, false, DPT_MODE_ATOMS>(a, tv, nu, n_cu, stream, e0);
                     }
-                } else if (raw && !generic_raw) {
+                } else if (raw && plain && !generic_raw) {
                     if (st16) launch_tok<SMALL_CH, 16, false, false, 1, true>(a, tv, nu, n_cu, stream, e0);
                     else launch_tok<SMALL_CH, 16, false, false, 2, true>(a, tv, nu, n_cu, stream, e0);
-                } else if (presplit && !generic_ps) {
+                } else if (presplit && spec) {
                     if (st16) launch_tok<SMALL_CH, 16, false, false, 1, false, false, DPT_MODE_PRESPLIT>(a, tv, nu, n_cu, stream, e0);
                     else launch_tok<SMALL_CH, 16, false, false, 2, false, false, DPT_MODE_PRESPLIT>(a, tv, nu, n_cu, stream, e0);
                 } else {
@@ -3540,9 +3546,9 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
 #if DPT_STOP == 3   // (this diagnostic build crashes ROCm 7.2's register allocator on the 64-lane first pass)
                 return hipErrorNotSupported;
 #else
-                if (wide && !generic_ps) launch_tok<SMALL_CH, 64, false, true, 0, false, false, DPT_MODE_ATOMS>(a, tv, p.n_str, n_cu, stream, e0);
+                if (wide && spec) launch_tok<SMALL_CH, 64, false, true, 0, false, false, DPT_MODE_ATOMS>(a, tv, p.n_str, n_cu, stream, e0);
                 else if (wide) launch_tok<SMALL_CH, 64, false, true>(a, tv, p.n_str, n_cu, stream, e0);
-                else if (raw) launch_tok<SMALL_CH, 64, false, false, 0, true>(a, tv, p.n_str, n_cu, stream, e0);
+                else if (raw && plain) launch_tok<SMALL_CH, 64, false, false, 0, true>(a, tv, p.n_str, n_cu, stream, e0);
                 else launch_tok<SMALL_CH, 64, false, false>(a, tv, p.n_str, n_cu, stream, e0);
 #endif
             }
@@ -3573,8 +3579,8 @@ hipError_t launch_encode(const EncodeLaunch &p, hipStream_t stream, hipEvent_t e
             uint64_t mb = (uint64_t)(p.max_blocks / 64) * mid_per_cu[dev];
             mb = mb < p.n_str ? mb : p.n_str;
             constexpr int mlds = block_lds_bytes<MID_CH, 16>();
-            // (wide <=> ATOMS mode; the mode-constant instantiations unless DPT_GENERIC_PS)
-            auto mk = generic_ps ? (st16 ? (wide ? mid_kernel<1, true> : mid_kernel<1, false>) : (wide ? mid_kernel<2, true> : mid_kernel<2, false>))
+            // (wide <=> ATOMS mode; the mode-constant instantiations for PLAIN calls unless DPT_GENERIC_PS)
+            auto mk = !spec ? (st16 ? (wide ? mid_kernel<1, true> : mid_kernel<1, false>) : (wide ? mid_kernel<2, true> : mid_kernel<2, false>))
                     : st16 ? (wide ? mid_kernel<1, true, DPT_MODE_ATOMS> : presplit ? mid_kernel<1, false, DPT_MODE_PRESPLIT> : mid_kernel<1, false>)
                            : (wide ? mid_kernel<2, true, DPT_MODE_ATOMS> : presplit ? mid_kernel<2, false, DPT_MODE_PRESPLIT> : mid_kernel<2, false>);
             hipLaunchKernelGGL(mk, dim3((unsigned)(mb ? mb : 1)), dim3(64), mlds, stream, KernArgs{m, tv});
