@@ -39,6 +39,10 @@ timeout -k 10 300 python tools/percall.py 3000 > $out/percall.json 2>/dev/null |
 bash tools/pmc.sh ${tag}_cfg4p 200000 s2orcp > $out/pmc_cfg4p.log 2>&1 || { tail -20 $out/pmc_cfg4p.log; exit 1; }
 cp gpurun_out/pmc_${tag}_cfg4p/summary.txt $out/pmc_cfg4p_summary.txt 2>/dev/null
 find gpurun_out/pmc_${tag}_cfg4p/trace -name "*kernel_stats.csv" | head -1 | xargs -I{} cp {} $out/cfg4p_kernel_stats.csv
+# BLOOM scale (the 64-lane ATOMS kernel): kernel trace + PMC summary
+bash tools/pmc.sh ${tag}_bloom 500000 bloom > $out/pmc_bloom.log 2>&1 || { tail -20 $out/pmc_bloom.log; exit 1; }
+cp gpurun_out/pmc_${tag}_bloom/summary.txt $out/pmc_bloom_summary.txt 2>/dev/null
+find gpurun_out/pmc_${tag}_bloom/trace -name "*kernel_stats.csv" | head -1 | xargs -I{} cp {} $out/bloom_kernel_stats.csv
 for f in $(ls $out/bench.json $out/bench_*.json $out/strong_*.json 2>/dev/null); do
   python3 -c "import json; d=json.loads(open('$f').read()); print('$f', '%.2f GB/s' % (d['value']/1e9), 'ms/step %.4f' % d['ms_per_step'], 'exact', d['exact_match']['rate'], d['exact_match']['sample'], 'tok ms %.4f' % d['stage_ms_per_step']['tokenize'], 'frac %.4f' % d['roofline']['frac'], 'traffic', d['roofline'].get('traffic'))"
 done

@@ -11,4 +11,6 @@ for f in $src/bench_*.json $src/strong_*.json $src/host_path_*.json; do cp $f ${
 cp $src/percall.json ${p}_percall.json
 [ -f $src/cfg4p_kernel_stats.csv ] && cp $src/cfg4p_kernel_stats.csv ${p}_cfg4p_kernel_stats.csv
 [ -f $src/pmc_cfg4p_summary.txt ] && cp $src/pmc_cfg4p_summary.txt ${p}_cfg4p_pmc_summary.txt
+[ -f $src/bloom_kernel_stats.csv ] && cp $src/bloom_kernel_stats.csv ${p}_bloom_kernel_stats.csv
+[ -f $src/pmc_bloom_summary.txt ] && cp $src/pmc_bloom_summary.txt ${p}_bloom_pmc_summary.txt
 ls ${p}_* | wc -l
