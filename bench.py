@@ -622,9 +622,11 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic_for(M, Lb) if (args.workload == "cfg2" and world == 1) else None,
-                         "kernel": ("tokenize_kernel<256,64,false,true,0,false>" if bloom else
-                                    "tokenize_kernel<256,16,false,false,%d,%s>" % (1 if id_bytes == 2 else 2,
-                                                                                 "false" if presplit else "true")),
+                         # (template arguments: CH, G, BIG, WIDE, staged id width, RAW, SOLO, mode constant)
+                         "kernel": ("tokenize_kernel<256,64,false,true,0,false,false,2>" if bloom else
+                                    "tokenize_kernel<256,16,false,false,%d,%s,false,%d>" % (1 if id_bytes == 2 else 2,
+                                                                                          "false" if presplit else "true",
+                                                                                          1 if presplit else -1)),
                          "alg_bytes_per_launch": alg_bytes,
                          "alg_bytes_formula": "N_in + 4*N_tok + 8(N+1) + 8(N+1) + 4N (SURVEY.md 8d)",
                          "alg_bytes_staged_width": alg_staged, "staged_id_bytes": id_bytes,

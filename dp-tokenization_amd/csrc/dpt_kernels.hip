@@ -907,11 +907,17 @@ constexpr unsigned A_REFILL64 = 32;   // the same for the 64-lane kernels (8 / 1
 #ifndef DPT_WPC_GRAN    // LDS allocation granule (bytes) that caps the resident waves per CU (resident_per_cu)
 #define DPT_WPC_GRAN 512
 #endif
+#ifndef DPT_PLAIN_RAW   // A/B knob: the RAW kernels without the edges / uncapped / len_only loop versions too
+#define DPT_PLAIN_RAW 0
+#endif
 #ifndef DPT_WPE16
 #define DPT_WPE16 6
 #endif
 constexpr int WPE16 = DPT_WPE16;
-constexpr int WPE64 = 6;
+#ifndef DPT_WPE64
+#define DPT_WPE64 6
+#endif
+constexpr int WPE64 = DPT_WPE64;
 // The kernel's arguments, as one struct at the start of the kernarg segment
 struct KernArgs {
     EncodeArgs ea;
@@ -999,7 +1005,7 @@ __device__ __forceinline__ void tokenize_body(const unsigned bid) {
     const bool raw = mode == 0;
     // PLAIN: the mode-constant instantiations serve only calls without edges, the uncapped DP or len_only
     // (launch_encode sends those to the runtime-mode kernels): their loop versions are compiled out
-    constexpr bool PLAIN = (RAW || MC >= 0) && !SOLO;
+    constexpr bool PLAIN = ((RAW && DPT_PLAIN_RAW) || MC >= 0) && !SOLO;
     const bool uncapped = !PLAIN && (a.mode & DPT_FLAG_UNCAPPED) != 0;   // f2: inspect_tokenizer's inf-initialised DP
     const bool len_only = !PLAIN && (a.mode & (DPT_FLAG_UNCAPPED | DPT_FLAG_LEN_ONLY)) != 0;
     // Strings are handed out by npart device counters (each in its own 256-byte line).  Partition p
