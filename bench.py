@@ -71,6 +71,9 @@ def parse():
                     help="processes for the synthetic corpus (default: the CPU share, at most 16; 1 under a profiler "
                          "that follows forks)")
     ap.add_argument("--cpu-budget", type=float, default=25.0, help="seconds of CPU-baseline wall time")
+    ap.add_argument("--inflight", type=int, choices=[0, 1, 2], default=0,
+                    help="batches in flight per GPU: step k on context + stream k mod 2 (2) or one stream (1); "
+                         "0 = 2 for shards of <= 524,288 strings, else 1")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--host-path", action="store_true",
                     help="instead of the headline line: the drop-in surface the reference's callers use "
@@ -224,6 +227,21 @@ def rank_strings(n_global: int, rank: int, world: int, scaling: str):
     if scaling == "strong":
         return shard_range(n_global, rank, world)
     return rank * n_global, (rank + 1) * n_global
+
+
+INFLIGHT_MAX_STRINGS = 524288   # auto: two batches in flight for shards up to this many strings
+
+
+def batches_in_flight(arg: int, n_str: int) -> int:
+    """--inflight: 1 or 2 as given; 0 (auto) = 2 for shards of <= INFLIGHT_MAX_STRINGS strings (the strong-
+    scaling shards, whose last slot-round and finish pass the next step's first pass then fills), else 1."""
+    if arg:
+        return arg
+    return 2 if n_str <= INFLIGHT_MAX_STRINGS else 1
+
+
+def n_tok_rank_of(d_idoff) -> int:
+    return int(d_idoff[-1].item())
 
 
 def algorithmic_bytes(n_bytes: int, n_str: int, n_tok: int, id_bytes: int = 4) -> int:
@@ -441,43 +459,54 @@ def main():
     dev = torch.device("cuda", gpu)
     red_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
     vocab = Vocab(t2i, device=gpu)
-    enc = Encoder(vocab)
+    # Batches in flight: with 2, step k runs on context + stream k % 2, so a step's last slot-round (the
+    # persistent grid's tail) and its finish pass overlap the next step's first pass -- two batches in
+    # flight, as a serving loop keeps them; the outputs of both contexts are checked.  The
+    # small shards of strong scaling gain (125k strings: +7 %, 250k: +4 %, tools/overlap_steps.py), 1M does not.
+    inflight = batches_in_flight(args.inflight, M)
+    encs = [Encoder(vocab) for _ in range(inflight)]
+    enc = encs[0]
     n_bytes = int(offs[-1] - offs[0])
     d_text = torch.from_numpy(text).to(dev)
     d_off = torch.from_numpy(offs.view(np.int64)).to(dev)
     d_cut = torch.from_numpy(cut).to(dev) if cut is not None else None
-    d_ids = torch.empty(max(n_bytes, 1), dtype=torch.int32, device=dev)
-    d_idoff = torch.empty(M + 1, dtype=torch.int64, device=dev)
-    d_status = torch.empty(max(M, 1), dtype=torch.int32, device=dev)
+    outs = [(torch.empty(max(n_bytes, 1), dtype=torch.int32, device=dev), torch.empty(M + 1, dtype=torch.int64, device=dev),
+             torch.empty(max(M, 1), dtype=torch.int32, device=dev)) for _ in range(inflight)]
+    d_ids, d_idoff, d_status = outs[0]
     # two histogram buffers: step k's all-reduce (RCCL, on its own stream, async) overlaps step k+1's
     # tokenize, which fills the other buffer; a buffer is reused only after its all-reduce completed
     d_hists = [torch.zeros(N_BINS + 8, dtype=torch.int64, device=dev) for _ in range(2)]
     pending = [None, None]
     n_step = [0]
-    enc.reserve(n_bytes, M)
+    for e in encs:
+        e.reserve(n_bytes, M)
     kmode = "atoms" if bloom else "presplit" if presplit else "raw"
-    stream = torch.cuda.current_stream(dev).cuda_stream
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(inflight - 1)]
+    stream = streams[0].cuda_stream
 
     def step():
         b = n_step[0] % 2
+        i = n_step[0] % inflight
         n_step[0] += 1
         h = d_hists[b]
-        if pending[b] is not None:   # the stream waits for this buffer's previous all-reduce
-            pending[b].wait()
-            pending[b] = None
-        # the histogram is folded into the encode's finish pass, which replaces h's contents
-        # (dpt_ctx_set_histogram_ex, DPT_HIST_OVERWRITE: no memset launch per step)
-        enc.set_histogram(h.data_ptr(), N_BINS, overwrite=True)
-        enc.encode_device(d_text.data_ptr(), n_bytes, d_off.data_ptr(), M, d_ids.data_ptr(), max(n_bytes, 1),
-                          d_idoff.data_ptr(), d_status.data_ptr(), stream=stream,
-                          cut_ptr=d_cut.data_ptr() if d_cut is not None else 0, mode=kmode)
-        if coll:   # the single collective: RCCL over xGMI with nccl, gloo in rehearsals
-            if red_dev.type == "cpu":
-                hc = h.cpu()
-                ddist.allreduce_histogram(hc)
-                h.copy_(hc)
-            else:
-                pending[b] = ddist.allreduce_histogram(h, async_op=True)
+        ids_i, idoff_i, st_i = outs[i]
+        with torch.cuda.stream(streams[i]):   # (the collective below orders itself after this stream's work)
+            if pending[b] is not None:   # the stream waits for this buffer's previous all-reduce
+                pending[b].wait()
+                pending[b] = None
+            # the histogram is folded into the encode's finish pass, which replaces h's contents
+            # (dpt_ctx_set_histogram_ex, DPT_HIST_OVERWRITE: no memset launch per step)
+            encs[i].set_histogram(h.data_ptr(), N_BINS, overwrite=True)
+            encs[i].encode_device(d_text.data_ptr(), n_bytes, d_off.data_ptr(), M, ids_i.data_ptr(), max(n_bytes, 1),
+                                  idoff_i.data_ptr(), st_i.data_ptr(), stream=streams[i].cuda_stream,
+                                  cut_ptr=d_cut.data_ptr() if d_cut is not None else 0, mode=kmode)
+            if coll:   # the single collective: RCCL over xGMI with nccl, gloo in rehearsals
+                if red_dev.type == "cpu":
+                    hc = h.cpu()
+                    ddist.allreduce_histogram(hc)
+                    h.copy_(hc)
+                else:
+                    pending[b] = ddist.allreduce_histogram(h, async_op=True)
 
     def drain():   # every outstanding all-reduce is ordered before what the stream does next
         for b in range(2):
@@ -499,7 +528,8 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    enc.profile(True)
+    for e in encs:
+        e.profile(True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -515,8 +545,14 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    ms_stage, launches = enc.profile_read()
-    enc.profile(False)
+    # (with two batches in flight each context times its own passes, which then share the GPU with the
+    # other context's: the roofline below is a single-stream line's, inflight 1)
+    ms_stage, launches = [0.0, 0.0, 0.0], 0
+    for e in encs:
+        m_e, l_e = e.profile_read()
+        ms_stage = [a + b for a, b in zip(ms_stage, m_e)]
+        launches += l_e
+        e.profile(False)
     # secondary: the encode alone through dpt_encode_padded (ids left at each string's byte offset,
     # per-string counts; no finish pass, no histogram) -- reported beside `value`, never as it
     d_pids = torch.empty(max(n_bytes, 1), dtype=torch.int32, device=dev)
@@ -545,6 +581,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dtp = float(t.item())
     padded_same = bool(torch.equal(d_cnt[:M], (d_idoff[1:] - d_idoff[:-1])[:M]) and torch.equal(d_pst[:M], d_status[:M]))
+    for ids_i, idoff_i, st_i in outs[1:]:   # the other context's last step: the same outputs, or the run is void
+        if not (torch.equal(idoff_i, d_idoff) and torch.equal(st_i[:M], d_status[:M]) and
+                torch.equal(ids_i[: n_tok_rank_of(d_idoff)], d_ids[: n_tok_rank_of(d_idoff)])):
+            raise SystemExit("bench: the two contexts' outputs differ")
 
     # every unbounded-pass string fitted the arena (else it has status 3 and the device path refused it)
     need, cap = enc.long_need()
@@ -618,6 +658,7 @@ def main():
                           "total_ids": n_tok_all, "total_strings": int(hist[N_BINS + 1]),
                           "status": [int(x) for x in hist[N_BINS + 2:N_BINS + 7]]},
             "exact_match": exact,
+            "batches_in_flight": inflight,   # 2: step k on context + stream k % 2 (small shards; see --inflight)
             "stage_ms_per_step": {"tokenize": ms_stage[0] / max(launches, 1)},   # finish (offsets + CSR ids): rocprof
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
@@ -630,7 +671,10 @@ def main():
                          "alg_bytes_per_launch": alg_bytes,
                          "alg_bytes_formula": "N_in + 4*N_tok + 8(N+1) + 8(N+1) + 4N (SURVEY.md 8d)",
                          "alg_bytes_staged_width": alg_staged, "staged_id_bytes": id_bytes,
-                         "frac_staged_width": alg_staged / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
+                         "frac_staged_width": alg_staged / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         **({"note": "two batches in flight: each call's pass times include the other context's "
+                                     "overlapping work, so achieved / frac understate the kernel; the roofline is "
+                                     "the one-stream line's (--inflight 1, the default at 1M)"} if inflight > 1 else {})},
             "cpu_baseline": cpu,
             "padded_layout": {"api": "dpt_encode_padded (ids at each string's byte offset + per-string counts, no CSR pass); encode only, no histogram",
                               "ms_per_step": dtp / args.steps * 1e3, "bytes_per_s": bytes_all * args.steps / dtp,
