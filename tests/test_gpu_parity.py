@@ -208,6 +208,36 @@ def test_device_path_output_at_high_addresses(engines, oracles):
     del big
 
 
+@pytest.mark.parametrize("shift", [0, 1, 3])
+def test_finish_one_slice_vector_copy(engines, oracles, shift):
+    """Calls of >= 2048 batches (one finish block per batch, no slices, no folded prefixes: the batch-scan
+    launch): the ids array `shift` ints past a 16-byte boundary, ragged strings of 0..40 bytes (many rows of the
+    copy's string map cross several strings, empty strings in between), every id against the oracle."""
+    torch = pytest.importorskip("torch")
+    n = 600_000
+    rng = np.random.default_rng(31 + shift)
+    lens = rng.integers(0, 41, n)
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens)
+    text = rng.integers(0x20, 0x7F, int(offs[-1])).astype(np.uint8)
+    enc = engines["llama32k"]
+    dt = torch.from_numpy(text).cuda()
+    do = torch.from_numpy(offs.view(np.int64)).cuda()
+    buf = torch.empty(len(text) + 8, dtype=torch.int32, device="cuda")
+    assert buf.data_ptr() % 16 == 0
+    ids = buf[shift: shift + len(text)]
+    id_off = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    st = torch.empty(n, dtype=torch.int32, device="cuda")
+    enc.encode_device(dt.data_ptr(), len(text), do.data_ptr(), n, ids.data_ptr(), len(text), id_off.data_ptr(),
+                      st.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    rids, roff, rst, _ = oracles["llama32k"].encode_csr(text, offs)
+    off_h = id_off.cpu().numpy().view(np.uint64)
+    assert np.array_equal(off_h, roff)
+    assert np.array_equal(st.cpu().numpy(), rst)
+    assert np.array_equal(ids[: int(off_h[-1])].cpu().numpy(), rids)
+
+
 @pytest.mark.parametrize("n,n_bins", [(50000, 258), (257, 258), (100, 2), (3000, 1500), (1, 16)])
 def test_histogram_folded_into_encode(n, n_bins, engines):
     """dpt_ctx_set_histogram: the finish pass's histogram (one call; n_bins > 1024 takes the separate
