@@ -3142,7 +3142,15 @@ __global__ void __launch_bounds__(FIN_THREADS) finish_kernel(FinishArgs f) {
         s_rel[tid] = incl - c;
         s_src[tid] = src;
     }
-    unsigned gs = 6;   // rows of 64 ids, coarser when the batch has more than FIN_MAP_ROWS of them
+    // rows of 64 ids -- finer when the batch's strings average fewer ids, so that an element's string is at
+    // most a step or two past its row's (short strings: a 64-id row spans tens of them); coarser when the
+    // batch has more than FIN_MAP_ROWS rows
+    unsigned gs = 6;
+    {
+        const uint64_t nb_s = f.n_str - s0 < FIN_BATCH ? f.n_str - s0 : FIN_BATCH;
+        const uint64_t avg = total / nb_s;
+        while (gs > 0 && (1ull << gs) > avg) gs--;
+    }
     while ((total >> gs) >= FIN_MAP_ROWS) gs++;
     if (has && c) {   // the rows starting inside this string's ids [incl - c, incl)
         const uint64_t rb = (incl - c + (1ull << gs) - 1u) >> gs, re = (incl - 1u) >> gs;

@@ -2,7 +2,8 @@
 
     python tools/ab_inproc.py <workload> <n_strings> <rounds> lib1.so lib2.so ...
 
-workload: ascii (cfg2), s2orc (cfg4), arabic (cfg5), bloom; ascii_p / s2orc_p: llama mode (cfg2p / cfg4p).  The corpus is generated and uploaded
+workload: ascii (cfg2), s2orc (cfg4), arabic (cfg5), bloom; ascii_p / s2orc_p: llama mode (cfg2p / cfg4p);
+short: 1..12-byte strings (per-word calls).  The corpus is generated and uploaded
 ONCE; every library gets its own vocab + ctx (ctypes.CDLL: each build's kernels in their own
 namespace, one HIP runtime -- torch's); each round times K encodes of every library back to back
 (HIP events on the stream), so drift of the box hits all of them alike.  Outputs of every library
@@ -34,6 +35,13 @@ def corpus(gen, n):
             _, text, offs, _ = corpus(gen[:-2], n)
             text, offs, cut = synth.llama_words(text, offs)
             return t2i, text, offs, cut
+        if gen == "short":   # per-word-sized strings: 1..12 random printable bytes (a few ids each)
+            rng = np.random.default_rng(3)
+            lens = rng.integers(1, 13, n)
+            offs = np.zeros(n + 1, dtype=np.uint64)
+            offs[1:] = np.cumsum(lens)
+            text = rng.integers(0x20, 0x7F, int(offs[-1])).astype(np.uint8)
+            return t2i, text, offs, None
         if gen == "ascii":
             text, offs = synth.random_ascii_corpus(n, 256, seed=1)
         elif gen == "s2orc":
