@@ -28,7 +28,11 @@ for wl in cfg1 cfg4 cfg5 bloom cfg2p cfg4p; do
 done
 for n in 500000 250000 125000; do
   timeout -k 10 300 python -u bench.py --strings $n --steps 40 --warmup 5 --no-cpu-baseline > $out/strong_$n.log 2>&1 || { tail -20 $out/strong_$n.log; exit 1; }
-  tail -1 $out/strong_$n.log > $out/strong_$n.json
+  grep '^{' $out/strong_$n.log | tail -1 > $out/strong_$n.json
+done
+for n in 250000 125000; do   # the same shards with one batch in flight (bench.py --inflight 1)
+  timeout -k 10 300 python -u bench.py --strings $n --steps 40 --warmup 5 --no-cpu-baseline --inflight 1 > $out/strong1_$n.log 2>&1 || { tail -20 $out/strong1_$n.log; exit 1; }
+  grep '^{' $out/strong1_$n.log | tail -1 > $out/strong_${n}_inflight1.json
 done
 for r in 1 2 3; do   # (three runs in one lease: the drop-in's spread across runs)
   timeout -k 10 400 python -u bench.py --host-path > $out/host_$r.log 2>&1 || { tail -20 $out/host_$r.log; exit 1; }
