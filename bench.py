@@ -73,7 +73,7 @@ def parse():
     ap.add_argument("--cpu-budget", type=float, default=25.0, help="seconds of CPU-baseline wall time")
     ap.add_argument("--inflight", type=int, choices=[0, 1, 2], default=0,
                     help="batches in flight per GPU: step k on context + stream k mod 2 (2) or one stream (1); "
-                         "0 = 2 for shards of <= 524,288 strings, else 1")
+                         "0 = 2 for shards of <= 524,288 strings (not bloom), else 1")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--host-path", action="store_true",
                     help="instead of the headline line: the drop-in surface the reference's callers use "
@@ -232,12 +232,13 @@ def rank_strings(n_global: int, rank: int, world: int, scaling: str):
 INFLIGHT_MAX_STRINGS = 524288   # auto: two batches in flight for shards up to this many strings
 
 
-def batches_in_flight(arg: int, n_str: int) -> int:
+def batches_in_flight(arg: int, n_str: int, rows64: bool = False) -> int:
     """--inflight: 1 or 2 as given; 0 (auto) = 2 for shards of <= INFLIGHT_MAX_STRINGS strings (the strong-
-    scaling shards, whose last slot-round and finish pass the next step's first pass then fills), else 1."""
+    scaling shards, whose last slot-round and finish pass the next step's first pass then fills), else 1; and 1
+    for the 64-lane (BLOOM-scale) kernel, one string per wave, where two in flight measured 1.4 % slower (r06ev6)."""
     if arg:
         return arg
-    return 2 if n_str <= INFLIGHT_MAX_STRINGS else 1
+    return 2 if n_str <= INFLIGHT_MAX_STRINGS and not rows64 else 1
 
 
 def n_tok_rank_of(d_idoff) -> int:
@@ -463,7 +464,7 @@ def main():
     # persistent grid's tail) and its finish pass overlap the next step's first pass -- two batches in
     # flight, as a serving loop keeps them; the outputs of both contexts are checked.  The
     # small shards of strong scaling gain (125k strings: +7 %, 250k: +4 %, tools/overlap_steps.py), 1M does not.
-    inflight = batches_in_flight(args.inflight, M)
+    inflight = batches_in_flight(args.inflight, M, rows64=bloom)
     encs = [Encoder(vocab) for _ in range(inflight)]
     enc = encs[0]
     n_bytes = int(offs[-1] - offs[0])

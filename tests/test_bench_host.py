@@ -72,6 +72,7 @@ def test_batches_in_flight_rule():
     assert bench.batches_in_flight(2, 1_000_000) == 2
     shard = [bench.rank_strings(1_000_000, 0, w, "strong") for w in (1, 2, 4, 8)]
     assert [bench.batches_in_flight(0, b - a) for a, b in shard] == [1, 2, 2, 2]
+    assert bench.batches_in_flight(0, 500_000, rows64=True) == 1   # BLOOM's 64-lane kernel
 
 
 def test_algorithmic_bytes_follow_survey_8d():
