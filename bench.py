@@ -71,9 +71,9 @@ def parse():
                     help="processes for the synthetic corpus (default: the CPU share, at most 16; 1 under a profiler "
                          "that follows forks)")
     ap.add_argument("--cpu-budget", type=float, default=25.0, help="seconds of CPU-baseline wall time")
-    ap.add_argument("--inflight", type=int, choices=[0, 1, 2], default=0,
-                    help="batches in flight per GPU: step k on context + stream k mod 2 (2) or one stream (1); "
-                         "0 = 2 for shards of <= 524,288 strings (not bloom), else 1")
+    ap.add_argument("--inflight", type=int, choices=[0, 1, 2, 3], default=0,
+                    help="batches in flight per GPU: step k on context + stream k mod N (N = 2, 3) or one stream (1); "
+                         "0 = 3 for shards of <= 524,288 strings (not bloom), else 1")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--host-path", action="store_true",
                     help="instead of the headline line: the drop-in surface the reference's callers use "
@@ -233,12 +233,13 @@ INFLIGHT_MAX_STRINGS = 524288   # auto: two batches in flight for shards up to t
 
 
 def batches_in_flight(arg: int, n_str: int, rows64: bool = False) -> int:
-    """--inflight: 1 or 2 as given; 0 (auto) = 2 for shards of <= INFLIGHT_MAX_STRINGS strings (the strong-
-    scaling shards, whose last slot-round and finish pass the next step's first pass then fills), else 1; and 1
-    for the 64-lane (BLOOM-scale) kernel, one string per wave, where two in flight measured 1.4 % slower (r06ev6)."""
+    """--inflight: 1..3 as given; 0 (auto) = 3 for shards of <= INFLIGHT_MAX_STRINGS strings (the strong-
+    scaling shards, whose last slot-round and finish pass the next steps' first passes then fill: 125k strings
+    91.8 -> 93.1 GB/s from two to three, 250k / 500k level, r06ap), else 1; and 1 for the 64-lane (BLOOM-scale)
+    kernel, one string per wave, where two in flight measured 1.4 % slower (r06ev6)."""
     if arg:
         return arg
-    return 2 if n_str <= INFLIGHT_MAX_STRINGS and not rows64 else 1
+    return 3 if n_str <= INFLIGHT_MAX_STRINGS and not rows64 else 1
 
 
 def n_tok_rank_of(d_idoff) -> int:
@@ -476,8 +477,9 @@ def main():
     d_ids, d_idoff, d_status = outs[0]
     # two histogram buffers: step k's all-reduce (RCCL, on its own stream, async) overlaps step k+1's
     # tokenize, which fills the other buffer; a buffer is reused only after its all-reduce completed
-    d_hists = [torch.zeros(N_BINS + 8, dtype=torch.int64, device=dev) for _ in range(2)]
-    pending = [None, None]
+    # (one per batch in flight, at least two: step k's buffer is k mod len, written on step k's stream only)
+    d_hists = [torch.zeros(N_BINS + 8, dtype=torch.int64, device=dev) for _ in range(max(2, inflight))]
+    pending = [None] * len(d_hists)
     n_step = [0]
     for e in encs:
         e.reserve(n_bytes, M)
@@ -486,7 +488,7 @@ def main():
     stream = streams[0].cuda_stream
 
     def step(one_stream: bool = False):
-        b = n_step[0] % 2
+        b = n_step[0] % len(d_hists)
         i = 0 if one_stream else n_step[0] % inflight
         n_step[0] += 1
         h = d_hists[b]
@@ -510,7 +512,7 @@ def main():
                     pending[b] = ddist.allreduce_histogram(h, async_op=True)
 
     def drain():   # every outstanding all-reduce is ordered before what the stream does next
-        for b in range(2):
+        for b in range(len(d_hists)):
             if pending[b] is not None:
                 pending[b].wait()
                 pending[b] = None
@@ -596,7 +598,7 @@ def main():
     need, cap = enc.long_need()
     if need > cap:
         raise SystemExit(f"bench: the unbounded pass needed {need} arena bytes of {cap}: reserve more")
-    hist = d_hists[(n_step[0] - 1) % 2].cpu().numpy()   # the last step's reduced histogram
+    hist = d_hists[(n_step[0] - 1) % len(d_hists)].cpu().numpy()   # the last step's reduced histogram
     n_tok_rank = int(d_idoff[-1].item())
     n_tok_all = int(hist[N_BINS])          # after the all-reduce: all ranks' ids
     ok_strings = int(hist[N_BINS + 2])
@@ -664,7 +666,7 @@ def main():
                           "total_ids": n_tok_all, "total_strings": int(hist[N_BINS + 1]),
                           "status": [int(x) for x in hist[N_BINS + 2:N_BINS + 7]]},
             "exact_match": exact,
-            "batches_in_flight": inflight,   # 2: step k on context + stream k % 2 (small shards; see --inflight)
+            "batches_in_flight": inflight,   # N > 1: step k on context + stream k % N (small shards; see --inflight)
             "stage_ms_per_step": {"tokenize": ms_stage[0] / max(launches, 1)},   # finish (offsets + CSR ids): rocprof
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,

@@ -63,15 +63,15 @@ def test_strong_shards_tile_the_corpus():
 
 
 def test_batches_in_flight_rule():
-    """--inflight: as given, else two batches in flight for the strong-scaling shards (<= 524,288 strings per
+    """--inflight: as given, else three batches in flight for the strong-scaling shards (<= 524,288 strings per
     rank: 125k / 250k / 500k at 8 / 4 / 2 ranks) and one for the 1M single-GPU line."""
-    assert bench.batches_in_flight(0, 125_000) == 2
-    assert bench.batches_in_flight(0, 500_000) == 2
+    assert bench.batches_in_flight(0, 125_000) == 3
+    assert bench.batches_in_flight(0, 500_000) == 3
     assert bench.batches_in_flight(0, 1_000_000) == 1
     assert bench.batches_in_flight(1, 125_000) == 1
     assert bench.batches_in_flight(2, 1_000_000) == 2
     shard = [bench.rank_strings(1_000_000, 0, w, "strong") for w in (1, 2, 4, 8)]
-    assert [bench.batches_in_flight(0, b - a) for a, b in shard] == [1, 2, 2, 2]
+    assert [bench.batches_in_flight(0, b - a) for a, b in shard] == [1, 3, 3, 3]
     assert bench.batches_in_flight(0, 500_000, rows64=True) == 1   # BLOOM's 64-lane kernel
 
 
