@@ -461,10 +461,10 @@ def main():
     dev = torch.device("cuda", gpu)
     red_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
     vocab = Vocab(t2i, device=gpu)
-    # Batches in flight: with 2, step k runs on context + stream k % 2, so a step's last slot-round (the
-    # persistent grid's tail) and its finish pass overlap the next step's first pass -- two batches in
-    # flight, as a serving loop keeps them; the outputs of both contexts are checked.  The
-    # small shards of strong scaling gain (125k strings: +7 %, 250k: +4 %, tools/overlap_steps.py), 1M does not.
+    # Batches in flight: with N > 1, step k runs on context + stream k % N, so a step's last slot-round (the
+    # persistent grid's tail) and its finish pass overlap the next steps' first passes -- batches in flight,
+    # as a serving loop keeps them; the outputs of every context are checked.  The small shards
+    # of strong scaling gain (125k strings: +6 %, 250k: +7 % with three, r06ab / r06ap), 1M does not (r06ai).
     inflight = batches_in_flight(args.inflight, M, rows64=bloom)
     encs = [Encoder(vocab) for _ in range(inflight)]
     enc = encs[0]
@@ -475,9 +475,9 @@ def main():
     outs = [(torch.empty(max(n_bytes, 1), dtype=torch.int32, device=dev), torch.empty(M + 1, dtype=torch.int64, device=dev),
              torch.empty(max(M, 1), dtype=torch.int32, device=dev)) for _ in range(inflight)]
     d_ids, d_idoff, d_status = outs[0]
-    # two histogram buffers: step k's all-reduce (RCCL, on its own stream, async) overlaps step k+1's
-    # tokenize, which fills the other buffer; a buffer is reused only after its all-reduce completed
-    # (one per batch in flight, at least two: step k's buffer is k mod len, written on step k's stream only)
+    # histogram buffers, one per batch in flight and at least two: step k's all-reduce (RCCL, on its own
+    # stream, async) overlaps step k+1's tokenize, which fills another buffer; buffer k mod len is written on
+    # step k's stream only and reused only after its all-reduce completed
     d_hists = [torch.zeros(N_BINS + 8, dtype=torch.int64, device=dev) for _ in range(max(2, inflight))]
     pending = [None] * len(d_hists)
     n_step = [0]
@@ -589,7 +589,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dtp = float(t.item())
     padded_same = bool(torch.equal(d_cnt[:M], (d_idoff[1:] - d_idoff[:-1])[:M]) and torch.equal(d_pst[:M], d_status[:M]))
-    for ids_i, idoff_i, st_i in outs[1:]:   # the other context's last step: the same outputs, or the run is void
+    for ids_i, idoff_i, st_i in outs[1:]:   # the other contexts' last steps: the same outputs, or the run is void
         if not (torch.equal(idoff_i, d_idoff) and torch.equal(st_i[:M], d_status[:M]) and
                 torch.equal(ids_i[: n_tok_rank_of(d_idoff)], d_ids[: n_tok_rank_of(d_idoff)])):
             raise SystemExit("bench: the two contexts' outputs differ")
