@@ -311,6 +311,10 @@ int kernel_variant(uint32_t max_cp) {
 
 }  // namespace
 
+namespace dpt {
+void set_last_error(const std::string &msg) { g_err = msg; }   // (dpt_rccl.cpp)
+}
+
 extern "C" {
 
 const char *dpt_last_error(void) { return g_err.c_str(); }

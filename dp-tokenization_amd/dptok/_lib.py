@@ -13,6 +13,8 @@ LIB_PATH = os.environ.get("DPT_LIB") or os.path.join(HERE, "libdpt.so")
 
 DPT_OK = 0
 DPT_E_CAP = -4
+DPT_E_RCCL = -6
+DPT_RCCL_ID_BYTES = 128
 DPT_MODE_RAW = 0
 DPT_MODE_PRESPLIT = 1
 DPT_MODE_ATOMS = 2
@@ -75,9 +77,14 @@ def lib():
     L.dpt_ctx_profile.argtypes = [P, I32]
     L.dpt_ctx_profile_read.argtypes = [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(U64)]
     L.dpt_ctx_debug_counter_bias.argtypes = [P, U64]
+    L.dpt_rccl_get_unique_id.argtypes = [P]
+    L.dpt_rccl_comm_create.argtypes = [P, I32, I32, I32, ctypes.POINTER(P)]
+    L.dpt_rccl_comm_destroy.argtypes = [P]
+    L.dpt_hist_allreduce.argtypes = [P, ctypes.c_size_t, P, P]
     for name in ("dpt_vocab_create", "dpt_vocab_destroy", "dpt_vocab_stats_get", "dpt_ctx_create", "dpt_ctx_destroy",
                  "dpt_ctx_reserve", "dpt_ctx_reserve_vocab", "dpt_ctx_workspace_bytes", "dpt_ctx_long_need", "dpt_encode", "dpt_encode_padded", "dpt_encode_host", "dpt_dp_host", "dpt_dp_host_far", "dpt_token_histogram",
-                 "dpt_ctx_set_histogram", "dpt_ctx_set_histogram_ex", "dpt_ctx_profile", "dpt_ctx_profile_read", "dpt_ctx_debug_counter_bias"):
+                 "dpt_ctx_set_histogram", "dpt_ctx_set_histogram_ex", "dpt_ctx_profile", "dpt_ctx_profile_read", "dpt_ctx_debug_counter_bias",
+                 "dpt_rccl_get_unique_id", "dpt_rccl_comm_create", "dpt_rccl_comm_destroy", "dpt_hist_allreduce"):
         getattr(L, name).restype = I32
     _lib = L
     return L
@@ -94,4 +101,5 @@ EXPORTED = ["dpt_last_error", "dpt_abi_version", "dpt_vocab_create", "dpt_vocab_
             "dpt_ctx_long_need",
             "dpt_encode", "dpt_encode_padded", "dpt_encode_host",
             "dpt_dp_host", "dpt_dp_host_far", "dpt_token_histogram", "dpt_ctx_set_histogram", "dpt_ctx_set_histogram_ex",
-            "dpt_ctx_profile", "dpt_ctx_profile_read", "dpt_ctx_debug_counter_bias"]
+            "dpt_ctx_profile", "dpt_ctx_profile_read", "dpt_ctx_debug_counter_bias",
+            "dpt_rccl_get_unique_id", "dpt_rccl_comm_create", "dpt_rccl_comm_destroy", "dpt_hist_allreduce"]

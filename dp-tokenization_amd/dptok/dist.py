@@ -61,3 +61,68 @@ def init_from_env(backend: str = "nccl", device=None):
     else:
         dist.init_process_group(backend)
     return rank, world, local
+
+
+class RcclComm:
+    """Direct RCCL through the C-ABI (ABI 6: dpt_rccl_get_unique_id / dpt_rccl_comm_create /
+    dpt_hist_allreduce), SURVEY.md §8(e)'s "direct RCCL with a file-store unique id": rank 0 writes the
+    communicator id to ``id_path`` (atomically: a temporary file renamed into place), the other ranks
+    wait for it.  For a caller that binds only libdpt.so; bench.py uses torch.distributed instead."""
+
+    def __init__(self, rank: int, world: int, device: int, id_path: str, timeout_s: float = 120.0):
+        import ctypes
+        from . import _lib
+        self._L = _lib.lib()
+        self.rank, self.world, self.device = rank, world, device
+        idb = (ctypes.c_uint8 * _lib.DPT_RCCL_ID_BYTES)()
+        if rank == 0:
+            _lib.check(self._L.dpt_rccl_get_unique_id(idb), "dpt_rccl_get_unique_id")
+            publish_id(id_path, bytes(idb))
+        else:
+            ctypes.memmove(idb, wait_for_id(id_path, _lib.DPT_RCCL_ID_BYTES, timeout_s), _lib.DPT_RCCL_ID_BYTES)
+        self._comm = ctypes.c_void_p()
+        _lib.check(self._L.dpt_rccl_comm_create(idb, world, rank, device, ctypes.byref(self._comm)),
+                   "dpt_rccl_comm_create")
+
+    def allreduce_histogram(self, hist, stream=None):
+        """Sum the int64 device tensor ``hist`` over the ranks in place, ordered on ``stream`` (a
+        torch.cuda.Stream; default: the current one).  Returns ``hist``."""
+        import torch
+        from . import _lib
+        if hist.dtype != torch.int64 or not hist.is_cuda or not hist.is_contiguous():
+            raise ValueError("hist must be a contiguous int64 device tensor")
+        s = stream if stream is not None else torch.cuda.current_stream(hist.device)
+        _lib.check(self._L.dpt_hist_allreduce(hist.data_ptr(), hist.numel(), self._comm, s.cuda_stream),
+                   "dpt_hist_allreduce")
+        return hist
+
+    def close(self):
+        from . import _lib
+        if self._comm:
+            _lib.check(self._L.dpt_rccl_comm_destroy(self._comm), "dpt_rccl_comm_destroy")
+            self._comm = None
+
+
+def publish_id(path: str, blob: bytes) -> None:
+    """Write the communicator id where the other ranks look (temporary file + rename: never half-read)."""
+    tmp = f"{path}.tmp{os.getpid()}"
+    with open(tmp, "wb") as f:
+        f.write(blob)
+    os.replace(tmp, path)
+
+
+def wait_for_id(path: str, n: int, timeout_s: float) -> bytes:
+    """Poll for rank 0's id file; TimeoutError after ``timeout_s``."""
+    import time
+    t_end = time.monotonic() + timeout_s
+    while True:
+        try:
+            with open(path, "rb") as f:
+                blob = f.read()
+            if len(blob) == n:
+                return blob
+        except FileNotFoundError:
+            pass
+        if time.monotonic() > t_end:
+            raise TimeoutError(f"no communicator id at {path} after {timeout_s} s")
+        time.sleep(0.01)

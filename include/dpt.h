@@ -18,6 +18,8 @@
  *                        (packages/tokenizer_utils.py:7-31, DPT_MODE_PRESPLIT)
  *   dpt_token_histogram <- the length comparison of the S2ORC probe,
  *                        reference main_analyze_s2orc.py:269-297 (len(dp_tokenize(x)))
+ *   dpt_hist_allreduce <- SURVEY.md §8(b)/(e): the one collective of a sharded corpus (the
+ *                        reference is single-process, llama_s2orc.sh:10; no call site there)
  *
  * Conventions: plain pointers and sizes, no C++ exceptions cross this boundary,
  * every function returns an int (0 = DPT_OK, < 0 = error; message in
@@ -36,7 +38,7 @@
 extern "C" {
 #endif
 
-#define DPT_ABI_VERSION 5
+#define DPT_ABI_VERSION 6
 
 /* return codes */
 #define DPT_OK 0
@@ -45,6 +47,7 @@ extern "C" {
 #define DPT_E_VOCAB (-3)    /* vocabulary not supported (e.g. a token longer than 65535 bytes) */
 #define DPT_E_CAP (-4)      /* output capacity too small */
 #define DPT_E_NODEV (-5)    /* no HIP device */
+#define DPT_E_RCCL (-6)     /* RCCL missing (librccl.so.1 not loadable) or an RCCL call failed (ABI 6) */
 
 /* modes (low 4 bits) */
 #define DPT_MODE_RAW 0      /* pretokenize_raw semantics (tokenizer_utils.py:33-50) */
@@ -225,6 +228,26 @@ int dpt_ctx_profile_read(dpt_ctx *c, double *ms, uint64_t *launches);
  * (two readfirstlane halves; an int low half sign-extends) without a 40-GiB arena
  * (tests/test_gpu_parity.py::test_long_pass_offsets_past_2g).  bias < 2^62; 0 turns it off. */
 int dpt_ctx_debug_counter_bias(dpt_ctx *c, uint64_t bias);
+
+/*
+ * Multi-GPU without torch (ABI 6; SURVEY.md §8(b) dpt_hist_allreduce, §8(e) "direct RCCL with a
+ * file-store unique id").  One process per GPU: rank 0 calls dpt_rccl_get_unique_id and hands the
+ * DPT_RCCL_ID_BYTES bytes to the other ranks by any means (a file, a socket, MPI); every rank then calls
+ * dpt_rccl_comm_create with the same id (collective: it blocks until all `world` ranks have joined).
+ * RCCL is loaded on first use (dlopen of librccl.so.1: the copy the process already holds -- e.g.
+ * PyTorch-ROCm's -- else the one on the library path), so libdpt.so itself does not depend on it;
+ * without it these calls return DPT_E_RCCL.
+ */
+#define DPT_RCCL_ID_BYTES 128
+int dpt_rccl_get_unique_id(uint8_t *id_out);
+int dpt_rccl_comm_create(const uint8_t *id, int world, int rank, int device, void **comm_out);
+int dpt_rccl_comm_destroy(void *rccl_comm);
+/*
+ * Sum hist[0..n) (device pointer, int64; the dpt_token_histogram layout) over every rank of
+ * rccl_comm, in place, stream-ordered on hip_stream (NULL = the default stream): one ncclAllReduce.
+ * rccl_comm is an ncclComm_t -- from dpt_rccl_comm_create or the caller's own RCCL setup.
+ */
+int dpt_hist_allreduce(int64_t *hist, size_t n, void *rccl_comm, void *hip_stream);
 
 #ifdef __cplusplus
 }

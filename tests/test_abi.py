@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     for name in _declared():
         assert hasattr(L, name), name
     assert set(_declared()) == set(_lib.EXPORTED)
-    assert L.dpt_abi_version() == 5
+    assert L.dpt_abi_version() == 6
     for gone in ("dpt_ctx_pipeline", "dpt_ctx_join", "dpt_ctx_copy_stats", "dpt_self_copy_available"):   # ABI 4 dropped them
         assert not hasattr(L, gone), gone
 
@@ -80,3 +80,17 @@ def test_host_path_rejects_bad_offsets():
     ok = (ctypes.c_uint64 * 4)(0, 2, 4, 6)
     rc = L.dpt_encode_host(None, None, 0, text, 6, ok, None, 3, ids, 8, id_off, status, None)
     assert rc == -1 and b"null ctx" in L.dpt_last_error()
+
+
+def test_rccl_entry_points_check_arguments():
+    """ABI 6 (SURVEY.md §8(b) dpt_hist_allreduce): argument errors before RCCL or a device is touched."""
+    from dptok import _lib
+    L = _lib.lib()
+    comm = ctypes.c_void_p()
+    idb = (ctypes.c_uint8 * _lib.DPT_RCCL_ID_BYTES)()
+    assert L.dpt_rccl_get_unique_id(None) == -1
+    assert L.dpt_hist_allreduce(None, 4, None, None) == -1 and b"null" in L.dpt_last_error()
+    for world, rank, dev in ((0, 0, 0), (2, 2, 0), (2, -1, 0), (1, 0, -1)):
+        assert L.dpt_rccl_comm_create(idb, world, rank, dev, ctypes.byref(comm)) == -1
+    assert L.dpt_rccl_comm_create(None, 1, 0, 0, ctypes.byref(comm)) == -1
+    assert L.dpt_rccl_comm_destroy(None) == 0

@@ -7,6 +7,7 @@ import subprocess
 import sys
 
 import numpy as np
+import pytest
 
 from conftest import PKG, ROOT
 
@@ -85,3 +86,19 @@ def test_histogram_allreduce_world2(tmp_path):
     got = np.array(json.loads(line[5:]), dtype=np.int64)
     assert np.array_equal(got, _single_process_hist())
     assert "ASYNC 1" in out.stdout
+
+
+def test_rccl_id_file_exchange(tmp_path):
+    """dptok.dist.RcclComm's id hand-over (SURVEY.md §8e "file-store unique id"): rank 0 publishes the
+    DPT_RCCL_ID_BYTES id with a rename, a waiting rank in another process reads exactly those bytes."""
+    from dptok.dist import publish_id, wait_for_id
+    path = str(tmp_path / "rccl.id")
+    blob = bytes(range(128))
+    code = ("import sys; sys.path[:0] = [%r]; from dptok.dist import wait_for_id; "
+            "sys.stdout.buffer.write(wait_for_id(%r, 128, 60.0))") % (PKG, path)
+    child = subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE)
+    publish_id(path, blob)
+    out, _ = child.communicate(timeout=60)
+    assert child.returncode == 0 and out == blob
+    with pytest.raises(TimeoutError):
+        wait_for_id(str(tmp_path / "absent.id"), 128, 0.05)

@@ -79,3 +79,46 @@ def test_bench_gpus_flag_launches_the_ranks(one_rccl_rank):
     _check(two, 2)
     assert two["config"]["strings_per_gpu"] == N // 2
     assert two["histogram"] == one_rccl_rank["histogram"]
+
+
+_RCCL_DIRECT = r"""
+import os, sys, json
+import numpy as np, torch
+from dptok import dist as ddist, synth, Vocab, Encoder, pack_strings
+rank, world, id_path = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3]
+torch.cuda.set_device(0)
+texts = synth.unpack(*synth.random_ascii_corpus(4000, 256, seed=41))
+text, offs = pack_strings(texts)
+m = len(offs) - 1
+enc = Encoder(Vocab(synth.llama_shaped_vocab(32000, seed=0), 0))
+dt = torch.from_numpy(np.array(text)).cuda(); do = torch.from_numpy(offs.view(np.int64)).cuda()
+ids = torch.empty(len(text), dtype=torch.int32, device="cuda")
+id_off = torch.empty(m + 1, dtype=torch.int64, device="cuda"); st = torch.empty(m, dtype=torch.int32, device="cuda")
+hist = torch.zeros(258 + 8, dtype=torch.int64, device="cuda")
+s = torch.cuda.current_stream().cuda_stream
+enc.set_histogram(hist.data_ptr(), 258)
+enc.encode_device(dt.data_ptr(), int(offs[-1]), do.data_ptr(), m, ids.data_ptr(), len(text), id_off.data_ptr(),
+                  st.data_ptr(), stream=s)
+before = hist.clone()
+comm = ddist.RcclComm(rank, world, 0, id_path)
+comm.allreduce_histogram(hist)
+torch.cuda.synchronize()
+comm.close()
+print(json.dumps({"before": before.cpu().tolist(), "after": hist.cpu().tolist(), "m": m}))
+"""
+
+
+def test_direct_rccl_hist_allreduce_world1(tmp_path):
+    """ABI 6: dpt_rccl_get_unique_id -> the id through a file (dptok.dist.RcclComm) ->
+    dpt_rccl_comm_create -> dpt_hist_allreduce on the encode stream, in a fresh child process at world
+    size 1 (one GPU on the box; RCCL refuses two ranks on one device).  The sum over one rank is the
+    rank's own histogram; it counts every string."""
+    script = tmp_path / "rccl_direct.py"
+    script.write_text(_RCCL_DIRECT)
+    env = _env(PYTHONPATH=os.pathsep.join([os.path.join(ROOT, "dp-tokenization_amd"), ROOT]))
+    out = subprocess.run([sys.executable, str(script), "0", "1", str(tmp_path / "rccl.id")], cwd=ROOT, env=env,
+                         capture_output=True, text=True, timeout=180)
+    assert out.returncode == 0, (out.returncode, out.stderr[-4000:])
+    r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    assert r["before"] == r["after"]
+    assert r["after"][258 + 1] == r["m"] == 4000
