@@ -8,14 +8,16 @@
   :44-60, a ``pass`` stub whose docstring and the README TODO, README.md:3, specify it):
   the same minimum over a list of atoms.
 * ``compute_shortest_tokenizations(base_representation_s, vocabulary, ...)`` (reference
-  :88-146): returns ``(tokenizations, length)``; ``length`` is the uncapped minimum (inf when
-  impossible), bit-exact with the reference.  The reference's list comes from a single-stack
-  backtrace that mixes branches (440/3000 random cases differ from the
-  packaged DP, e.g. ``babaaa`` -> ``['ba','baaa']`` with ``baaa`` not in V); this drop-in
-  returns the well-formed shortest tokenizations of the packaged DP when its capped length
-  equals the minimum, else ``[]``.  Callers use only the length (dialect_arabic.py:79-81).
-  An empty input raises ``IndexError`` like the reference (``segment_index_dp[-1]`` of ``[]``,
-  :132); lengths and exceptions are pinned by ``tests/golden/inspect_cst_cases.json.gz``.
+  :88-146): returns ``(tokenizations, length)``, both the reference's.  ``length`` is the uncapped
+  minimum (inf when impossible).  The list is what the reference's single-stack backtrace (:131-146)
+  produces -- including its mixed branches (e.g. ``babaaa`` -> ``['ba','baaa']`` with
+  ``baaa`` not in V): the GPU runs the uncapped DP with edges (DPT_FLAG_UNCAPPED, DPT_MODE_ATOMS) and
+  returns each end's optimal predecessors -- ``segment_index_dp[i-1]`` of :109-129, ascending -- and the
+  host replays the backtrace over them (round 6; rounds 1-5 returned the packaged DP's well-formed list).
+  Only reachable ends are ever visited by that backtrace, so the GPU's reachable-only masks are the whole
+  of what it reads; an unreachable string end yields ``[]`` as in the reference.  An empty input raises
+  ``IndexError`` like the reference (``segment_index_dp[-1]`` of ``[]``, :132); lengths, lists and
+  exceptions are pinned by ``tests/golden/inspect_cst_cases.json.gz``.
 * ``obtain_token_compositions(token_str, vocab, merges)`` (reference :17-42): merge-tree
   decompositions, host-side recursion over the merge list (no DP).
 """
@@ -29,7 +31,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 if _HERE not in sys.path:
     sys.path.insert(0, _HERE)
 
-from packages.dp_tokenize import _dp_length, compute_shortest_tokenizations as _packaged_cst  # noqa: E402
+from dptok import DptError  # noqa: E402
+from dptok.engine import atoms_to_csr  # noqa: E402
+from packages.dp_tokenize import _dp_length, _engine_for  # noqa: E402
 
 _INF_WORD = 0xFFFF
 
@@ -78,8 +82,60 @@ def compute_shortest_tokenizations(base_representation_s, vocabulary, disregard_
     atoms = list(base_representation_s)
     if not atoms:   # the reference indexes segment_index_dp[-1] of an empty list (:112, :132)
         raise IndexError("list index out of range")
-    length = _uncapped_min(atoms, vocabulary)
-    if length == float("inf"):
-        return [], length
-    toks, capped = _packaged_cst(atoms, vocabulary, False, None)
-    return (toks if capped == length else []), length
+    if not any(isinstance(t, str) and t for t in vocabulary):
+        return [], float("inf")
+    status, lengths, edges, far = _dp_uncapped_edges(atoms, vocabulary)
+    if status not in (0, 1):
+        raise DptError("engine status %d" % status)
+    length = int(lengths[0])
+    if status == 1 or length >= _INF_WORD:
+        return [], float("inf")
+    far_by_end: Dict[int, List[int]] = {}
+    for e, d in far.tolist():
+        far_by_end.setdefault(int(e), []).append(int(d))
+
+    def preds(end: int) -> List[int]:   # segment_index_dp[end - 1] of a reachable end, ascending
+        m = int(edges[end - 1])
+        out = [end - 1 - d for d in far_by_end.get(end - 1, ())]
+        while m:
+            low = m & -m
+            out.append(end - 1 - (low.bit_length() - 1))
+            m ^= low
+        out.sort()
+        return out
+
+    return _single_stack_backtrace(atoms, preds), length
+
+
+def _dp_uncapped_edges(atoms, vocabulary):
+    """GPU DP over one atom list, inf-initialised (:109-129): (status, minimum, per-end optimal-predecessor
+    masks of reachable ends, far pairs for predecessors more than 64 atoms back)."""
+    enc = _engine_for(vocabulary)
+    text, offs, cut = atoms_to_csr([atoms])
+    status, lengths, edges, far = enc.dp(text, offs, mode="atoms", cut_mask=cut, uncapped=True, edges=True,
+                                         far=True)
+    return int(status[0]), lengths, edges, far
+
+
+def _single_stack_backtrace(atoms: List[str], preds) -> List[List[str]]:
+    """The reference's backtrace (:131-146) as it behaves: ONE stack of start indices for all branches.  A
+    popped start b closes the token atoms[b .. end] onto the tokenization being built, where `end` is the
+    atom before the previous pop's start -- or the last atom once a tokenization has just been completed
+    (the reference then restarts from the string end, whatever depth the next stacked start came from) --
+    and pushes the optimal predecessors of b unless b == 0, which completes the tokenization."""
+    n = len(atoms)
+    pending = list(preds(n))
+    last = n           # exclusive end of the next token
+    building: List[str] = []
+    done: List[List[str]] = []
+    while pending:
+        b = pending.pop()
+        building = ["".join(atoms[b:last])] + building
+        if b == 0:
+            done.append(building)
+            building = []
+            last = n
+        else:
+            last = b
+            pending.extend(preds(b))
+    return done

@@ -138,3 +138,44 @@ def min_tokens_for_string(s: Iterable[str], vocabulary) -> float:
             if "".join(s[j:i]) in vocabulary:
                 best[i] = min(best[i], best[j] + 1)
     return best[n]
+
+
+def inspect_shortest_tokenizations(atoms: Sequence[str], vocabulary) -> Tuple[List[List[str]], float]:
+    """``inspect_tokenizer.compute_shortest_tokenizations`` after its marker rule (inspect_tokenizer.py:109-146):
+    the inf-initialised DP whose per-end lists keep every j with len[j] + 1 == len[i] -- for an unreachable
+    end that is inf == inf, so they hold its unreachable in-vocabulary starts (:117-129) -- then the
+    one-stack backtrace: pop a start, prepend atoms[start .. cursor], move the cursor before the start, and
+    on reaching index -1 record the tokenization and put the cursor back at the last atom (:131-146)."""
+    n = len(atoms)
+    if n == 0:
+        raise IndexError("list index out of range")
+    inf = float("inf")
+    length = [inf] * (n + 1)
+    length[0] = 0
+    lists: List[List[int]] = []
+    for i in range(1, n + 1):
+        cur: List[int] = []
+        for j in range(i):
+            if "".join(atoms[j:i]) not in vocabulary:
+                continue
+            if length[j] + 1 < length[i]:
+                length[i] = length[j] + 1
+                cur = [j]
+            elif length[j] + 1 == length[i] and j not in cur:
+                cur.append(j)
+        lists.append(cur)
+    stack = list(lists[n - 1])
+    cursor = n - 1
+    out: List[List[str]] = []
+    part: List[str] = []
+    while stack:
+        s = stack.pop()
+        part.insert(0, "".join(atoms[s:cursor + 1]))
+        cursor = s - 1
+        if cursor < 0:
+            out.append(part)
+            part = []
+            cursor = n - 1
+        else:
+            stack.extend(lists[cursor])
+    return out, length[n]

@@ -268,17 +268,70 @@ def test_inspect_cst_lengths_pinned_by_the_oracle(inspect_cst):
         assert ref_port.min_tokens_for_string(list(c["atoms"]), vocab) == want, c
 
 
+def test_inspect_cst_lists_pinned_by_the_oracle(inspect_cst):
+    """The reference's LISTS (its one-stack backtrace, :131-146, mixed branches included) equal the CPU
+    restatement's (oracle/ref_port.inspect_shortest_tokenizations) on every case: the checker of the GPU
+    test below is pinned."""
+    from oracle import ref_port
+    good = [c for c in inspect_cst if not c["error"]]
+    mixed = 0
+    for c in good:
+        vocab = set(c["vocab"])
+        if c["disregard"]:
+            vocab = {t.lstrip(c["marker"]) for t in vocab}
+        toks, n = ref_port.inspect_shortest_tokenizations(list(c["atoms"]), vocab)
+        assert toks == c["tokenizations"], c
+        mixed += any(t not in vocab for tk in toks for t in tk)
+    assert mixed >= 5   # the fixture exercises the backtrace's mixed branches
+
+
+def test_inspect_cst_backtrace_replay_matches_oracle():
+    """The drop-in's host replay of the backtrace (inspect_tokenizer._single_stack_backtrace), fed the
+    optimal-predecessor lists of reachable ends, equals the restatement on random cases (no GPU: the lists
+    come from a CPU DP here; on the GPU they come from the uncapped DP's edge masks)."""
+    import random
+    import inspect_tokenizer as it
+    from oracle import ref_port
+    rng = random.Random(7)
+    for _ in range(400):
+        alpha = "abc"[: rng.randint(2, 3)]
+        vocab = set(alpha) | {"".join(rng.choice(alpha) for _ in range(rng.randint(2, 4))) for _ in range(rng.randint(0, 9))}
+        atoms = [rng.choice(alpha) for _ in range(rng.randint(1, 11))]
+        want, n = ref_port.inspect_shortest_tokenizations(atoms, vocab)
+        cost, preds = ref_port.forward_dp(atoms, vocab)   # every atom is a token: capped == uncapped here
+        assert cost[-1] == n
+        assert it._single_stack_backtrace(atoms, lambda e: list(preds[e])) == want
+
+
 @pytest.mark.gpu
-def test_inspect_cst_lengths_match_reference(inspect_cst):
-    """The drop-in's length (GPU, uncapped DP) equals the reference's on every case; its list is the
-    packaged DP's well-formed one (documented deviation), so only its shape is checked."""
+def test_inspect_cst_lists_match_reference(inspect_cst):
+    """Round 6: the drop-in's list AND length equal the reference's on every case (GPU uncapped DP with edges
+    + the host replay of the one-stack backtrace)."""
     import inspect_tokenizer as it
     for c in inspect_cst:
         if c["error"]:
             continue
         toks, n = it.compute_shortest_tokenizations(list(c["atoms"]), set(c["vocab"]), c["disregard"], c["marker"])
         want = math.inf if c["length"] == "inf" else c["length"]
-        assert n == want, c
-        assert all(len(t) == n for t in toks), c
-        if want == math.inf:
-            assert toks == [] == c["tokenizations"]
+        assert n == want and toks == c["tokenizations"], c
+
+
+@pytest.mark.gpu
+def test_inspect_cst_random_vs_oracle():
+    """Beyond the fixture: random cases with out-of-vocabulary atoms (unreachable ends, capped != uncapped)
+    and tokens of up to 70 atoms (far predecessors), the drop-in against the restatement."""
+    import random
+    import inspect_tokenizer as it
+    from oracle import ref_port
+    rng = random.Random(17)
+    for k in range(300):
+        alpha = "abcd"[: rng.randint(2, 4)]
+        vocab = {ch for ch in alpha if rng.random() < 0.85}
+        vocab |= {"".join(rng.choice(alpha) for _ in range(rng.randint(2, 5))) for _ in range(rng.randint(0, 14))}
+        atoms = [rng.choice(alpha) for _ in range(rng.randint(1, 14))]
+        if k % 50 == 0:   # a token of 66..70 atoms: its predecessor comes back as a far pair
+            long = [rng.choice(alpha) for _ in range(rng.randint(66, 70))]
+            vocab.add("".join(long))
+            atoms = atoms + long
+        want = ref_port.inspect_shortest_tokenizations(atoms, vocab)
+        assert it.compute_shortest_tokenizations(atoms, set(vocab), False, None) == want, (atoms, sorted(vocab))
