@@ -71,9 +71,9 @@ def parse():
                     help="processes for the synthetic corpus (default: the CPU share, at most 16; 1 under a profiler "
                          "that follows forks)")
     ap.add_argument("--cpu-budget", type=float, default=25.0, help="seconds of CPU-baseline wall time")
-    ap.add_argument("--inflight", type=int, choices=[0, 1, 2, 3], default=0,
-                    help="batches in flight per GPU: step k on context + stream k mod N (N = 2, 3) or one stream (1); "
-                         "0 = 3 for shards of <= 524,288 strings (not bloom), else 1")
+    ap.add_argument("--inflight", type=int, choices=range(0, 9), default=0,
+                    help="batches in flight per GPU: step k on context + stream k mod N (N = 2..8) or one stream (1); "
+                         "0 = 4 for shards of >= 65,536 strings and <= 64 MiB, 3 up to 524,288 strings (not bloom), else 1")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--host-path", action="store_true",
                     help="instead of the headline line: the drop-in surface the reference's callers use "
@@ -229,17 +229,25 @@ def rank_strings(n_global: int, rank: int, world: int, scaling: str):
     return rank * n_global, (rank + 1) * n_global
 
 
-INFLIGHT_MAX_STRINGS = 524288   # auto: two batches in flight for shards up to this many strings
+INFLIGHT_MAX_STRINGS = 524288   # auto: batches in flight for shards up to this many strings ...
+INFLIGHT4_MIN_STRINGS = 65536   # ... four of them for shards of at least this many strings
+INFLIGHT4_MAX_BYTES = 1 << 26   # ... and at most 64 MiB of text, else three
 
 
-def batches_in_flight(arg: int, n_str: int, rows64: bool = False) -> int:
-    """--inflight: 1..3 as given; 0 (auto) = 3 for shards of <= INFLIGHT_MAX_STRINGS strings (the strong-
-    scaling shards, whose last slot-round and finish pass the next steps' first passes then fill: 125k strings
-    91.8 -> 93.1 GB/s from two to three, 250k / 500k level, r06ap), else 1; and 1 for the 64-lane (BLOOM-scale)
-    kernel, one string per wave, where two in flight measured 1.4 % slower (r06ev6)."""
+def batches_in_flight(arg: int, n_str: int, rows64: bool = False, n_bytes: int = 0) -> int:
+    """--inflight: 1..8 as given; 0 (auto) = 4 for shards of INFLIGHT4_MIN_STRINGS.. strings and <= 64 MiB of text
+    (8 / 4 ranks of the strong-scaling run: 125k, 250k strings), 3 for others of <= INFLIGHT_MAX_STRINGS strings
+    (2 ranks: 500k; cfg4; cfg1), else 1.  The small shards' last slot-round and finish pass the next steps' first
+    passes then fill: 125k strings 91.8 -> 93.1 GB/s from two to three (r06ap); three -> four with the per-step RCCL
+    all-reduce the N > 1 runs do: 94.9 -> 98.1 at 125k, 104.7 -> 106.7 at 250k (r06ih).  Four measured SLOWER where a
+    batch holds more text (500k x 256 B: 84 against 104; cfg4's 200k x ~1.2 KB: 76 against 83.5) or is tiny (cfg1),
+    and six or eight were slower everywhere (125k: 91; r06ig, r06ii).  1 for the 64-lane (BLOOM-scale) kernel, one
+    string per wave, where two in flight measured 1.4 % slower (r06ev6)."""
     if arg:
         return arg
-    return 3 if n_str <= INFLIGHT_MAX_STRINGS and not rows64 else 1
+    if rows64 or n_str > INFLIGHT_MAX_STRINGS:
+        return 1
+    return 4 if n_str >= INFLIGHT4_MIN_STRINGS and n_bytes <= INFLIGHT4_MAX_BYTES else 3
 
 
 def n_tok_rank_of(d_idoff) -> int:
@@ -464,8 +472,9 @@ def main():
     # Batches in flight: with N > 1, step k runs on context + stream k % N, so a step's last slot-round (the
     # persistent grid's tail) and its finish pass overlap the next steps' first passes -- batches in flight,
     # as a serving loop keeps them; the outputs of every context are checked.  The small shards
-    # of strong scaling gain (125k strings: +6 %, 250k: +7 % with three, r06ab / r06ap), 1M does not (r06ai).
-    inflight = batches_in_flight(args.inflight, M, rows64=bloom)
+    # of strong scaling gain (125k strings: +6 %, 250k: +7 % with three, r06ab / r06ap; four with the all-reduce:
+    # +3.3 / +1.9 % more, r06ih), 1M does not (r06ai); batches_in_flight has the rule.
+    inflight = batches_in_flight(args.inflight, M, rows64=bloom, n_bytes=int(offs[-1] - offs[0]))
     encs = [Encoder(vocab) for _ in range(inflight)]
     enc = encs[0]
     n_bytes = int(offs[-1] - offs[0])
@@ -481,6 +490,7 @@ def main():
     d_hists = [torch.zeros(N_BINS + 8, dtype=torch.int64, device=dev) for _ in range(max(2, inflight))]
     pending = [None] * len(d_hists)
     n_step = [0]
+    ran = [False] * inflight   # contexts that ran a step (a short run may not reach all of them)
     for e in encs:
         e.reserve(n_bytes, M)
     kmode = "atoms" if bloom else "presplit" if presplit else "raw"
@@ -491,6 +501,7 @@ def main():
         b = n_step[0] % len(d_hists)
         i = 0 if one_stream else n_step[0] % inflight
         n_step[0] += 1
+        ran[i] = True
         h = d_hists[b]
         ids_i, idoff_i, st_i = outs[i]
         with torch.cuda.stream(streams[i]):   # (the collective below orders itself after this stream's work)
@@ -548,7 +559,7 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    # With two batches in flight the passes of consecutive steps overlap, so a call's own pass times mean
+    # With batches in flight the passes of consecutive steps overlap, so a call's own pass times mean
     # little and their events cost the timed steps ~1 %: the roofline's pass timing then comes from a
     # separate one-stream run of prof_steps steps after the timed region (the same calls, one context).
     prof_steps = 0
@@ -589,10 +600,11 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dtp = float(t.item())
     padded_same = bool(torch.equal(d_cnt[:M], (d_idoff[1:] - d_idoff[:-1])[:M]) and torch.equal(d_pst[:M], d_status[:M]))
-    for ids_i, idoff_i, st_i in outs[1:]:   # the other contexts' last steps: the same outputs, or the run is void
-        if not (torch.equal(idoff_i, d_idoff) and torch.equal(st_i[:M], d_status[:M]) and
-                torch.equal(ids_i[: n_tok_rank_of(d_idoff)], d_ids[: n_tok_rank_of(d_idoff)])):
-            raise SystemExit("bench: the two contexts' outputs differ")
+    # the other contexts' last steps (those that ran one): the same outputs, or the run is void
+    for (ids_i, idoff_i, st_i), ran_i in list(zip(outs, ran))[1:]:
+        if ran_i and not (torch.equal(idoff_i, d_idoff) and torch.equal(st_i[:M], d_status[:M]) and
+                          torch.equal(ids_i[: n_tok_rank_of(d_idoff)], d_ids[: n_tok_rank_of(d_idoff)])):
+            raise SystemExit("bench: the contexts' outputs differ")
 
     # every unbounded-pass string fitted the arena (else it has status 3 and the device path refused it)
     need, cap = enc.long_need()
@@ -680,9 +692,9 @@ def main():
                          "alg_bytes_formula": "N_in + 4*N_tok + 8(N+1) + 8(N+1) + 4N (SURVEY.md 8d)",
                          "alg_bytes_staged_width": alg_staged, "staged_id_bytes": id_bytes,
                          "frac_staged_width": alg_staged / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                         **({"note": "two batches in flight overlap consecutive steps' passes: the pass timing here "
+                         **({"note": "%d batches in flight overlap consecutive steps' passes: the pass timing here "
                                      "is from a separate one-stream run of %d steps after the timed region (HIP events "
-                                     "on its dispatches), not from the timed steps" % prof_steps} if inflight > 1 else {})},
+                                     "on its dispatches), not from the timed steps" % (inflight, prof_steps)} if inflight > 1 else {})},
             "cpu_baseline": cpu,
             "padded_layout": {"api": "dpt_encode_padded (ids at each string's byte offset + per-string counts, no CSR pass); encode only, no histogram",
                               "ms_per_step": dtp / args.steps * 1e3, "bytes_per_s": bytes_all * args.steps / dtp,

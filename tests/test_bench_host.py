@@ -63,16 +63,18 @@ def test_strong_shards_tile_the_corpus():
 
 
 def test_batches_in_flight_rule():
-    """--inflight: as given, else three batches in flight for the strong-scaling shards (<= 524,288 strings per
-    rank: 125k / 250k / 500k at 8 / 4 / 2 ranks) and one for the 1M single-GPU line."""
-    assert bench.batches_in_flight(0, 125_000) == 3
-    assert bench.batches_in_flight(0, 500_000) == 3
-    assert bench.batches_in_flight(0, 1_000_000) == 1
+    """--inflight: as given, else four batches in flight for the strong-scaling shards of 65,536.. strings and
+    <= 64 MiB of text (125k / 250k x 256 B at 8 / 4 ranks), three for other shards of <= 524,288 strings (500k at 2
+    ranks, cfg4's 200k S2ORC-shaped strings, cfg1) and one for the 1M single-GPU line."""
+    b = lambda n, nb=None, **kw: bench.batches_in_flight(0, n, n_bytes=256 * n if nb is None else nb, **kw)  # noqa: E731
+    assert b(125_000) == 4 and b(250_000) == 4
+    assert b(500_000) == 3 and b(200_000, 245_000_000) == 3 and b(1000, 64_000) == 3
+    assert b(1_000_000) == 1
     assert bench.batches_in_flight(1, 125_000) == 1
     assert bench.batches_in_flight(2, 1_000_000) == 2
     shard = [bench.rank_strings(1_000_000, 0, w, "strong") for w in (1, 2, 4, 8)]
-    assert [bench.batches_in_flight(0, b - a) for a, b in shard] == [1, 3, 3, 3]
-    assert bench.batches_in_flight(0, 500_000, rows64=True) == 1   # BLOOM's 64-lane kernel
+    assert [b(hi - lo) for lo, hi in shard] == [1, 3, 4, 4]
+    assert b(250_000, rows64=True) == 1   # BLOOM's 64-lane kernel
 
 
 def test_algorithmic_bytes_follow_survey_8d():
