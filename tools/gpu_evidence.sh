@@ -30,6 +30,10 @@ for n in 500000 250000 125000; do
   timeout -k 10 300 python -u bench.py --strings $n --steps 40 --warmup 5 --no-cpu-baseline > $out/strong_$n.log 2>&1 || { tail -20 $out/strong_$n.log; exit 1; }
   grep '^{' $out/strong_$n.log | tail -1 > $out/strong_$n.json
 done
+for n in 500000 250000 125000; do   # the same shards with the per-step RCCL all-reduce the N > 1 runs do (world 1)
+  DPT_BENCH_COLL=1 timeout -k 10 300 python -u bench.py --strings $n --steps 40 --warmup 5 --no-cpu-baseline > $out/strongc_$n.log 2>&1 || { tail -20 $out/strongc_$n.log; exit 1; }
+  grep '^{' $out/strongc_$n.log | tail -1 > $out/strong_${n}_rccl.json
+done
 for n in 250000 125000; do   # the same shards with one batch in flight (bench.py --inflight 1)
   timeout -k 10 300 python -u bench.py --strings $n --steps 40 --warmup 5 --no-cpu-baseline --inflight 1 > $out/strong1_$n.log 2>&1 || { tail -20 $out/strong1_$n.log; exit 1; }
   grep '^{' $out/strong1_$n.log | tail -1 > $out/strong_${n}_inflight1.json
