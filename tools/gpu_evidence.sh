@@ -3,12 +3,13 @@
 # bench, so its line reports the traffic of the same source), the default bench line (CPU baseline
 # included), its rocprofv3 kernel trace + stats, the PMC summary; then the other workloads, the
 # strong-scaling points, the host path and the per-call floor.
-# Usage: bash tools/gpu_evidence.sh <tag> [1|2]   (part 1: up to the PMC summary; part 2: the rest)
+# Usage: bash tools/gpu_evidence.sh <tag> [1|2|2a|2b]   (part 1: up to the PMC summary; part 2: the rest = 2a (the other
+# workloads and the strong-scaling points) + 2b (host path, per-call floor, cfg4p / BLOOM traces and PMC summaries))
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 tag=$1; part=${2:-all}; out=gpurun_out/round_$tag; mkdir -p $out
-if [ $part != 2 ]; then
+if [ $part = 1 ] || [ $part = all ]; then
 timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $out/pytest_gpu.log 2>&1 || { tail -40 $out/pytest_gpu.log; exit 1; }
 tail -1 $out/pytest_gpu.log
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 || { tail -20 $out/smoke.log; exit 1; }
@@ -22,6 +23,7 @@ bash tools/pmc.sh $tag > $out/pmc.log 2>&1 || { tail -20 $out/pmc.log; exit 1; }
 cp gpurun_out/pmc_$tag/summary.txt $out/pmc_summary.txt 2>/dev/null
 fi
 [ $part = 1 ] && exit 0
+if [ $part != 2b ]; then
 for wl in cfg1 cfg4 cfg5 bloom cfg2p cfg4p; do
   timeout -k 10 400 python -u bench.py --workload $wl --steps 10 --warmup 3 > $out/bench_$wl.log 2>&1 || { tail -20 $out/bench_$wl.log; exit 1; }
   tail -1 $out/bench_$wl.log > $out/bench_$wl.json
@@ -38,6 +40,8 @@ for n in 250000 125000; do   # the same shards with one batch in flight (bench.p
   timeout -k 10 300 python -u bench.py --strings $n --steps 40 --warmup 5 --no-cpu-baseline --inflight 1 > $out/strong1_$n.log 2>&1 || { tail -20 $out/strong1_$n.log; exit 1; }
   grep '^{' $out/strong1_$n.log | tail -1 > $out/strong_${n}_inflight1.json
 done
+fi
+[ $part = 2a ] && exit 0
 for r in 1 2 3; do   # (three runs in one lease: the drop-in's spread across runs)
   timeout -k 10 400 python -u bench.py --host-path > $out/host_$r.log 2>&1 || { tail -20 $out/host_$r.log; exit 1; }
   tail -1 $out/host_$r.log > $out/host_path_$r.json
